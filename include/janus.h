@@ -1,0 +1,112 @@
+/*
+ * janus.h — C-ABI of libjanus_hip.so, the MI355X-native (gfx950) hot path of Janus.
+ *
+ * Every entry point returns int (0 = OK, non-zero = error; message from
+ * janus_last_error(), per calling thread). No C++ exception crosses this ABI.
+ * Arrays marked [device] are HIP device pointers the caller owns (e.g. torch
+ * tensors); [host] arrays are ordinary memory. `stream` is a hipStream_t (NULL =
+ * the null stream). Kernels are enqueued asynchronously on `stream`; host-side
+ * entry points (packet codec) are synchronous and thread-safe.
+ *
+ * Each declaration names the reference interface it replaces (path:line in
+ * akshatvasisht/janus). Reference bindings a maintainer would add: INTEGRATION.md.
+ */
+#ifndef JANUS_H_
+#define JANUS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+const char* janus_last_error(void);
+/* ABI version: major*10000 + minor*100 + patch. */
+int janus_version(void);
+
+/* ------------------------------------------------------------- prosody --- */
+/*
+ * Batched ProsodyExtractor core: aubio YIN per hop + RMS per utterance.
+ * Replaces aubio.pitch('yin', 4096, hop, sr) with unit Hz / tolerance `tolerance`
+ * (backend/services/prosody.py:32-34) called once per hop (prosody.py:78-87), and
+ * numpy's rms = sqrt(mean(x**2)) (prosody.py:67). One stream per utterance:
+ *   pcm            [device] f32, utterances back to back
+ *   sample_offsets [device] int64[B+1], prefix offsets into pcm
+ *   hop_offsets    [device] int64[B+1], prefix sum of ceil(n_b / hop)
+ *   total_hops     host copy of hop_offsets[B]
+ *   silence_db     aubio pitch silence threshold (aubio default -50 dB)
+ *   state_in       [device] f32[B][4096] detector buffer before the call, or NULL (zeros)
+ *   state_out      [device] f32[B][4096] buffer after the call, or NULL; must not alias state_in
+ *   f0_out         [device] f32[total_hops] per-hop pitch in Hz (0 = unvoiced/silent)
+ *   rms_out, mean_f0_out [device] f32[B]; n_voiced_out [device] int32[B]
+ * rms_out is NaN for an empty utterance (numpy mean of an empty array).
+ */
+int janus_prosody_analyze(const float* pcm, const int64_t* sample_offsets,
+                          const int64_t* hop_offsets, int batch, int64_t total_hops,
+                          int sample_rate, int hop_size, float tolerance, float silence_db,
+                          const float* state_in, float* state_out, float* f0_out,
+                          float* rms_out, float* mean_f0_out, int32_t* n_voiced_out,
+                          void* stream);
+
+/* -------------------------------------------------------- packet codec --- */
+enum {
+  JANUS_VAL_NIL = 0,
+  JANUS_VAL_BOOL = 1,
+  JANUS_VAL_INT = 2,   /* signed 64-bit in .i */
+  JANUS_VAL_UINT = 3,  /* unsigned 64-bit in .i (bit pattern), > INT64_MAX only */
+  JANUS_VAL_FLOAT = 4, /* float64 in .f */
+  JANUS_VAL_STR = 5,   /* UTF-8 bytes: .s/.len (pack) or .offset/.len into the buffer (unpack) */
+  JANUS_VAL_BIN = 6,
+  JANUS_VAL_ARRAY = 7, /* .len children follow (pre-order) */
+  JANUS_VAL_MAP = 8    /* .len key/value pairs follow (pre-order) */
+};
+
+typedef struct {
+  int32_t type;
+  int64_t i;
+  double f;
+  const char* s;
+  size_t len;
+} janus_value;
+
+typedef struct {
+  const char* text; /* UTF-8 */
+  size_t text_len;
+  int64_t mode; /* int(JanusMode) */
+  int32_t n_prosody;
+  const janus_value* prosody_keys; /* JANUS_VAL_STR, in dict insertion order */
+  const janus_value* prosody_vals;
+  const char* override_emotion; /* NULL => key 'o' omitted (override == "Auto") */
+  size_t override_len;
+  janus_value timestamp; /* JANUS_VAL_FLOAT (time.time()) or JANUS_VAL_INT */
+} janus_packet;
+
+/*
+ * Replaces msgpack.packb(JanusPacket.to_dict(), use_bin_type=True)
+ * (backend/common/protocol.py:57-76, :97-107). Keys in insertion order t, m, p, ts[, o].
+ * Writes up to `cap` bytes; *out_len is the full size (error if it exceeds cap).
+ */
+int janus_pack_packet(const janus_packet* pkt, uint8_t* out, size_t cap, size_t* out_len);
+
+typedef struct {
+  int32_t type;  /* JANUS_VAL_* */
+  int64_t i;     /* INT/UINT/BOOL value */
+  double f;      /* FLOAT value */
+  size_t offset; /* STR/BIN: byte offset of the payload in the input buffer */
+  size_t len;    /* STR/BIN: payload bytes; ARRAY: items; MAP: pairs */
+} janus_mp_node;
+
+/*
+ * Replaces msgpack.unpackb(payload, raw=False) (backend/common/protocol.py:109-121).
+ * Decodes one MessagePack object into `nodes` (pre-order); fails on truncated input,
+ * trailing bytes (msgpack ExtraData), the reserved byte 0xc1 and ext types.
+ */
+int janus_unpack(const uint8_t* buf, size_t len, janus_mp_node* nodes, size_t cap,
+                 size_t* n_nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JANUS_H_ */

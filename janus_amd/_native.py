@@ -1,0 +1,97 @@
+"""Loader for libjanus_hip.so, the gfx950 HIP library behind include/janus.h.
+
+torch is imported first so that libjanus_hip.so binds to the same HIP runtime
+(libamdhip64.so.7) torch already loaded; device pointers from torch tensors are then
+valid in both. There is no fallback: if the library is missing or fails to load,
+every janus_amd entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libjanus_hip.so")
+
+
+class JanusNativeError(RuntimeError):
+    """A libjanus_hip.so entry point returned a non-zero status."""
+
+
+class janus_value(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("i", ctypes.c_int64), ("f", ctypes.c_double),
+                ("s", ctypes.c_char_p), ("len", ctypes.c_size_t)]
+
+
+class janus_packet(ctypes.Structure):
+    _fields_ = [("text", ctypes.c_char_p), ("text_len", ctypes.c_size_t),
+                ("mode", ctypes.c_int64), ("n_prosody", ctypes.c_int32),
+                ("prosody_keys", ctypes.POINTER(janus_value)),
+                ("prosody_vals", ctypes.POINTER(janus_value)),
+                ("override_emotion", ctypes.c_char_p), ("override_len", ctypes.c_size_t),
+                ("timestamp", janus_value)]
+
+
+class janus_mp_node(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("i", ctypes.c_int64), ("f", ctypes.c_double),
+                ("offset", ctypes.c_size_t), ("len", ctypes.c_size_t)]
+
+
+VAL_NIL, VAL_BOOL, VAL_INT, VAL_UINT, VAL_FLOAT, VAL_STR, VAL_BIN, VAL_ARRAY, VAL_MAP = range(9)
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int
+_I64 = ctypes.c_int64
+_F32 = ctypes.c_float
+
+# name -> (argtypes). Every entry point returns int status.
+SIGNATURES = {
+    "janus_version": [],
+    "janus_prosody_analyze": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
+                              _P, _P, _P],
+    "janus_pack_packet": [ctypes.POINTER(janus_packet), _P, ctypes.c_size_t,
+                          ctypes.POINTER(ctypes.c_size_t)],
+    "janus_unpack": [_P, ctypes.c_size_t, ctypes.POINTER(janus_mp_node), ctypes.c_size_t,
+                     ctypes.POINTER(ctypes.c_size_t)],
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library (raises ImportError if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc --offload-arch=gfx950). janus_amd has no CPU fallback.")
+        l = ctypes.CDLL(LIB_PATH)
+        l.janus_last_error.restype = ctypes.c_char_p
+        l.janus_last_error.argtypes = []
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = l
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise JanusNativeError(lib().janus_last_error().decode("utf-8", "replace"))
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args))
+
+
+def require_gpu() -> torch.device:
+    """The product path runs on the GPU only; fail loudly otherwise."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("janus_amd needs an AMD Instinct GPU (gfx950); none is visible")
+    lib()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

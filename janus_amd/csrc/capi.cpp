@@ -1,0 +1,34 @@
+// C-ABI glue: error slot, version, thin extern "C" wrappers over the launchers.
+#include "common.h"
+#include "../../include/janus.h"
+
+namespace janus {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
+                    int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,
+                    const float* state_in, float* state_out, float* f0_out, float* rms_out,
+                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream);
+
+}  // namespace janus
+
+using namespace janus;
+
+extern "C" const char* janus_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int janus_version(void) { return 100; }
+
+extern "C" int janus_prosody_analyze(const float* pcm, const int64_t* sample_offsets,
+                                     const int64_t* hop_offsets, int batch, int64_t total_hops,
+                                     int sample_rate, int hop_size, float tolerance,
+                                     float silence_db, const float* state_in, float* state_out,
+                                     float* f0_out, float* rms_out, float* mean_f0_out,
+                                     int32_t* n_voiced_out, void* stream) {
+  return guarded([&] {
+    prosody_launch(pcm, sample_offsets, hop_offsets, batch, total_hops, sample_rate, hop_size,
+                   tolerance, silence_db, state_in, state_out, f0_out, rms_out, mean_f0_out,
+                   n_voiced_out, (hipStream_t)stream);
+  });
+}

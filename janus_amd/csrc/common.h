@@ -1,0 +1,58 @@
+// Shared helpers for the janus HIP library (gfx950 / CDNA4 only).
+//
+// Error model: every extern "C" entry point returns int (0 = OK) and never lets a
+// C++ exception cross the ABI; the message is kept per thread and read back with
+// janus_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <stdexcept>
+
+namespace janus {
+
+void set_error(const std::string& msg);
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define JANUS_HIP(expr)                                                          \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess)                                                        \
+      throw ::janus::Error(std::string(#expr) + ": " + hipGetErrorString(e_) +   \
+                           " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")"); \
+  } while (0)
+
+#define JANUS_CHECK(cond, msg)                                                   \
+  do {                                                                           \
+    if (!(cond)) throw ::janus::Error(std::string(msg));                         \
+  } while (0)
+
+// Wrap an entry-point body: map exceptions to status codes.
+template <class F>
+inline int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return 1;
+  } catch (...) {
+    set_error("unknown C++ exception");
+    return 1;
+  }
+}
+
+// Launch check after <<<>>> (launch config errors surface here, not faults).
+#define JANUS_LAUNCH_CHECK() JANUS_HIP(hipGetLastError())
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace janus

@@ -1,0 +1,282 @@
+// Prosody hot path: per-hop YIN pitch (aubio 'yin', buf 4096) + RMS energy, batched
+// over a ragged set of utterances (one stream each).
+//
+// Replaces, for the reference's ProsodyExtractor (backend/services/prosody.py):
+//   :32-34  aubio.pitch('yin', 4096, hop, sr), unit Hz, tolerance 0.8  (one stateful detector)
+//   :67     rms = sqrt(mean(x**2))
+//   :78-87  per-hop loop: zero-pad last hop to `hop`, pitch = detector(chunk)[0], keep > 0
+//   :90     mean of voiced pitches
+// aubio 0.4.9 is a third-party C library absent from this container; its published
+// algorithm (src/pitch/pitch.c aubio_pitch_do / aubio_pitch_do_yin / slideblock,
+// src/pitch/pitchyin.c aubio_pitchyin_do, src/mathutils.c aubio_quadratic_peak_pos /
+// fvec_min_elem / aubio_level_lin / aubio_db_spl) is restated here and in
+// oracle/yin_oracle.c. The arithmetic below keeps aubio's float rounding order
+// (sequential j-sum, separate mul/add, sequential tau running sum, float divide),
+// so per-hop f0 is bit-identical to the sequential C restatement.
+//
+// Layout in HBM: pcm is one flat f32 array of all utterances back to back
+// (sample_offsets[B+1]); hops are numbered globally (hop_offsets[B+1]); per-stream
+// detector state is the 4096-sample aubio buffer, [B][4096] f32.
+//
+// Roofline: VALU-bound (fp32 non-contracted sub/mul/add), ≈3·2048 flop per tau,
+// up to 2047 taus per hop; HBM traffic is 16 KB window per hop (L2-served overlap).
+#include "common.h"
+
+namespace janus {
+
+constexpr int kYinBuf = 4096;          // aubio pitch buffer (prosody.py:32)
+constexpr int kYinLen = kYinBuf / 2;   // yin fvec length
+constexpr int kYinThreads = 256;       // 4 waves; each lane owns 4 consecutive taus
+constexpr int kTauChunk = kYinThreads * 4;  // 1024 taus per pass
+
+__device__ __forceinline__ int find_utt(const int64_t* offs, int B, int64_t g) {
+  // largest b with offs[b] <= g (offs is non-decreasing, offs[0]=0, offs[B]=total)
+  int lo = 0, hi = B;  // invariant: offs[lo] <= g < offs[hi]
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (offs[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Window sample k (0..4095) of hop i of stream b: the aubio buffer after sliding
+// hop i in (prosody.py:81-84, aubio_pitch_slideblock).
+__device__ __forceinline__ float window_sample(const float* pcm, int64_t base, int64_t n,
+                                               const float* state, int64_t i, int hop, int k) {
+  int64_t p = (i + 1) * (int64_t)hop - kYinBuf + k;
+  if (p < 0) return state ? state[kYinBuf + p] : 0.0f;
+  return p < n ? pcm[base + p] : 0.0f;
+}
+
+__global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
+    const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
+    const int64_t* __restrict__ hop_off, int B, int hop, const float* __restrict__ state_in,
+    float tol, float silence_db, unsigned sample_rate, float* __restrict__ f0_out,
+    int64_t total_hops) {
+  __shared__ __attribute__((aligned(16))) float w[kYinBuf];
+  __shared__ __attribute__((aligned(16))) float dd[kYinLen];   // d(tau), then yin(tau)
+  __shared__ float cum[kYinLen];                               // running sum (tmp2)
+  __shared__ int s_found;
+  __shared__ float s_level;
+  __shared__ unsigned long long s_best;  // argmin key
+
+  const int tid = threadIdx.x;
+  for (int64_t g = blockIdx.x; g < total_hops; g += gridDim.x) {
+    const int b = find_utt(hop_off, B, g);
+    const int64_t i = g - hop_off[b];
+    const int64_t base = sample_off[b];
+    const int64_t n = sample_off[b + 1] - base;
+    const float* st = state_in ? state_in + (int64_t)b * kYinBuf : nullptr;
+
+    for (int k = tid; k < kYinBuf; k += kYinThreads)
+      w[k] = window_sample(pcm, base, n, st, i, hop, k);
+    if (tid == 0) s_found = 0x7fffffff;
+    __syncthreads();
+
+    // aubio_level_lin on the new hop (sequential float sum, as aubio).
+    if (tid == kYinThreads - 1) {
+      float e = 0.0f;
+      for (int j = kYinBuf - hop; j < kYinBuf; ++j) e = __fadd_rn(e, __fmul_rn(w[j], w[j]));
+      s_level = __fdiv_rn(e, (float)hop);
+    }
+
+    float running = 0.0f;  // tmp2, carried across chunks (only lane 0 uses it)
+    int found = 0x7fffffff;
+    for (int chunk = 0; chunk < kYinLen / kTauChunk; ++chunk) {
+      const int tau0 = chunk * kTauChunk + 4 * tid;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+#pragma unroll 2
+      for (int j = 0; j < kYinLen; j += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(&w[j]);
+        const float4 p = *reinterpret_cast<const float4*>(&w[j + tau0]);
+        const float4 q = *reinterpret_cast<const float4*>(&w[j + tau0 + 4]);
+        const float av[4] = {a.x, a.y, a.z, a.w};
+        const float bv[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          float t0 = __fsub_rn(av[jj], bv[jj + 0]);
+          float t1 = __fsub_rn(av[jj], bv[jj + 1]);
+          float t2 = __fsub_rn(av[jj], bv[jj + 2]);
+          float t3 = __fsub_rn(av[jj], bv[jj + 3]);
+          acc0 = __fadd_rn(acc0, __fmul_rn(t0, t0));
+          acc1 = __fadd_rn(acc1, __fmul_rn(t1, t1));
+          acc2 = __fadd_rn(acc2, __fmul_rn(t2, t2));
+          acc3 = __fadd_rn(acc3, __fmul_rn(t3, t3));
+        }
+      }
+      dd[tau0 + 0] = acc0;
+      dd[tau0 + 1] = acc1;
+      dd[tau0 + 2] = acc2;
+      dd[tau0 + 3] = acc3;
+      __syncthreads();
+      // tmp2 += yin[tau] in tau order (pitchyin.c), one lane.
+      if (tid == 0) {
+        const int t_begin = chunk == 0 ? 1 : chunk * kTauChunk;
+        for (int t = t_begin; t < (chunk + 1) * kTauChunk; ++t) {
+          running = __fadd_rn(running, dd[t]);
+          cum[t] = running;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int t = tau0 + m;
+        float y;
+        if (t == 0) y = 1.0f;
+        else {
+          const float s = cum[t];
+          y = (s != 0.0f) ? __fmul_rn(dd[t], __fdiv_rn((float)t, s)) : 1.0f;
+        }
+        dd[t] = y;
+      }
+      __syncthreads();
+      // Early exit: first period p in [2, 2044] (tau = p+3 computed) with
+      // yin[p] < tol && yin[p] < yin[p+1]. Periods whose p+1 lies in the next chunk wait.
+      const int p_hi = min((chunk + 1) * kTauChunk - 2, kYinLen - 4);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int p = tau0 + m - (chunk == 0 ? 0 : 1);  // chunk>0 also re-checks its first-1
+        if (p >= 2 && p <= p_hi && p >= chunk * kTauChunk - 1) {
+          const float yp = dd[p];
+          if (yp < tol && yp < dd[p + 1]) atomicMin(&s_found, p);
+        }
+      }
+      __syncthreads();
+      found = s_found;
+      if (found != 0x7fffffff) break;
+    }
+
+    int pos;
+    if (found != 0x7fffffff) {
+      pos = found;
+    } else {
+      // fvec_min_elem: smallest value, ties -> LAST index.
+      if (tid == 0) s_best = ~0ull;
+      __syncthreads();
+      unsigned long long best = ~0ull;
+      for (int t = tid; t < kYinLen; t += kYinThreads) {
+        // yin >= 0, so the float bit pattern orders like the value; invert index for ties.
+        const unsigned long long key =
+            ((unsigned long long)__float_as_uint(dd[t]) << 32) | (unsigned)(kYinLen - 1 - t);
+        best = key < best ? key : best;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(best, off);
+        best = o < best ? o : best;
+      }
+      if ((tid & 63) == 0) atomicMin(&s_best, best);
+      __syncthreads();
+      pos = kYinLen - 1 - (int)(s_best & 0xffffffffu);
+    }
+
+    if (tid == 0) {
+      // aubio_quadratic_peak_pos
+      float period;
+      if (pos == 0 || pos == kYinLen - 1) {
+        period = (float)pos;
+      } else {
+        const float s0 = dd[pos - 1], s1 = dd[pos], s2 = dd[pos + 1];
+        const float num = __fmul_rn(0.5f, __fsub_rn(s0, s2));
+        const float den = __fadd_rn(__fsub_rn(s0, __fmul_rn(2.0f, s1)), s2);
+        period = __fadd_rn((float)pos, __fdiv_rn(num, den));
+      }
+      // aubio_pitch_do_yin: samplerate / (pitch + 0.) in double, stored as float.
+      float f0 = period > 0.0f ? (float)((double)sample_rate / (double)period) : 0.0f;
+      // aubio_silence_detection(ibuf, silence): 10*log10f(level) < silence -> 0
+      const float db = (float)(10.0 * (double)log10f(s_level));
+      if (db < silence_db) f0 = 0.0f;
+      f0_out[g] = f0;
+    }
+    __syncthreads();
+  }
+}
+
+// Per-utterance: RMS over the buffer (prosody.py:67), mean and count of voiced f0 (:86-90).
+__global__ __launch_bounds__(256) void prosody_reduce_kernel(
+    const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
+    const int64_t* __restrict__ hop_off, const float* __restrict__ f0, float* __restrict__ rms_out,
+    float* __restrict__ mean_f0_out, int32_t* __restrict__ n_voiced_out) {
+  const int b = blockIdx.x;
+  const int64_t base = sample_off[b], n = sample_off[b + 1] - base;
+  const int64_t h0 = hop_off[b], nh = hop_off[b + 1] - h0;
+  double ss = 0.0, fs = 0.0;
+  int cnt = 0;
+  const float* x = pcm + base;
+  // vectorised when aligned; pcm offsets are arbitrary, so peel to 16 B.
+  int64_t head = (int64_t)((16 - ((uintptr_t)x & 15)) & 15) / 4;
+  if (head > n) head = n;
+  for (int64_t k = threadIdx.x; k < head; k += blockDim.x) ss += (double)x[k] * x[k];
+  const int64_t nv = (n - head) / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x + head);
+  for (int64_t k = threadIdx.x; k < nv; k += blockDim.x) {
+    const float4 v = x4[k];
+    ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (int64_t k = head + nv * 4 + threadIdx.x; k < n; k += blockDim.x) ss += (double)x[k] * x[k];
+  for (int64_t k = threadIdx.x; k < nh; k += blockDim.x) {
+    const float v = f0[h0 + k];
+    if (v > 0.0f) { fs += v; ++cnt; }
+  }
+  __shared__ double sh_ss[4], sh_fs[4];
+  __shared__ int sh_c[4];
+  for (int off = 32; off > 0; off >>= 1) {
+    ss += __shfl_xor(ss, off);
+    fs += __shfl_xor(fs, off);
+    cnt += __shfl_xor(cnt, off);
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh_ss[wid] = ss; sh_fs[wid] = fs; sh_c[wid] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0, f = 0;
+    int c = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { s += sh_ss[k]; f += sh_fs[k]; c += sh_c[k]; }
+    rms_out[b] = n > 0 ? (float)sqrt(s / (double)n) : __int_as_float(0x7fc00000);  // mean([]) = nan
+    mean_f0_out[b] = c > 0 ? (float)(f / c) : 0.0f;
+    n_voiced_out[b] = c;
+  }
+}
+
+// Detector state after the call = the aubio buffer after the last hop.
+__global__ void prosody_state_kernel(const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
+                                     const int64_t* __restrict__ hop_off, int hop,
+                                     const float* __restrict__ state_in, float* __restrict__ state_out) {
+  const int b = blockIdx.x;
+  const int64_t base = sample_off[b], n = sample_off[b + 1] - base;
+  const int64_t nh = hop_off[b + 1] - hop_off[b];
+  const float* st = state_in ? state_in + (int64_t)b * kYinBuf : nullptr;
+  for (int k = threadIdx.x; k < kYinBuf; k += blockDim.x) {
+    float v;
+    if (nh == 0) v = st ? st[k] : 0.0f;
+    else v = window_sample(pcm, base, n, st, nh - 1, hop, k);
+    state_out[(int64_t)b * kYinBuf + k] = v;
+  }
+}
+
+void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
+                    int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,
+                    const float* state_in, float* state_out, float* f0_out, float* rms_out,
+                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream) {
+  JANUS_CHECK(B >= 0, "batch must be >= 0");
+  JANUS_CHECK(hop > 0 && hop <= kYinBuf, "hop_size must be in [1, 4096]");
+  JANUS_CHECK(sample_rate > 0, "sample_rate must be > 0");
+  if (B == 0) return;
+  JANUS_CHECK(state_in != state_out || state_in == nullptr, "state_in and state_out must not alias");
+  if (total_hops > 0) {
+    const int64_t grid = total_hops < (1ll << 30) ? total_hops : (1ll << 30);
+    yin_hops_kernel<<<dim3((unsigned)grid), dim3(kYinThreads), 0, stream>>>(
+        pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate, f0_out,
+        total_hops);
+    JANUS_LAUNCH_CHECK();
+  }
+  prosody_reduce_kernel<<<dim3(B), dim3(256), 0, stream>>>(pcm, sample_off, hop_off, f0_out, rms_out,
+                                                           mean_f0_out, n_voiced_out);
+  JANUS_LAUNCH_CHECK();
+  if (state_out) {
+    prosody_state_kernel<<<dim3(B), dim3(256), 0, stream>>>(pcm, sample_off, hop_off, hop, state_in,
+                                                            state_out);
+    JANUS_LAUNCH_CHECK();
+  }
+}
+
+}  // namespace janus

@@ -1,0 +1,94 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+CPU restatement of ``ProsodyExtractor`` (backend/services/prosody.py:11-104):
+energy from numpy float32 RMS (:67-74), pitch from the sequential aubio-YIN
+restatement in oracle/yin_oracle.c (:32-34, :78-87), mean of voiced pitches and
+bucketing (:89-99), result dict in ``energy, pitch`` order (:101-104).
+
+Pinned by the reference's known-answer tests (tests/test_oracle.py):
+test_input_processing.py:461-468 (0.02 amplitude -> 'Quiet'), :470-478 (ranges),
+:480-490 (440 Hz sine -> 'High'), :492-505 (list input).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import BUILD_DIR, build
+
+YIN_BUF = 4096
+DEFAULT_SILENCE_DB = -50.0   # aubio src/pitch/pitch.c DEFAULT_PITCH_SILENCE
+DEFAULT_TOLERANCE = 0.8      # prosody.py:34
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        path = os.path.join(BUILD_DIR, "libjanus_oracle.so")
+        if not os.path.exists(path):
+            build()
+        lib = ctypes.CDLL(path)
+        lib.yin_oracle_stream.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+            ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        lib.yin_oracle_stream.restype = None
+        _lib = lib
+    return _lib
+
+
+def yin_stream(x, sample_rate=48000, hop=512, tol=DEFAULT_TOLERANCE,
+               silence_db=DEFAULT_SILENCE_DB, state=None):
+    """Per-hop f0 (Hz) of a stream, aubio semantics. Returns (f0[nhops], new_state)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    st = np.zeros(YIN_BUF, np.float32) if state is None else np.array(state, np.float32, copy=True)
+    nh = (len(x) + hop - 1) // hop
+    f0 = np.zeros(max(nh, 0), np.float32)
+    _load().yin_oracle_stream(x.ctypes.data, len(x), sample_rate, hop, tol, silence_db,
+                              st.ctypes.data, f0.ctypes.data)
+    return f0, st
+
+
+def energy_tag(rms) -> str:
+    """prosody.py:69-74 (NaN from an empty buffer compares False -> 'Loud')."""
+    if rms < 0.05:
+        return 'Quiet'
+    elif rms < 0.15:
+        return 'Normal'
+    return 'Loud'
+
+
+def pitch_tag(voiced) -> str:
+    """prosody.py:89-99."""
+    if len(voiced) > 0:
+        avg = np.mean(voiced)
+        if avg < 120:
+            return 'Deep'
+        elif avg < 200:
+            return 'Normal'
+        return 'High'
+    return 'Normal'
+
+
+class OracleProsody:
+    """Stateful mirror of ProsodyExtractor on the CPU (one aubio buffer per object)."""
+
+    def __init__(self, sample_rate: int = 48000, hop_size: int = 512):
+        self.sample_rate = sample_rate
+        self.hop_size = hop_size
+        self.state = np.zeros(YIN_BUF, np.float32)
+
+    def analyze_buffer(self, audio_buffer):
+        if isinstance(audio_buffer, list):
+            audio_buffer = np.concatenate(audio_buffer)
+        if not isinstance(audio_buffer, np.ndarray):
+            audio_buffer = np.array(audio_buffer, dtype=np.float32)
+        if audio_buffer.dtype != np.float32:
+            audio_buffer = audio_buffer.astype(np.float32)
+        with np.errstate(all='ignore'):
+            rms = np.sqrt(np.mean(audio_buffer ** 2))
+        f0, self.state = yin_stream(audio_buffer, self.sample_rate, self.hop_size,
+                                    state=self.state)
+        voiced = [p for p in f0 if p > 0.0]
+        return {'energy': energy_tag(rms), 'pitch': pitch_tag(voiced)}, f0, rms

@@ -1,0 +1,41 @@
+"""The C-ABI library loads and exports every symbol include/janus.h declares (CPU)."""
+import ctypes
+import os
+import re
+
+from janus_amd import _native
+
+HEADER_DIR = os.path.join(os.path.dirname(__file__), "..", "include")
+
+
+def declared_symbols():
+    names = set()
+    for fn in os.listdir(HEADER_DIR):
+        if fn.endswith(".h"):
+            src = open(os.path.join(HEADER_DIR, fn)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names |= set(re.findall(r"\b(janus_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_header_symbols_exported(native_lib):
+    names = declared_symbols()
+    assert "janus_prosody_analyze" in names and "janus_pack_packet" in names
+    for name in sorted(names):
+        assert hasattr(native_lib, name), f"{name} declared in include/ but not exported"
+
+
+def test_python_signatures_cover_header(native_lib):
+    names = declared_symbols() - {"janus_last_error"}
+    missing = names - set(_native.SIGNATURES)
+    assert not missing, f"no ctypes signature for {sorted(missing)}"
+
+
+def test_version_and_error_slot(native_lib):
+    assert native_lib.janus_version() >= 100
+    assert isinstance(native_lib.janus_last_error(), bytes)
+
+
+def test_gfx950_code_object():
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
