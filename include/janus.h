@@ -106,6 +106,75 @@ typedef struct {
 int janus_unpack(const uint8_t* buf, size_t len, janus_mp_node* nodes, size_t cap,
                  size_t* n_nodes);
 
+
+/* ------------------------------------------------------------ whisper --- */
+/*
+ * Whisper speech-to-text on the GPU. Replaces faster-whisper's WhisperModel
+ * (CTranslate2) as constructed at backend/services/transcriber.py:23-27 and driven by
+ * model.transcribe(audio[::3], beam_size=1, language='en') at :51-57 (one 30 s window
+ * per utterance). fp16 tensors are passed as uint16_t (IEEE binary16 bits).
+ */
+typedef struct {
+  int n_mels;      /* 80 */
+  int n_audio_ctx; /* 1500 encoder positions (3000 mel frames) */
+  int d_model;     /* 384 tiny, 512 base */
+  int n_heads;     /* d_model / 64 */
+  int enc_layers;
+  int dec_layers;
+  int n_vocab;     /* 51864 for *.en */
+  int n_text_ctx;  /* 448 */
+} janus_whisper_config;
+
+typedef struct janus_whisper janus_whisper;
+
+int janus_whisper_create(const janus_whisper_config* cfg, janus_whisper** out);
+int janus_whisper_destroy(janus_whisper* w);
+/*
+ * Upload one fp32 parameter [host] by its Hugging Face Whisper name without the
+ * "model." prefix (e.g. "encoder.layers.0.fc1.weight"), plus the two front-end
+ * constants "mel.basis" [400][416] (periodic-Hann-weighted cos|sin DFT basis, 208
+ * bins each) and "mel.filters" [208][80] (slaney mel filters, transposed, zero-padded).
+ */
+int janus_whisper_set_tensor(janus_whisper* w, const char* name, const float* host,
+                             int64_t numel);
+/*
+ * Log-mel features (faster-whisper FeatureExtractor, n_fft 400, hop 160, 80 mels,
+ * 3000 frames) of x[::decim] for each utterance of pcm [device] (offsets [device]
+ * int64[B+1]; <= 30 s after decimation). logmel [device] f32 [B][3000][80] (raw
+ * log10 mel, may be NULL), mel [device] fp16 [B][3000][80] (clamped and scaled).
+ */
+int janus_whisper_logmel(janus_whisper* w, const float* pcm, const int64_t* offsets, int batch,
+                         int decim, float* logmel, uint16_t* mel, void* stream);
+/* Encoder forward: mel [device] fp16 [B][3000][80] -> enc [device] fp16 [B][1500][d]. */
+int janus_whisper_encode(janus_whisper* w, const uint16_t* mel, int batch, uint16_t* enc,
+                         void* stream);
+
+typedef struct {
+  const int32_t* prompt;   /* [host] initial tokens, e.g. {<|startoftranscript|>} for *.en */
+  int prompt_len;
+  int max_length;          /* total tokens incl. prompt (faster-whisper max_length 448) */
+  int eot;
+  const int32_t* suppress; /* [host] always-suppressed token ids (suppress_tokens=[-1] set) */
+  int n_suppress;
+  int suppress_blank;      /* SuppressBlank at the first sampled token */
+  int blank_token;         /* " " token id */
+  int timestamp_begin;     /* first timestamp token id, -1 = no timestamp rules */
+  int no_timestamps;       /* <|notimestamps|> id */
+  int max_initial_timestamp_index; /* 50 (= 1.0 s), -1 = unbounded */
+  int check_every;         /* poll for all-rows-finished every N steps (0 = never) */
+} janus_decode_options;
+
+/*
+ * Batched greedy decoding (temperature 0) with the Whisper logit rules
+ * (SuppressBlank, SuppressTokens, ApplyTimestampRules), KV cache on the device.
+ * tokens [device] int32 [B][max_length] (prompt, then sampled tokens; -1 past the
+ * end), n_tokens [device] int32 [B] sampled tokens incl. <|endoftext|>,
+ * sum_logprob [device] f32 [B] (sum of chosen-token log-probabilities).
+ */
+int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc, int batch,
+                                const janus_decode_options* opt, int32_t* tokens,
+                                int32_t* n_tokens, float* sum_logprob, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

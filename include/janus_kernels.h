@@ -1,0 +1,65 @@
+/*
+ * janus_kernels.h — kernel-level C-ABI of libjanus_hip.so (gfx950).
+ *
+ * The building blocks the whisper / vocoder entry points of janus.h are made of,
+ * exposed for parity tests and for callers that orchestrate their own graphs. All
+ * pointers are [device]; fp16 tensors are uint16_t (binary16 bits); all calls are
+ * asynchronous on `stream`. Return 0 on success (janus_last_error() otherwise).
+ */
+#ifndef JANUS_KERNELS_H_
+#define JANUS_KERNELS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Epilogues of janus_gemm_f16 */
+enum { JANUS_EPI_F16 = 0, JANUS_EPI_GELU_F16 = 1, JANUS_EPI_RESID_F32 = 2, JANUS_EPI_F32 = 3 };
+/* Activations of janus_conv1d_f16 */
+enum { JANUS_ACT_NONE = 0, JANUS_ACT_SILU = 1, JANUS_ACT_GELU = 2, JANUS_ACT_TANH = 3 };
+
+/*
+ * C[M,N] = epi(A[M,K] · W[N,K]^T + bias[N]); A, W fp16 (K contiguous, K % 8 == 0);
+ * C fp16 or fp32 by epilogue; JANUS_EPI_RESID_F32: C = R + (A·W^T + bias) in fp32.
+ * Replaces the dense projections inside CTranslate2's Whisper (transcriber.py:23-27).
+ */
+int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                   const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
+                   int N, int K, void* stream);
+
+/* LayerNorm rows of an fp32 [rows][d] tensor into fp16 (eps as given). */
+int janus_layernorm_f16(const float* x, const float* gamma, const float* beta, uint16_t* out,
+                        int rows, int d, float eps, void* stream);
+
+/* Non-causal multi-head attention, head_dim 64: qkv fp16 [B*T][3*H*64] -> out fp16 [B*T][H*64]. */
+int janus_attention_f16(const uint16_t* qkv, uint16_t* out, int batch, int T, int H, float scale,
+                        void* stream);
+
+/* Size in fp16 elements of the packed weight buffer janus_conv1d_pack expects/produces. */
+int64_t janus_conv1d_packed_size(int Cin, int Cout, int taps, int transposed, int stride);
+/*
+ * Pack fp32 PyTorch conv weights for janus_conv1d_f16: Conv1d [Cout][Cin][taps]
+ * (transposed=0) or ConvTranspose1d [Cin][Cout][2*stride] (transposed=1).
+ */
+int janus_conv1d_pack(const float* w, uint16_t* packed, int Cin, int Cout, int taps,
+                      int transposed, int stride, void* stream);
+/*
+ * Time-major 1-D convolution on MFMA: in [B][T_in][Cin], out [B][T_out][Cout] (fp16).
+ * transposed=0: PyTorch Conv1d(Cin, Cout, taps, stride, padding, dilation)
+ * transposed=1: ConvTranspose1d(Cin, Cout, 2*stride, stride, padding) (taps ignored).
+ * y = post_act(conv(pre_act(x)) + bias); y += res (fp16 [B][T_out][Cout], may be NULL,
+ * res_bs = batch stride in elements, 0 to broadcast); out = (accumulate ? out : 0) + scale*y.
+ */
+int janus_conv1d_f16(const uint16_t* in, int batch, int T_in, int Cin, const uint16_t* packed,
+                     const float* bias, uint16_t* out, int T_out, int Cout, int taps, int stride,
+                     int padding, int dilation, int transposed, int pre_act, int post_act,
+                     const uint16_t* res, int64_t res_bs, float scale, int accumulate,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JANUS_KERNELS_H_ */

@@ -52,7 +52,22 @@ SIGNATURES = {
                           ctypes.POINTER(ctypes.c_size_t)],
     "janus_unpack": [_P, ctypes.c_size_t, ctypes.POINTER(janus_mp_node), ctypes.c_size_t,
                      ctypes.POINTER(ctypes.c_size_t)],
+    "janus_whisper_create": [_P, _P],
+    "janus_whisper_destroy": [_P],
+    "janus_whisper_set_tensor": [_P, ctypes.c_char_p, _P, _I64],
+    "janus_whisper_logmel": [_P, _P, _P, _I32, _I32, _P, _P, _P],
+    "janus_whisper_encode": [_P, _P, _I32, _P, _P],
+    "janus_whisper_decode_greedy": [_P, _P, _I32, _P, _P, _P, _P, _P],
+    # include/janus_kernels.h
+    "janus_gemm_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
+    "janus_layernorm_f16": [_P, _P, _P, _P, _I32, _I32, _F32, _P],
+    "janus_attention_f16": [_P, _P, _I32, _I32, _I32, _F32, _P],
+    "janus_conv1d_packed_size": [_I32, _I32, _I32, _I32, _I32],
+    "janus_conv1d_pack": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P],
+    "janus_conv1d_f16": [_P, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32,
+                         _I32, _I32, _I32, _P, _I64, _F32, _I32, _P],
 }
+RESTYPES = {"janus_conv1d_packed_size": ctypes.c_int64}
 
 _lib = None
 
@@ -71,7 +86,7 @@ def lib() -> ctypes.CDLL:
         for name, argtypes in SIGNATURES.items():
             fn = getattr(l, name)
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_int
+            fn.restype = RESTYPES.get(name, ctypes.c_int)
         _lib = l
     return _lib
 

@@ -1,0 +1,231 @@
+// Attention for the Whisper encoder (non-causal, T = 1500, head_dim 64) and decoder
+// (one query per step against a K/V cache).
+//
+// Encoder: flash-style, fp16 MFMA 16x16x32 with fp32 online softmax (exp2 domain).
+// Block = 4 waves = 64 query rows of one (b, h); each wave owns 16 rows. Q fragments
+// stay in registers; 64-key K and V tiles are staged in LDS (V transposed on the way
+// in so P·V reads 16-byte B fragments); P goes through a per-wave LDS tile to become
+// the A operand. The S = QK^T score matrix is never materialised in HBM.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+constexpr int kHd = 64;        // Whisper head_dim (all model sizes)
+constexpr int kQT = 64;        // query rows per block
+constexpr int kKT = 64;        // keys per tile
+constexpr int kLS = kHd + 8;   // LDS row stride (halves): 144 B, 16-B aligned, odd x16
+
+__global__ __launch_bounds__(256) void attention_kernel(const _Float16* __restrict__ qkv,
+                                                        _Float16* __restrict__ out, int T, int H,
+                                                        float scale_log2) {
+  __shared__ __attribute__((aligned(16))) _Float16 sK[kKT * kLS];
+  __shared__ __attribute__((aligned(16))) _Float16 sVt[kHd * kLS];
+  __shared__ __attribute__((aligned(16))) _Float16 sP[4][16 * kLS];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int d = H * kHd;
+  const int64_t ld = 3 * (int64_t)d;
+  const _Float16* base = qkv + (int64_t)b * T * ld;
+  const int q0 = blockIdx.x * kQT + w * 16;
+
+  // Q fragments (A operand): row q0 + (lane&15), dims ks*32 + 8*(lane>>4) .. +7
+  half8 aq[2];
+  {
+    const int qr = q0 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      aq[ks] = qr < T ? *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + h * kHd + ks * 32 + 8 * (lane >> 4))
+                      : zero_half8();
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = zero_f32x4();
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mrow[r] = -INFINITY; lrow[r] = 0.f; }
+
+  for (int k0 = 0; k0 < T; k0 += kKT) {
+    __syncthreads();
+    // stage K tile [key][dim] and V^T tile [dim][key]; 64 keys x 8 chunks of 16 B each
+    for (int idx = tid; idx < kKT * 8; idx += 256) {
+      const int key = idx >> 3, c = idx & 7;
+      const int kr = k0 + key;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (kr < T) {
+        const _Float16* rowp = base + (int64_t)kr * ld + h * kHd + c * 8;
+        kv = *reinterpret_cast<const uint4*>(rowp + d);
+        vv = *reinterpret_cast<const uint4*>(rowp + 2 * d);
+      }
+      *reinterpret_cast<uint4*>(sK + key * kLS + c * 8) = kv;
+      const _Float16* vh = reinterpret_cast<const _Float16*>(&vv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[(c * 8 + j) * kLS + key] = vh[j];
+    }
+    __syncthreads();
+
+    // S = Q K^T for 4 key tiles of 16
+    f32x4 s[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      s[n] = zero_f32x4();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const half8 bk = *reinterpret_cast<const half8*>(sK + (n * 16 + (lane & 15)) * kLS + ks * 32 + 8 * (lane >> 4));
+        s[n] = mfma16(aq[ks], bk, s[n]);
+      }
+    }
+    // scale (log2 domain), mask the tail, row max over this tile
+    float tmax[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tmax[r] = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const bool valid = (k0 + n * 16 + (lane & 15)) < T;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = valid ? s[n][r] * scale_log2 : -INFINITY;
+        s[n][r] = v;
+        tmax[r] = fmaxf(tmax[r], v);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) tmax[r] = fmaxf(tmax[r], __shfl_xor(tmax[r], off));
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mn = fmaxf(mrow[r], tmax[r]);
+      alpha[r] = exp2f(mrow[r] - mn);  // mrow = -inf on the first tile -> 0
+      mrow[r] = mn;
+      lrow[r] *= alpha[r];
+    }
+    _Float16* pw = sP[w];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(s[n][r] - mrow[r]);
+        lrow[r] += pv;
+        pw[(4 * (lane >> 4) + r) * kLS + n * 16 + (lane & 15)] = (_Float16)pv;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P stores visible to this wave
+    __builtin_amdgcn_wave_barrier();
+    half8 ap[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      ap[ks] = *reinterpret_cast<const half8*>(pw + (lane & 15) * kLS + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const half8 bv = *reinterpret_cast<const half8*>(sVt + (n * 16 + (lane & 15)) * kLS + ks * 32 + 8 * (lane >> 4));
+        o[n] = mfma16(ap[ks], bv, o[n]);
+      }
+    }
+  }
+  // row sums live spread over the 16 lanes of each row group
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) lrow[r] += __shfl_xor(lrow[r], off);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qr = q0 + 4 * (lane >> 4) + r;
+    if (qr >= T) continue;
+    const float inv = 1.0f / lrow[r];
+    _Float16* orow = out + ((int64_t)b * T + qr) * d + h * kHd;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) orow[n * 16 + (lane & 15)] = (_Float16)(o[n][r] * inv);
+  }
+}
+
+void attention_launch(const _Float16* qkv, _Float16* out, int B, int T, int H, float scale,
+                      hipStream_t s) {
+  if (B <= 0 || T <= 0) return;
+  dim3 grid((T + kQT - 1) / kQT, H, B);
+  attention_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
+  JANUS_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- decode
+// One block per (h, b): scores for all cached keys into LDS, block softmax, then
+// 4 key-groups x 64 dims accumulate P·V with coalesced 128-byte V rows.
+constexpr int kMaxKv = 2048;
+
+__global__ __launch_bounds__(256) void decode_attention_kernel(
+    const _Float16* __restrict__ q, int64_t q_bs, const _Float16* __restrict__ k,
+    const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv,
+    const int32_t* __restrict__ tkv, _Float16* __restrict__ out, int64_t o_bs, float scale) {
+  __shared__ float sq[kHd];
+  __shared__ float sp[kMaxKv];
+  __shared__ float red[8];
+  __shared__ float acc[4][kHd];
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int T = tkv ? tkv[b] : Tkv;
+  if (tid < kHd) sq[tid] = (float)q[(int64_t)b * q_bs + h * kHd + tid];
+  __syncthreads();
+  const _Float16* kb = k + (int64_t)b * kv_bs + h * kHd;
+  const _Float16* vb = v + (int64_t)b * kv_bs + h * kHd;
+  float mx = -INFINITY;
+  for (int t = tid; t < T; t += 256) {
+    const uint4* kr = reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs);
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 u = kr[c];
+      const _Float16* hh = reinterpret_cast<const _Float16*>(&u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot += (float)hh[j] * sq[c * 8 + j];
+    }
+    dot *= scale;
+    sp[t] = dot;
+    mx = fmaxf(mx, dot);
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int t = tid; t < T; t += 256) {
+    const float e = __expf(sp[t] - mx);
+    sp[t] = e;
+    sum += e;
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  __syncthreads();
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+  __syncthreads();
+  const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
+  const int grp = tid >> 6, dd = tid & 63;
+  float a = 0.f;
+  for (int t = grp; t < T; t += 4) a += sp[t] * (float)vb[(int64_t)t * kv_rs + dd];
+  acc[grp][dd] = a;
+  __syncthreads();
+  if (tid < kHd) {
+    const float r = (acc[0][tid] + acc[1][tid] + acc[2][tid] + acc[3][tid]) * inv;
+    out[(int64_t)b * o_bs + h * kHd + tid] = (_Float16)r;
+  }
+}
+
+void decode_attention_launch(const _Float16* q, int64_t q_bs, const _Float16* k, const _Float16* v,
+                             int64_t kv_bs, int64_t kv_rs, int Tkv, const int32_t* tkv,
+                             _Float16* out, int64_t o_bs, int B, int H, float scale,
+                             hipStream_t s) {
+  JANUS_CHECK(Tkv <= kMaxKv, "decode attention: too many keys");
+  if (B <= 0) return;
+  decode_attention_kernel<<<dim3(H, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, tkv, out,
+                                                     o_bs, scale);
+  JANUS_LAUNCH_CHECK();
+}
+
+}  // namespace janus

@@ -1,0 +1,268 @@
+// Implicit-GEMM 1-D convolution / transposed convolution on MFMA (fp16 in, fp32 acc).
+//
+// Used by the Whisper encoder stem (conv1 80->d k3 p1 + GELU; conv2 d->d k3 s2 p1 +
+// GELU + positional embedding) and by every layer of the Firefly-GAN generator
+// (conv_pre k13, ConvTranspose upsamplers, residual dilated ResBlock1 convs with
+// fused pre-SiLU, post-SiLU, residual add and the ParallelBlock 1/3-mean).
+//
+// Layout: activations are time-major [B][T][C] fp16, so output row t of a conv is a
+// GEMM row whose K = taps x Cin operand is the same input tile shifted by tap*dil
+// rows. A block stages an input tile of (BM-1)*stride + (taps-1)*|dil| + 1 rows x CK
+// channels in LDS ONCE per channel chunk and every tap reads it at a row offset (no
+// im2col in HBM). Weights are pre-packed into contiguous [BN x 64] k-blocks
+// (chunk, tap-group) and double-buffered in LDS. Pre-activation (SiLU) is applied
+// while staging; bias, post-activation, residual and scaled accumulation in the
+// epilogue. ConvTranspose1d(stride u, kernel 2u) runs as u phases of a 2-tap conv.
+// Roofline: MFMA-bound for C >= 64; HBM-bound for the 16/32-channel tail stages.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+constexpr int kConvKB = 64;  // K per k-block (two 16x16x32 MFMA k-steps)
+
+ConvPack conv_pack_geometry(int Cin, int Cout, int taps) {
+  ConvPack g;
+  g.ck = (Cin % 64 == 0) ? 64 : (Cin % 32 == 0) ? 32 : 16;
+  g.kb = kConvKB;
+  const int tpg = g.kb / g.ck;
+  g.chunks = Cin / g.ck;
+  g.groups = (taps + tpg - 1) / tpg;
+  g.phase_elems = (int64_t)g.chunks * g.groups * Cout * g.kb;
+  return g;
+}
+
+__global__ void conv_pack_kernel(const float* __restrict__ w, _Float16* __restrict__ packed, int Cin,
+                                 int Cout, int taps, int transposed, int u, int ck, int chunks,
+                                 int groups, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int kb = kConvKB, tpg = kb / ck;
+  int64_t t = idx;
+  const int kk = (int)(t % kb); t /= kb;
+  const int co = (int)(t % Cout); t /= Cout;
+  const int g = (int)(t % groups); t /= groups;
+  const int c = (int)(t % chunks); t /= chunks;
+  const int ph = (int)t;
+  const int tap = g * tpg + kk / ck;
+  const int ci = c * ck + kk % ck;
+  float v = 0.0f;
+  if (tap < taps) {
+    if (!transposed) {
+      v = w[((int64_t)co * Cin + ci) * taps + tap];
+    } else {
+      // ConvTranspose1d weight [Cin][Cout][2u]; phase ph uses kernel index ph (input q)
+      // and ph + u (input q - 1).
+      const int j = tap == 0 ? ph : ph + u;
+      v = w[((int64_t)ci * Cout + co) * (2 * u) + j];
+    }
+  }
+  packed[idx] = (_Float16)v;
+}
+
+void conv_pack_weights(const float* w, _Float16* packed, int Cin, int Cout, int taps,
+                       int transposed, int u, hipStream_t s) {
+  const int real_taps = transposed ? 2 : taps;
+  const int phases = transposed ? u : 1;
+  const ConvPack g = conv_pack_geometry(Cin, Cout, real_taps);
+  const int64_t total = g.phase_elems * phases;
+  conv_pack_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(w, packed, Cin, Cout, real_taps,
+                                                               transposed, u, g.ck, g.chunks,
+                                                               g.groups, total);
+  JANUS_LAUNCH_CHECK();
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_apply(float x) {
+  if constexpr (ACT == ACT_SILU) return silu(x);
+  else if constexpr (ACT == ACT_GELU) return gelu_erf(x);
+  else if constexpr (ACT == ACT_TANH) return tanhf(x);
+  else return x;
+}
+
+__device__ __forceinline__ float act_rt(int act, float x) {
+  switch (act) {
+    case ACT_SILU: return silu(x);
+    case ACT_GELU: return gelu_erf(x);
+    case ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+template <int BM, int BN, int WMT, int WNT, int CK>
+__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
+  constexpr int KB = kConvKB, TPG = KB / CK;
+  constexpr int LI = CK + 8;   // input row stride in halves (odd multiple of 16 B)
+  constexpr int LW = KB + 8;   // weight row stride
+  constexpr int WN = BN / (16 * WNT);
+  static_assert((BM / (16 * WMT)) * WN == 4, "4 waves");
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* sIn = smem;
+  _Float16* sW = smem + rows_max * LI;  // [2][BN][LW]
+
+  const int nbn = (a.Cout + BN - 1) / BN, nbm = (a.n_rows + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int ph = blockIdx.y, b = blockIdx.z;
+  const int r0 = bm * BM, co0 = bn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int lo_tap = min(0, (a.taps - 1) * a.dil);
+  const int row_base = r0 * a.in_stride + a.in_off + lo_tap;   // global input row of LDS row 0
+  const int nrows = (BM - 1) * a.in_stride + abs((a.taps - 1) * a.dil) + 1;
+  const int chunks = a.Cin / CK, groups = (a.taps + TPG - 1) / TPG;
+  const _Float16* inb = a.in + (int64_t)b * a.in_bs;
+  const _Float16* wph = a.w + (int64_t)ph * chunks * groups * a.Cout * KB;
+
+  constexpr int W_CH = (BN * KB / 8 + 255) / 256;
+  uint4 rw[W_CH];
+  auto wload = [&](int c, int g) {
+    const _Float16* src = wph + ((int64_t)(c * groups + g) * a.Cout + co0) * KB;
+#pragma unroll
+    for (int k = 0; k < W_CH; ++k) {
+      const int idx = tid + k * 256;
+      const int row = idx / (KB / 8), cc = idx % (KB / 8);
+      rw[k] = (idx < BN * KB / 8 && co0 + row < a.Cout)
+                  ? *reinterpret_cast<const uint4*>(src + (int64_t)row * KB + cc * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto wstore = [&](int buf) {
+    _Float16* dst = sW + buf * BN * LW;
+#pragma unroll
+    for (int k = 0; k < W_CH; ++k) {
+      const int idx = tid + k * 256;
+      if (idx < BN * KB / 8) {
+        const int row = idx / (KB / 8), cc = idx % (KB / 8);
+        *reinterpret_cast<uint4*>(dst + row * LW + cc * 8) = rw[k];
+      }
+    }
+  };
+  auto stage_input = [&](int c) {
+    const int per_row = CK / 8;
+    for (int idx = tid; idx < nrows * per_row; idx += 256) {
+      const int row = idx / per_row, cc = idx % per_row;
+      const int gr = row_base + row;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gr >= 0 && gr < a.T_in) {
+        v = *reinterpret_cast<const uint4*>(inb + (int64_t)gr * a.Cin + c * CK + cc * 8);
+        if (a.pre_act != ACT_NONE) {
+          _Float16* hv = reinterpret_cast<_Float16*>(&v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = (_Float16)act_rt(a.pre_act, (float)hv[j]);
+        }
+      }
+      *reinterpret_cast<uint4*>(sIn + row * LI + cc * 8) = v;
+    }
+  };
+
+  f32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int m = 0; m < WMT; ++m)
+#pragma unroll
+    for (int n = 0; n < WNT; ++n) acc[m][n] = zero_f32x4();
+
+  const int nkb = chunks * groups;
+  wload(0, 0);
+  wstore(0);
+  for (int kbi = 0; kbi < nkb; ++kbi) {
+    const int c = kbi / groups, g = kbi % groups;
+    if (g == 0) {
+      __syncthreads();  // previous chunk's input tile fully consumed
+      stage_input(c);
+    }
+    __syncthreads();    // input tile + weights[kbi&1] visible
+    if (kbi + 1 < nkb) wload((kbi + 1) / groups, (kbi + 1) % groups);
+    const _Float16* w_cur = sW + (kbi & 1) * BN * LW;
+#pragma unroll
+    for (int ks = 0; ks < KB / 32; ++ks) {
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const int tap = g * TPG + kk / CK;
+      const int ci = kk % CK;
+      const bool tap_ok = tap < a.taps;
+      const int lrow_off = tap * a.dil - lo_tap;
+      half8 av[WMT], bv[WNT];
+#pragma unroll
+      for (int m = 0; m < WMT; ++m) {
+        const int r = wm * WMT * 16 + m * 16 + (lane & 15);
+        av[m] = tap_ok ? *reinterpret_cast<const half8*>(sIn + (r * a.in_stride + lrow_off) * LI + ci)
+                       : zero_half8();
+      }
+#pragma unroll
+      for (int n = 0; n < WNT; ++n)
+        bv[n] = *reinterpret_cast<const half8*>(w_cur + (wn * WNT * 16 + n * 16 + (lane & 15)) * LW + kk);
+#pragma unroll
+      for (int m = 0; m < WMT; ++m)
+#pragma unroll
+        for (int n = 0; n < WNT; ++n) acc[m][n] = mfma16(av[m], bv[n], acc[m][n]);
+    }
+    if (kbi + 1 < nkb) wstore((kbi + 1) & 1);
+  }
+
+  // epilogue
+  _Float16* outb = a.out + (int64_t)b * a.out_bs;
+  const _Float16* resb = a.res ? a.res + (int64_t)b * a.res_bs : nullptr;
+#pragma unroll
+  for (int n = 0; n < WNT; ++n) {
+    const int co = co0 + wn * WNT * 16 + n * 16 + (lane & 15);
+    if (co >= a.Cout) continue;
+    const float bias = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+    for (int m = 0; m < WMT; ++m) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = r0 + wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + rr;
+        if (r >= a.n_rows) continue;
+        const int t = r * a.out_stride + a.out_off + ph;
+        if (t < 0 || t >= a.T_out) continue;
+        float v = act_rt(a.post_act, acc[m][n][rr] + bias);
+        const int64_t o = (int64_t)t * a.Cout + co;
+        if (resb) v += (float)resb[o];
+        v *= a.out_scale;
+        if (a.accumulate) v += (float)outb[o];
+        outb[o] = (_Float16)v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WMT, int WNT, int CK>
+static void conv_cfg(const ConvArgs& a, hipStream_t s) {
+  constexpr int LI = CK + 8, LW = kConvKB + 8;
+  const int rows_max = (BM - 1) * a.in_stride + std::abs((a.taps - 1) * a.dil) + 1;
+  const size_t lds = (size_t)rows_max * LI * 2 + 2 * (size_t)BN * LW * 2;
+  JANUS_CHECK(lds <= 160 * 1024, "conv: LDS tile too large (" + std::to_string(lds) + " B)");
+  const int blocks = (int)(cdiv(a.n_rows, BM) * cdiv(a.Cout, BN));
+  auto kern = conv_kernel<BM, BN, WMT, WNT, CK>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr_set = true;
+  }
+  kern<<<dim3(blocks, a.phases, a.B), 256, lds, s>>>(a, rows_max);
+  JANUS_LAUNCH_CHECK();
+}
+
+template <int BM, int BN, int WMT, int WNT>
+static void conv_ck(const ConvArgs& a, hipStream_t s) {
+  const ConvPack g = conv_pack_geometry(a.Cin, a.Cout, a.taps);
+  if (g.ck == 64) conv_cfg<BM, BN, WMT, WNT, 64>(a, s);
+  else if (g.ck == 32) conv_cfg<BM, BN, WMT, WNT, 32>(a, s);
+  else conv_cfg<BM, BN, WMT, WNT, 16>(a, s);
+}
+
+void conv_launch(const ConvArgs& a, hipStream_t s) {
+  JANUS_CHECK(a.Cin % 16 == 0, "conv: Cin must be a multiple of 16");
+  JANUS_CHECK(a.Cout % 16 == 0, "conv: Cout must be a multiple of 16");
+  JANUS_CHECK(a.in_stride >= 1 && a.taps >= 1 && a.phases >= 1, "conv: bad geometry");
+  if (a.B <= 0 || a.n_rows <= 0) return;
+  if (a.Cout >= 128) conv_ck<128, 128, 4, 4>(a, s);
+  else if (a.Cout == 64) conv_ck<256, 64, 4, 4>(a, s);
+  else if (a.Cout == 32) conv_ck<256, 32, 4, 2>(a, s);
+  else if (a.Cout == 16) conv_ck<256, 16, 4, 1>(a, s);
+  else throw Error("conv: unsupported Cout " + std::to_string(a.Cout));
+}
+
+}  // namespace janus

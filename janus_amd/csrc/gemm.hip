@@ -1,0 +1,149 @@
+// fp16 "NT" GEMM on MFMA (v_mfma_f32_16x16x32_f16, fp32 accumulate) with fused
+// epilogues, for the Whisper encoder/decoder projections:
+//   C[M,N] = epi( A[M,K] · W[N,K]^T + bias[N] )
+// A row-major (K contiguous), W in nn.Linear layout [out][in] (K contiguous), so both
+// operands feed MFMA fragments as 16-byte LDS reads with no transpose.
+// Epilogues: store fp16 | erf-GELU -> fp16 | fp32 residual add (x += ...) | store fp32.
+//
+// Tiling: BMxBNx64 block tile, 4 waves (each WMT x WNT 16x16 tiles), register-staged
+// double-buffered LDS (one barrier per 64-deep K step; next tile's global loads issued
+// before the current tile's MFMAs), rows padded by 16 B so the 16-lane ds_read_b128
+// groups are conflict-free, XCD-aware tile order (blocks sharing an A panel on one L2).
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+template <int BM, int BN, int WMT, int WNT, int EPI>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
+  constexpr int BK = 64, LS = BK + 8;  // LDS row stride in halves (144 B = 16 B * 9)
+  constexpr int WN = BN / (16 * WNT);
+  static_assert((BM / (16 * WMT)) * WN == 4, "4 waves per block");
+  constexpr int KC = BK / 8;                  // 16-byte chunks per tile row
+  constexpr int A_CH = BM * KC / 256, B_CH = BN * KC / 256;
+  static_assert(A_CH * 256 == BM * KC && B_CH * 256 == BN * KC, "tile/threads mismatch");
+  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (BM + BN) * LS];
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int row0 = bm * BM, col0 = bn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  uint4 ra[A_CH], rb[B_CH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < A_CH; ++c) {
+      const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
+      const int gr = row0 + r, gk = k0 + kc * 8;
+      ra[c] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(p.A + (int64_t)gr * p.lda + gk)
+                                 : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < B_CH; ++c) {
+      const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
+      const int gr = col0 + r, gk = k0 + kc * 8;
+      rb[c] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(p.W + (int64_t)gr * p.ldw + gk)
+                                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+    _Float16* sA = smem + buf * (BM + BN) * LS;
+    _Float16* sB = sA + BM * LS;
+#pragma unroll
+    for (int c = 0; c < A_CH; ++c) {
+      const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
+      *reinterpret_cast<uint4*>(sA + r * LS + kc * 8) = ra[c];
+    }
+#pragma unroll
+    for (int c = 0; c < B_CH; ++c) {
+      const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
+      *reinterpret_cast<uint4*>(sB + r * LS + kc * 8) = rb[c];
+    }
+  };
+
+  f32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int m = 0; m < WMT; ++m)
+#pragma unroll
+    for (int n = 0; n < WNT; ++n) acc[m][n] = zero_f32x4();
+
+  const int nk = (K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const _Float16* sA = smem + cur * (BM + BN) * LS;
+    const _Float16* sB = sA + BM * LS;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      half8 a[WMT], b[WNT];
+      const int ko = ks * 32 + 8 * (lane >> 4);
+#pragma unroll
+      for (int m = 0; m < WMT; ++m)
+        a[m] = *reinterpret_cast<const half8*>(sA + (wm * WMT * 16 + m * 16 + (lane & 15)) * LS + ko);
+#pragma unroll
+      for (int n = 0; n < WNT; ++n)
+        b[n] = *reinterpret_cast<const half8*>(sB + (wn * WNT * 16 + n * 16 + (lane & 15)) * LS + ko);
+#pragma unroll
+      for (int m = 0; m < WMT; ++m)
+#pragma unroll
+        for (int n = 0; n < WNT; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int n = 0; n < WNT; ++n) {
+    const int col = col0 + wn * WNT * 16 + n * 16 + (lane & 15);
+    if (col >= N) continue;
+    const float bv = p.bias ? p.bias[col] : 0.0f;
+#pragma unroll
+    for (int m = 0; m < WMT; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + r;
+        if (row >= M) continue;
+        float v = acc[m][n][r] + bv;
+        if constexpr (EPI == EPI_F16) {
+          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+        } else if constexpr (EPI == EPI_GELU_F16) {
+          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
+        } else if constexpr (EPI == EPI_RESID_F32) {
+          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col;
+          *c = p.R[(int64_t)row * p.ldr + col] + v;
+        } else {
+          static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WMT, int WNT>
+static void launch_cfg(int epi, const GemmArgs& p, hipStream_t s) {
+  const int blocks = (int)(cdiv(p.M, BM) * cdiv(p.N, BN));
+  switch (epi) {
+    case EPI_F16: gemm_nt_kernel<BM, BN, WMT, WNT, EPI_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_nt_kernel<BM, BN, WMT, WNT, EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_RESID_F32: gemm_nt_kernel<BM, BN, WMT, WNT, EPI_RESID_F32><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_F32: gemm_nt_kernel<BM, BN, WMT, WNT, EPI_F32><<<blocks, 256, 0, s>>>(p); break;
+    default: throw Error("bad gemm epilogue");
+  }
+  JANUS_LAUNCH_CHECK();
+}
+
+void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
+  JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
+  JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");
+  if (p.M <= 0 || p.N <= 0) return;
+  if (p.M <= 64) launch_cfg<64, 64, 4, 1>(epi, p, s);
+  else launch_cfg<128, 128, 4, 4>(epi, p, s);
+}
+
+}  // namespace janus

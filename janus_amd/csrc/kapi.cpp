@@ -1,0 +1,94 @@
+// Kernel-level C-ABI (include/janus_kernels.h): thin wrappers over the launchers.
+#include "kernels.h"
+#include "../../include/janus_kernels.h"
+
+namespace janus {
+
+// Shared by janus_conv1d_f16 and the vocoder: PyTorch conv hyper-parameters ->
+// the implicit-GEMM row mapping of ConvArgs.
+ConvArgs conv_args_torch(const _Float16* in, int B, int T_in, int Cin, const _Float16* packed,
+                         const float* bias, _Float16* out, int T_out, int Cout, int taps,
+                         int stride, int padding, int dilation, int transposed, int pre_act,
+                         int post_act, const _Float16* res, int64_t res_bs, float scale,
+                         int accumulate) {
+  ConvArgs a{};
+  a.in = in; a.in_bs = (int64_t)T_in * Cin; a.T_in = T_in; a.Cin = Cin;
+  a.w = packed; a.bias = bias;
+  a.out = out; a.out_bs = (int64_t)T_out * Cout; a.T_out = T_out; a.Cout = Cout;
+  a.res = res; a.res_bs = res_bs;
+  a.pre_act = pre_act; a.post_act = post_act; a.out_scale = scale; a.accumulate = accumulate;
+  a.B = B;
+  if (!transposed) {
+    a.taps = taps; a.dil = dilation; a.in_stride = stride; a.in_off = -padding;
+    a.out_stride = 1; a.out_off = 0; a.n_rows = T_out; a.phases = 1;
+  } else {
+    // ConvTranspose1d(k = 2u, stride u, padding p): output t = q*u + ph - p reads input
+    // rows q (kernel index ph) and q-1 (kernel index ph+u).
+    const int u = stride;
+    a.taps = 2; a.dil = -1; a.in_stride = 1; a.in_off = 0;
+    a.out_stride = u; a.out_off = -padding; a.phases = u;
+    a.n_rows = (T_out + padding) / u + 1;
+  }
+  return a;
+}
+
+}  // namespace janus
+
+using namespace janus;
+
+extern "C" int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W,
+                              int64_t ldw, const float* bias, void* C, int64_t ldc, const float* R,
+                              int64_t ldr, int M, int N, int K, void* stream) {
+  return guarded([&] {
+    GemmArgs g;
+    g.A = reinterpret_cast<const _Float16*>(A); g.lda = lda;
+    g.W = reinterpret_cast<const _Float16*>(W); g.ldw = ldw;
+    g.bias = bias; g.C = C; g.ldc = ldc; g.R = R; g.ldr = ldr; g.M = M; g.N = N; g.K = K;
+    gemm_launch(epi, g, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_layernorm_f16(const float* x, const float* gamma, const float* beta,
+                                   uint16_t* out, int rows, int d, float eps, void* stream) {
+  return guarded([&] {
+    layernorm_launch(x, gamma, beta, reinterpret_cast<_Float16*>(out), rows, d, eps,
+                     (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_attention_f16(const uint16_t* qkv, uint16_t* out, int batch, int T, int H,
+                                   float scale, void* stream) {
+  return guarded([&] {
+    attention_launch(reinterpret_cast<const _Float16*>(qkv), reinterpret_cast<_Float16*>(out),
+                     batch, T, H, scale, (hipStream_t)stream);
+  });
+}
+
+extern "C" int64_t janus_conv1d_packed_size(int Cin, int Cout, int taps, int transposed,
+                                            int stride) {
+  const ConvPack g = conv_pack_geometry(Cin, Cout, transposed ? 2 : taps);
+  return g.phase_elems * (transposed ? stride : 1);
+}
+
+extern "C" int janus_conv1d_pack(const float* w, uint16_t* packed, int Cin, int Cout, int taps,
+                                 int transposed, int stride, void* stream) {
+  return guarded([&] {
+    conv_pack_weights(w, reinterpret_cast<_Float16*>(packed), Cin, Cout, taps, transposed, stride,
+                      (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_conv1d_f16(const uint16_t* in, int batch, int T_in, int Cin,
+                                const uint16_t* packed, const float* bias, uint16_t* out, int T_out,
+                                int Cout, int taps, int stride, int padding, int dilation,
+                                int transposed, int pre_act, int post_act, const uint16_t* res,
+                                int64_t res_bs, float scale, int accumulate, void* stream) {
+  return guarded([&] {
+    ConvArgs a = conv_args_torch(
+        reinterpret_cast<const _Float16*>(in), batch, T_in, Cin,
+        reinterpret_cast<const _Float16*>(packed), bias, reinterpret_cast<_Float16*>(out), T_out,
+        Cout, taps, stride, padding, dilation, transposed, pre_act, post_act,
+        reinterpret_cast<const _Float16*>(res), res_bs, scale, accumulate);
+    conv_launch(a, (hipStream_t)stream);
+  });
+}

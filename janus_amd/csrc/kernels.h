@@ -1,0 +1,75 @@
+// Launcher declarations shared by the host-side orchestration (whisper.cpp, vocoder.cpp).
+#pragma once
+#include "common.h"
+
+namespace janus {
+
+// ------------------------------------------------------------------ GEMM
+enum GemmEpi { EPI_F16 = 0, EPI_GELU_F16 = 1, EPI_RESID_F32 = 2, EPI_F32 = 3 };
+
+struct GemmArgs {
+  const _Float16* A; int64_t lda;  // [M][K]
+  const _Float16* W; int64_t ldw;  // [N][K]
+  const float* bias;               // [N] or null
+  void* C; int64_t ldc;            // fp16 or fp32 by epilogue
+  const float* R; int64_t ldr;     // fp32 residual (EPI_RESID_F32), may alias C
+  int M, N, K;
+};
+void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
+
+// ------------------------------------------------------------- LayerNorm
+// out[r][:] = fp16( (x[r]-mean)/sqrt(var+eps) * g + b ), x fp32 [rows][d]
+void layernorm_launch(const float* x, const float* g, const float* b, _Float16* out, int rows,
+                      int d, float eps, hipStream_t s);
+// fp32 out variant (final encoder LN keeps fp32 for the cross-attention K/V GEMMs' input)
+void layernorm_f32_launch(const float* x, const float* g, const float* b, float* out, int rows,
+                          int d, float eps, hipStream_t s);
+
+// ------------------------------------------------------------ attention
+// Encoder self-attention over T positions, head_dim 64. qkv fp16 [B*T][3*d]
+// (q | k | v, head h at columns h*64), out fp16 [B*T][d].
+void attention_launch(const _Float16* qkv, _Float16* out, int B, int T, int H, float scale,
+                      hipStream_t s);
+// One query per (b, h) against Tkv cached keys (decoder self/cross attention).
+// q[b*q_bs + h*64 + d]; k/v[b*kv_bs + t*kv_rs + h*64 + d]; out[b*o_bs + h*64 + d].
+// tkv: device int32 per batch row (NULL => Tkv for all).
+void decode_attention_launch(const _Float16* q, int64_t q_bs, const _Float16* k, const _Float16* v,
+                             int64_t kv_bs, int64_t kv_rs, int Tkv, const int32_t* tkv,
+                             _Float16* out, int64_t o_bs, int B, int H, float scale,
+                             hipStream_t s);
+
+// ----------------------------------------------------------------- conv
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
+
+// Implicit-GEMM 1-D convolution on MFMA, time-major [B][T][C] fp16 activations.
+// For output row r (0 <= r < n_rows) of phase ph, tap j reads input row
+//   r*in_stride + j*dil + in_off            (zero outside [0, T_in))
+// and writes output time  r*out_stride + out_off + ph  (skipped outside [0, T_out)).
+// Weights are pre-packed by conv_pack_weights (blocked [ph][chunk][group][Cout][KB]).
+struct ConvArgs {
+  const _Float16* in; int64_t in_bs; int T_in; int Cin;
+  const _Float16* w; const float* bias;
+  _Float16* out; int64_t out_bs; int T_out; int Cout;
+  const _Float16* res; int64_t res_bs;  // added after post_act (fp16, [B][T_out][Cout]); may be null
+  int taps, dil, in_stride, in_off, out_stride, out_off, n_rows, phases;
+  int pre_act, post_act;
+  float out_scale; int accumulate;      // out = (accumulate ? out : 0) + out_scale * y
+  int B;
+};
+struct ConvPack { int ck, kb, chunks, groups; int64_t phase_elems; };
+ConvPack conv_pack_geometry(int Cin, int Cout, int taps);
+// Pack fp32 PyTorch weights into the blocked fp16 layout (device pointers).
+//   transposed=0: w is Conv1d [Cout][Cin][taps], phases=1
+//   transposed=1: w is ConvTranspose1d [Cin][Cout][2u] (stride u): phases=u, 2 taps/phase
+void conv_pack_weights(const float* w, _Float16* packed, int Cin, int Cout, int taps,
+                       int transposed, int u, hipStream_t s);
+void conv_launch(const ConvArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ mel
+void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* basis,
+                const float* filters, float* logmel, uint32_t* maxkey, int n_frames_out,
+                int decim, hipStream_t s);
+void mel_normalize_launch(const float* logmel, const uint32_t* maxkey, _Float16* out, int B,
+                          int frames, int n_mels, int out_ld, hipStream_t s);
+
+}  // namespace janus

@@ -1,0 +1,45 @@
+// MFMA fragment helpers for gfx950 (CDNA4): v_mfma_f32_16x16x32_f16.
+//
+// Lane maps (cdna_hip_programming.md §3): lane l holds A[row l&15][k 8(l>>4)+j] and
+// B[k 8(l>>4)+j][col l&15], j = 0..7 (16 B per lane); C/D: col l&15,
+// row 4(l>>4)+r, r = 0..3.
+#pragma once
+#include "common.h"
+
+namespace janus {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(const half8& a, const half8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ half8 zero_half8() {
+  half8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (_Float16)0.0f;
+  return z;
+}
+
+__device__ __forceinline__ f32x4 zero_f32x4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// XCD-aware remap of a 1-D block index (bijective; MI355X deals blocks round-robin
+// over 8 XCDs, so consecutive logical tiles are placed on one XCD's L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  constexpr int kXcd = 8;
+  if (nblocks < kXcd) return bid;
+  const int q = nblocks / kXcd, r = nblocks % kXcd;
+  const int xcd = bid % kXcd, idx = bid / kXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace janus

@@ -1,0 +1,84 @@
+// LayerNorm over the fp32 residual stream (Whisper pre-LN blocks, eps 1e-5), one
+// wavefront per row; two-pass mean/variance from registers, wave-shuffle reductions,
+// 16-byte loads/stores. HBM-bound: 4·d B read + 2·d B written per row.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+template <int MAXV, bool F32OUT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ b, void* out,
+                                                        int rows, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = d / 4;
+  const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * d);
+  float4 v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int i = lane + k * 64;
+    v[k] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += v[k].x + v[k].y + v[k].z + v[k].w;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int i = lane + k * 64;
+    if (i < nv) {
+      const float a = v[k].x - mean, bb = v[k].y - mean, c = v[k].z - mean, e = v[k].w - mean;
+      q += a * a + bb * bb + c * c + e * e;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q / d + eps);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int i = lane + k * 64;
+    if (i >= nv) continue;
+    const float4 gg = g4[i], bb = b4[i];
+    float4 y;
+    y.x = (v[k].x - mean) * rstd * gg.x + bb.x;
+    y.y = (v[k].y - mean) * rstd * gg.y + bb.y;
+    y.z = (v[k].z - mean) * rstd * gg.z + bb.z;
+    y.w = (v[k].w - mean) * rstd * gg.w + bb.w;
+    if constexpr (F32OUT) {
+      reinterpret_cast<float4*>(static_cast<float*>(out) + (int64_t)row * d)[i] = y;
+    } else {
+      half4 h = {(_Float16)y.x, (_Float16)y.y, (_Float16)y.z, (_Float16)y.w};
+      reinterpret_cast<half4*>(static_cast<_Float16*>(out) + (int64_t)row * d)[i] = h;
+    }
+  }
+}
+
+template <bool F32OUT>
+static void ln_dispatch(const float* x, const float* g, const float* b, void* out, int rows, int d,
+                        float eps, hipStream_t s) {
+  JANUS_CHECK(d % 4 == 0 && d <= 2048, "layernorm: d must be a multiple of 4 and <= 2048");
+  if (rows <= 0) return;
+  const int grid = (rows + 3) / 4;
+  if (d <= 256) layernorm_kernel<1, F32OUT><<<grid, 256, 0, s>>>(x, g, b, out, rows, d, eps);
+  else if (d <= 512) layernorm_kernel<2, F32OUT><<<grid, 256, 0, s>>>(x, g, b, out, rows, d, eps);
+  else if (d <= 1024) layernorm_kernel<4, F32OUT><<<grid, 256, 0, s>>>(x, g, b, out, rows, d, eps);
+  else layernorm_kernel<8, F32OUT><<<grid, 256, 0, s>>>(x, g, b, out, rows, d, eps);
+  JANUS_LAUNCH_CHECK();
+}
+
+void layernorm_launch(const float* x, const float* g, const float* b, _Float16* out, int rows,
+                      int d, float eps, hipStream_t s) {
+  ln_dispatch<false>(x, g, b, out, rows, d, eps, s);
+}
+
+void layernorm_f32_launch(const float* x, const float* g, const float* b, float* out, int rows,
+                          int d, float eps, hipStream_t s) {
+  ln_dispatch<true>(x, g, b, out, rows, d, eps, s);
+}
+
+}  // namespace janus

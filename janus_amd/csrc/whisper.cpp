@@ -1,0 +1,379 @@
+// Whisper STT on gfx950: log-mel -> encoder -> batched greedy decoder.
+//
+// Replaces faster-whisper's WhisperModel (CTranslate2, int8 on CPU) as driven by
+// Transcriber.transcribe_buffer (backend/services/transcriber.py:29-64):
+// model.transcribe(audio[::3], beam_size=1, language='en') for one 30 s window.
+// Weights arrive by name (HF Whisper checkpoint naming) as fp32 and are re-laid out
+// on the device: fused fp16 QKV, packed conv weights, fp16 embeddings; the residual
+// stream stays fp32, GEMM/attention operands are fp16 on MFMA with fp32 accumulation.
+#include <mutex>
+#include <cstring>
+#include "devmem.h"
+#include "kernels.h"
+#include "decoder.h"
+#include "../../include/janus.h"
+
+namespace janus {
+
+struct EncLayer {
+  DevMem wqkv, bqkv, wo, w1, w2;  // fp16 weights / fp32 fused bias
+  const float *bo, *b1, *b2, *ln1g, *ln1b, *ln2g, *ln2b;
+};
+struct DecLayer {
+  DevMem wqkv, bqkv, wo, wq_c, wk_c, wv_c, wo_c, w1, w2;
+  const float *bo, *bq_c, *bv_c, *bo_c, *b1, *b2;
+  const float *ln1g, *ln1b, *ln2g, *ln2b, *ln3g, *ln3b;
+};
+
+}  // namespace janus
+
+struct janus_whisper {
+  janus_whisper_config cfg;
+  janus::ParamStore params;
+  bool prepared = false;
+  std::mutex mu;
+  // device-side prepared weights
+  janus::DevMem conv1p, conv2p, pos16, tok16;
+  std::vector<janus::EncLayer> enc;
+  std::vector<janus::DecLayer> dec;
+  // workspaces
+  janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
+  janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
+      d_done, d_prompt, d_supp, d_ntok_scratch;
+};
+
+namespace janus {
+
+static _Float16* to_f16(const float* src, int64_t n, DevMem& dst, hipStream_t s) {
+  dst.ensure(sizeof(_Float16) * n);
+  cast_f32_f16_launch(src, dst.as<_Float16>(), n, s);
+  return dst.as<_Float16>();
+}
+
+// concat rows of fp32 matrices into one fp16 matrix (missing name => zeros)
+static void fuse_f16(const ParamStore& P, const std::vector<std::string>& names, int64_t each,
+                     DevMem& dst, hipStream_t s) {
+  dst.ensure(sizeof(_Float16) * each * names.size());
+  for (size_t i = 0; i < names.size(); ++i) {
+    _Float16* d = dst.as<_Float16>() + i * each;
+    if (P.has(names[i])) cast_f32_f16_launch(P.get(names[i], each), d, each, s);
+    else JANUS_HIP(hipMemsetAsync(d, 0, sizeof(_Float16) * each, s));
+  }
+}
+
+static void fuse_f32(const ParamStore& P, const std::vector<std::string>& names, int64_t each,
+                     DevMem& dst, hipStream_t s) {
+  dst.ensure(sizeof(float) * each * names.size());
+  for (size_t i = 0; i < names.size(); ++i) {
+    float* d = dst.as<float>() + i * each;
+    if (P.has(names[i]))
+      JANUS_HIP(hipMemcpyAsync(d, P.get(names[i], each), sizeof(float) * each,
+                               hipMemcpyDeviceToDevice, s));
+    else JANUS_HIP(hipMemsetAsync(d, 0, sizeof(float) * each, s));
+  }
+}
+
+static void prepare(janus_whisper* w, hipStream_t s) {
+  if (w->prepared) return;
+  const auto& c = w->cfg;
+  const int d = c.d_model, ff = 4 * d;
+  const ParamStore& P = w->params;
+  auto pk = [&](const std::string& name, int cin, DevMem& dst) {
+    const float* src = P.get(name, (int64_t)d * cin * 3);
+    const ConvPack g = conv_pack_geometry(cin, d, 3);
+    dst.ensure(sizeof(_Float16) * g.phase_elems);
+    conv_pack_weights(src, dst.as<_Float16>(), cin, d, 3, 0, 1, s);
+  };
+  pk("encoder.conv1.weight", c.n_mels, w->conv1p);
+  pk("encoder.conv2.weight", d, w->conv2p);
+  to_f16(P.get("encoder.embed_positions.weight", (int64_t)c.n_audio_ctx * d),
+         (int64_t)c.n_audio_ctx * d, w->pos16, s);
+  to_f16(P.get("decoder.embed_tokens.weight", (int64_t)c.n_vocab * d), (int64_t)c.n_vocab * d,
+         w->tok16, s);
+  const int64_t dd = (int64_t)d * d, fd = (int64_t)ff * d;
+  w->enc.clear();
+  w->enc.resize(c.enc_layers);
+  for (int l = 0; l < c.enc_layers; ++l) {
+    const std::string p = "encoder.layers." + std::to_string(l) + ".";
+    EncLayer& L = w->enc[l];
+    fuse_f16(P, {p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"}, dd, L.wqkv, s);
+    fuse_f32(P, {p + "self_attn.q_proj.bias", p + "self_attn.k_proj.bias", p + "self_attn.v_proj.bias"}, d, L.bqkv, s);
+    to_f16(P.get(p + "self_attn.out_proj.weight", dd), dd, L.wo, s);
+    to_f16(P.get(p + "fc1.weight", fd), fd, L.w1, s);
+    to_f16(P.get(p + "fc2.weight", fd), fd, L.w2, s);
+    L.bo = P.get(p + "self_attn.out_proj.bias", d);
+    L.b1 = P.get(p + "fc1.bias", ff);
+    L.b2 = P.get(p + "fc2.bias", d);
+    L.ln1g = P.get(p + "self_attn_layer_norm.weight", d);
+    L.ln1b = P.get(p + "self_attn_layer_norm.bias", d);
+    L.ln2g = P.get(p + "final_layer_norm.weight", d);
+    L.ln2b = P.get(p + "final_layer_norm.bias", d);
+  }
+  w->dec.clear();
+  w->dec.resize(c.dec_layers);
+  for (int l = 0; l < c.dec_layers; ++l) {
+    const std::string p = "decoder.layers." + std::to_string(l) + ".";
+    DecLayer& L = w->dec[l];
+    fuse_f16(P, {p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"}, dd, L.wqkv, s);
+    fuse_f32(P, {p + "self_attn.q_proj.bias", p + "self_attn.k_proj.bias", p + "self_attn.v_proj.bias"}, d, L.bqkv, s);
+    to_f16(P.get(p + "self_attn.out_proj.weight", dd), dd, L.wo, s);
+    to_f16(P.get(p + "encoder_attn.q_proj.weight", dd), dd, L.wq_c, s);
+    to_f16(P.get(p + "encoder_attn.k_proj.weight", dd), dd, L.wk_c, s);
+    to_f16(P.get(p + "encoder_attn.v_proj.weight", dd), dd, L.wv_c, s);
+    to_f16(P.get(p + "encoder_attn.out_proj.weight", dd), dd, L.wo_c, s);
+    to_f16(P.get(p + "fc1.weight", fd), fd, L.w1, s);
+    to_f16(P.get(p + "fc2.weight", fd), fd, L.w2, s);
+    L.bo = P.get(p + "self_attn.out_proj.bias", d);
+    L.bq_c = P.get(p + "encoder_attn.q_proj.bias", d);
+    L.bv_c = P.get(p + "encoder_attn.v_proj.bias", d);
+    L.bo_c = P.get(p + "encoder_attn.out_proj.bias", d);
+    L.b1 = P.get(p + "fc1.bias", ff);
+    L.b2 = P.get(p + "fc2.bias", d);
+    L.ln1g = P.get(p + "self_attn_layer_norm.weight", d);
+    L.ln1b = P.get(p + "self_attn_layer_norm.bias", d);
+    L.ln2g = P.get(p + "encoder_attn_layer_norm.weight", d);
+    L.ln2b = P.get(p + "encoder_attn_layer_norm.bias", d);
+    L.ln3g = P.get(p + "final_layer_norm.weight", d);
+    L.ln3b = P.get(p + "final_layer_norm.bias", d);
+  }
+  JANUS_HIP(hipStreamSynchronize(s));
+  w->prepared = true;
+}
+
+static GemmArgs gargs(const _Float16* A, int64_t lda, const _Float16* W, int64_t ldw,
+                      const float* bias, void* C, int64_t ldc, int M, int N, int K,
+                      const float* R = nullptr, int64_t ldr = 0) {
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.C = C; g.ldc = ldc;
+  g.R = R; g.ldr = ldr; g.M = M; g.N = N; g.K = K;
+  return g;
+}
+
+static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, hipStream_t s) {
+  const auto& c = w->cfg;
+  const int d = c.d_model, H = c.n_heads, Tm = 2 * c.n_audio_ctx, Te = c.n_audio_ctx;
+  const int64_t M = (int64_t)B * Te;
+  JANUS_CHECK(M < (1ll << 31), "encode: batch too large");
+  w->ws_x1.ensure(sizeof(_Float16) * B * Tm * d);
+  w->ws_x2.ensure(sizeof(_Float16) * M * d);
+  w->ws_r.ensure(sizeof(float) * M * d);
+  w->ws_a.ensure(sizeof(_Float16) * M * d);
+  w->ws_qkv.ensure(sizeof(_Float16) * M * 3 * d);
+  w->ws_o.ensure(sizeof(_Float16) * M * d);
+  w->ws_f.ensure(sizeof(_Float16) * M * 4 * d);
+  _Float16 *x1 = w->ws_x1.as<_Float16>(), *x2 = w->ws_x2.as<_Float16>();
+  float* r = w->ws_r.as<float>();
+  _Float16 *a = w->ws_a.as<_Float16>(), *qkv = w->ws_qkv.as<_Float16>(), *o = w->ws_o.as<_Float16>(),
+           *f = w->ws_f.as<_Float16>();
+
+  ConvArgs ca{};
+  ca.in = mel; ca.in_bs = (int64_t)Tm * c.n_mels; ca.T_in = Tm; ca.Cin = c.n_mels;
+  ca.w = w->conv1p.as<_Float16>(); ca.bias = w->params.get("encoder.conv1.bias", d);
+  ca.out = x1; ca.out_bs = (int64_t)Tm * d; ca.T_out = Tm; ca.Cout = d;
+  ca.res = nullptr; ca.res_bs = 0;
+  ca.taps = 3; ca.dil = 1; ca.in_stride = 1; ca.in_off = -1; ca.out_stride = 1; ca.out_off = 0;
+  ca.n_rows = Tm; ca.phases = 1; ca.pre_act = ACT_NONE; ca.post_act = ACT_GELU;
+  ca.out_scale = 1.0f; ca.accumulate = 0; ca.B = B;
+  conv_launch(ca, s);
+  ConvArgs cb = ca;
+  cb.in = x1; cb.in_bs = (int64_t)Tm * d; cb.T_in = Tm; cb.Cin = d;
+  cb.w = w->conv2p.as<_Float16>(); cb.bias = w->params.get("encoder.conv2.bias", d);
+  cb.out = x2; cb.out_bs = (int64_t)Te * d; cb.T_out = Te; cb.n_rows = Te; cb.in_stride = 2;
+  cb.res = w->pos16.as<_Float16>(); cb.res_bs = 0;
+  conv_launch(cb, s);
+  cast_f16_f32_launch(x2, r, M * d, s);
+
+  const float scale = 0.125f;  // head_dim 64 ** -0.5
+  for (int l = 0; l < c.enc_layers; ++l) {
+    EncLayer& L = w->enc[l];
+    layernorm_launch(r, L.ln1g, L.ln1b, a, (int)M, d, 1e-5f, s);
+    gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, (int)M, 3 * d, d), s);
+    attention_launch(qkv, o, B, Te, H, scale, s);
+    gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, r, d, (int)M, d, d, r, d), s);
+    layernorm_launch(r, L.ln2g, L.ln2b, a, (int)M, d, 1e-5f, s);
+    gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, (int)M, 4 * d, d), s);
+    gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, r, d, (int)M, d, 4 * d, r, d), s);
+  }
+  layernorm_launch(r, w->params.get("encoder.layer_norm.weight", d),
+                   w->params.get("encoder.layer_norm.bias", d), out, (int)M, d, 1e-5f, s);
+}
+
+static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const janus_decode_options* opt,
+                          int32_t* tokens, int32_t* n_tokens, float* sum_lp, hipStream_t s) {
+  const auto& c = w->cfg;
+  const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
+  const int maxlen = opt->max_length;
+  JANUS_CHECK(opt->prompt_len >= 1 && opt->prompt_len < maxlen && maxlen <= NC,
+              "decode: need 1 <= prompt_len < max_length <= n_text_ctx");
+  const int64_t Me = (int64_t)B * Te;
+  const int nl = c.dec_layers;
+  w->d_x.ensure(sizeof(float) * B * d);
+  w->d_a.ensure(sizeof(_Float16) * B * d);
+  w->d_qkv.ensure(sizeof(_Float16) * B * 3 * d);
+  w->d_o.ensure(sizeof(_Float16) * B * d);
+  w->d_q2.ensure(sizeof(_Float16) * B * d);
+  w->d_f.ensure(sizeof(_Float16) * B * 4 * d);
+  w->d_logits.ensure(sizeof(float) * (int64_t)B * V);
+  w->d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
+  w->d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
+  w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+  w->d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+  w->d_smask.ensure(V);
+  w->d_done.ensure(sizeof(int32_t) * B);
+  w->d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
+  w->d_supp.ensure(sizeof(int32_t) * (opt->n_suppress > 0 ? opt->n_suppress : 1));
+  float* x = w->d_x.as<float>();
+  _Float16 *a = w->d_a.as<_Float16>(), *qkv = w->d_qkv.as<_Float16>(), *o = w->d_o.as<_Float16>(),
+           *q2 = w->d_q2.as<_Float16>(), *f = w->d_f.as<_Float16>();
+  float* logits = w->d_logits.as<float>();
+  int32_t* done = w->d_done.as<int32_t>();
+
+  JANUS_HIP(hipMemcpyAsync(w->d_prompt.p, opt->prompt, sizeof(int32_t) * opt->prompt_len,
+                           hipMemcpyHostToDevice, s));
+  if (opt->n_suppress > 0)
+    JANUS_HIP(hipMemcpyAsync(w->d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
+                             hipMemcpyHostToDevice, s));
+  build_mask_launch(w->d_supp.as<int32_t>(), opt->n_suppress, w->d_smask.as<uint8_t>(), V, s);
+  init_tokens_launch(tokens, maxlen, w->d_prompt.as<int32_t>(), opt->prompt_len, done, sum_lp,
+                     n_tokens, B, s);
+
+  // cross-attention keys/values, once per window
+  for (int l = 0; l < nl; ++l) {
+    DecLayer& L = w->dec[l];
+    _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
+    _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
+    gemm_launch(EPI_F16, gargs(enc, d, L.wk_c.as<_Float16>(), d, nullptr, ck, d, (int)Me, d, d), s);
+    gemm_launch(EPI_F16, gargs(enc, d, L.wv_c.as<_Float16>(), d, L.bv_c, cv, d, (int)Me, d, d), s);
+  }
+
+  DecodeRules R;
+  R.eot = opt->eot;
+  R.suppress_blank = opt->suppress_blank;
+  R.blank = opt->blank_token;
+  R.ts_begin = opt->timestamp_begin;
+  R.no_timestamps = opt->no_timestamps;
+  R.max_initial_ts = opt->max_initial_timestamp_index;
+  const float scale = 0.125f;
+  const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
+  std::vector<int32_t> h_done(B);
+  const int sample_begin = opt->prompt_len;  // index of the first sampled token
+  for (int pos = 0; pos + 1 < maxlen; ++pos) {
+    embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x, B, s);
+    for (int l = 0; l < nl; ++l) {
+      DecLayer& L = w->dec[l];
+      _Float16* kc = w->d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
+      _Float16* vc = w->d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
+      _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
+      _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
+      layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
+      gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
+      kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
+      decode_attention_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, nullptr, o, d, B, H, scale, s);
+      gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, x, d, B, d, d, x, d), s);
+      layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+      gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+      decode_attention_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, nullptr, o, d, B, H, scale, s);
+      gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo_c.as<_Float16>(), d, L.bo_c, x, d, B, d, d, x, d), s);
+      layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+      gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
+      gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, x, d, B, d, 4 * d, x, d), s);
+    }
+    if (pos + 1 < sample_begin) continue;  // still inside the prompt
+    layernorm_launch(x, w->params.get("decoder.layer_norm.weight", d),
+                     w->params.get("decoder.layer_norm.bias", d), a, B, d, 1e-5f, s);
+    gemm_launch(EPI_F32, gargs(a, d, w->tok16.as<_Float16>(), d, nullptr, logits, V, B, V, d), s);
+    select_launch(logits, V, R, w->d_smask.as<uint8_t>(), tokens, maxlen, pos, sample_begin, done,
+                  sum_lp, n_tokens, B, s);
+    if (opt->check_every > 0 && ((pos + 1 - sample_begin) % opt->check_every) == opt->check_every - 1) {
+      JANUS_HIP(hipMemcpyAsync(h_done.data(), done, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+      JANUS_HIP(hipStreamSynchronize(s));
+      bool all = true;
+      for (int b = 0; b < B; ++b) all = all && h_done[b];
+      if (all) {
+        // remaining positions stay eot-free (-1); callers stop at the first eot
+        break;
+      }
+    }
+  }
+}
+
+}  // namespace janus
+
+using namespace janus;
+
+extern "C" int janus_whisper_create(const janus_whisper_config* cfg, janus_whisper** out) {
+  return guarded([&] {
+    JANUS_CHECK(cfg && out, "null argument");
+    JANUS_CHECK(cfg->d_model % 64 == 0 && cfg->n_heads * 64 == cfg->d_model,
+                "whisper: head_dim must be 64");
+    JANUS_CHECK(cfg->n_mels == 80, "whisper: 80 mel bins supported");
+    auto* w = new janus_whisper();
+    w->cfg = *cfg;
+    *out = w;
+  });
+}
+
+extern "C" int janus_whisper_destroy(janus_whisper* w) {
+  return guarded([&] {
+    if (w) {
+      (void)hipDeviceSynchronize();
+      delete w;
+    }
+  });
+}
+
+extern "C" int janus_whisper_set_tensor(janus_whisper* w, const char* name, const float* host,
+                                        int64_t numel) {
+  return guarded([&] {
+    JANUS_CHECK(w && name && host && numel > 0, "bad argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->params.set(name, host, numel);
+    w->prepared = false;
+  });
+}
+
+extern "C" int janus_whisper_logmel(janus_whisper* w, const float* pcm, const int64_t* offsets,
+                                    int batch, int decim, float* logmel, uint16_t* mel,
+                                    void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(w && pcm && offsets && mel, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    hipStream_t s = (hipStream_t)stream;
+    const int frames = 2 * w->cfg.n_audio_ctx;
+    float* lm = logmel;
+    if (!lm) {
+      w->ws_logmel.ensure(sizeof(float) * (int64_t)batch * frames * 80);
+      lm = w->ws_logmel.as<float>();
+    }
+    w->ws_maxkey.ensure(sizeof(uint32_t) * (batch > 0 ? batch : 1));
+    mel_launch(pcm, offsets, batch, w->params.get("mel.basis", 400 * 416),
+               w->params.get("mel.filters", 208 * 80), lm, w->ws_maxkey.as<uint32_t>(), frames,
+               decim, s);
+    mel_normalize_launch(lm, w->ws_maxkey.as<uint32_t>(), reinterpret_cast<_Float16*>(mel), batch,
+                         frames, 80, 80, s);
+  });
+}
+
+extern "C" int janus_whisper_encode(janus_whisper* w, const uint16_t* mel, int batch, uint16_t* enc,
+                                    void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(w && mel && enc, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    hipStream_t s = (hipStream_t)stream;
+    prepare(w, s);
+    encode(w, reinterpret_cast<const _Float16*>(mel), batch, reinterpret_cast<_Float16*>(enc), s);
+  });
+}
+
+extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc, int batch,
+                                           const janus_decode_options* opt, int32_t* tokens,
+                                           int32_t* n_tokens, float* sum_logprob, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(w && enc && opt && tokens && n_tokens && sum_logprob, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    hipStream_t s = (hipStream_t)stream;
+    prepare(w, s);
+    decode_greedy(w, reinterpret_cast<const _Float16*>(enc), batch, opt, tokens, n_tokens,
+                  sum_logprob, s);
+  });
+}

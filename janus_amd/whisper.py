@@ -1,0 +1,262 @@
+"""Whisper model host side: configs, weights, front-end constants and the GPU engine.
+
+The engine owns one ``janus_whisper`` context (include/janus.h) and calls
+``janus_whisper_logmel`` -> ``janus_whisper_encode`` -> ``janus_whisper_decode_greedy``
+on torch-allocated device buffers and torch's current stream.
+
+Weights: if ``JANUS_WHISPER_DIR`` points at a Hugging Face Whisper checkpoint
+(``model.safetensors``), it is loaded (safetensors, no pickle). Otherwise the model has
+seeded synthetic weights of the real shapes (no checkpoints are reachable offline).
+"""
+import ctypes
+import dataclasses
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from . import tokenizer as tok
+
+
+@dataclasses.dataclass(frozen=True)
+class WhisperConfig:
+    name: str
+    d_model: int
+    n_heads: int
+    enc_layers: int
+    dec_layers: int
+    n_mels: int = 80
+    n_audio_ctx: int = 1500
+    n_vocab: int = tok.N_VOCAB_EN
+    n_text_ctx: int = 448
+
+    @property
+    def ffn(self):
+        return 4 * self.d_model
+
+
+CONFIGS = {
+    "tiny.en": WhisperConfig("tiny.en", 384, 6, 4, 4),
+    "base.en": WhisperConfig("base.en", 512, 8, 6, 6),
+    "small.en": WhisperConfig("small.en", 768, 12, 12, 12),
+}
+
+
+class janus_whisper_config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("n_mels", "n_audio_ctx", "d_model", "n_heads",
+                                            "enc_layers", "dec_layers", "n_vocab", "n_text_ctx")]
+
+
+class janus_decode_options(ctypes.Structure):
+    _fields_ = [("prompt", ctypes.POINTER(ctypes.c_int32)), ("prompt_len", ctypes.c_int),
+                ("max_length", ctypes.c_int), ("eot", ctypes.c_int),
+                ("suppress", ctypes.POINTER(ctypes.c_int32)), ("n_suppress", ctypes.c_int),
+                ("suppress_blank", ctypes.c_int), ("blank_token", ctypes.c_int),
+                ("timestamp_begin", ctypes.c_int), ("no_timestamps", ctypes.c_int),
+                ("max_initial_timestamp_index", ctypes.c_int), ("check_every", ctypes.c_int)]
+
+
+# ----------------------------------------------------------------- front end
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
+    """Whisper's fixed encoder positional embedding (openai whisper model.sinusoids)."""
+    inc = np.log(max_timescale) / (channels // 2 - 1)
+    inv = np.exp(-inc * np.arange(channels // 2))
+    t = np.arange(length)[:, None] * inv[None, :]
+    return np.concatenate([np.sin(t), np.cos(t)], axis=1).astype(np.float32)
+
+
+def hz_to_mel_slaney(f):
+    f = np.asarray(f, dtype=np.float64)
+    f_sp, min_log_hz, min_log_mel, logstep = 200.0 / 3, 1000.0, 15.0, np.log(6.4) / 27.0
+    mel = f / f_sp
+    return np.where(f >= min_log_hz, min_log_mel + np.log(np.maximum(f, 1e-10) / min_log_hz) / logstep, mel)
+
+
+def mel_to_hz_slaney(m):
+    m = np.asarray(m, dtype=np.float64)
+    f_sp, min_log_hz, min_log_mel, logstep = 200.0 / 3, 1000.0, 15.0, np.log(6.4) / 27.0
+    return np.where(m >= min_log_mel, min_log_hz * np.exp(logstep * (m - min_log_mel)), f_sp * m)
+
+
+def mel_filters(sr=16000, n_fft=400, n_mels=80, fmin=0.0, fmax=8000.0) -> np.ndarray:
+    """Slaney-normalised, slaney-scale triangular mel filters, [n_fft//2+1][n_mels]
+    (librosa.filters.mel(htk=False, norm='slaney'), as faster-whisper's get_mel_filters)."""
+    fft_freqs = np.linspace(0, sr // 2, 1 + n_fft // 2)
+    mel_pts = np.linspace(hz_to_mel_slaney(fmin), hz_to_mel_slaney(fmax), n_mels + 2)
+    f_pts = mel_to_hz_slaney(mel_pts)
+    fdiff = np.diff(f_pts)
+    ramps = f_pts[:, None] - fft_freqs[None, :]
+    w = np.zeros((n_mels, len(fft_freqs)))
+    for i in range(n_mels):
+        lower = -ramps[i] / fdiff[i]
+        upper = ramps[i + 2] / fdiff[i + 1]
+        w[i] = np.maximum(0, np.minimum(lower, upper))
+    enorm = 2.0 / (f_pts[2:n_mels + 2] - f_pts[:n_mels])
+    w *= enorm[:, None]
+    return w.T.astype(np.float32)  # [201][80]
+
+
+def mel_constants():
+    """("mel.basis" [400][416], "mel.filters" [208][80]) for janus_whisper_set_tensor."""
+    n = np.arange(400)
+    hann = 0.5 - 0.5 * np.cos(2 * np.pi * n / 400)  # periodic (torch.hann_window / np.hanning(401)[:-1])
+    k = np.arange(201)
+    ang = 2 * np.pi * np.outer(n, k) / 400
+    basis = np.zeros((400, 416))
+    basis[:, :201] = hann[:, None] * np.cos(ang)
+    basis[:, 208:208 + 201] = hann[:, None] * np.sin(ang)
+    filt = np.zeros((208, 80), np.float32)
+    filt[:201] = mel_filters()
+    return basis.astype(np.float32), filt
+
+
+# -------------------------------------------------------------------- weights
+def synthetic_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
+    """Seeded fp32 weights of the real shapes, HF naming (no 'model.' prefix)."""
+    g = torch.Generator().manual_seed(seed)
+    d, ff = cfg.d_model, cfg.ffn
+    W = {}
+
+    def rn(name, *shape, std=0.02):
+        W[name] = (torch.randn(*shape, generator=g) * std).numpy().astype(np.float32)
+
+    def ln(name):
+        W[name + ".weight"] = (1.0 + 0.1 * torch.randn(d, generator=g)).numpy().astype(np.float32)
+        W[name + ".bias"] = (0.02 * torch.randn(d, generator=g)).numpy().astype(np.float32)
+
+    rn("encoder.conv1.weight", d, cfg.n_mels, 3, std=1.0 / math.sqrt(cfg.n_mels * 3))
+    rn("encoder.conv1.bias", d)
+    rn("encoder.conv2.weight", d, d, 3, std=1.0 / math.sqrt(d * 3))
+    rn("encoder.conv2.bias", d)
+    W["encoder.embed_positions.weight"] = sinusoids(cfg.n_audio_ctx, d)
+
+    def attn(p, cross=False):
+        for n in ("q", "k", "v", "out"):
+            rn(f"{p}.{n}_proj.weight", d, d, std=1.0 / math.sqrt(d))
+            if n != "k":
+                rn(f"{p}.{n}_proj.bias", d)
+
+    def mlp(p):
+        rn(f"{p}.fc1.weight", ff, d, std=1.0 / math.sqrt(d))
+        rn(f"{p}.fc1.bias", ff)
+        rn(f"{p}.fc2.weight", d, ff, std=1.0 / math.sqrt(ff))
+        rn(f"{p}.fc2.bias", d)
+
+    for i in range(cfg.enc_layers):
+        p = f"encoder.layers.{i}"
+        attn(p + ".self_attn")
+        ln(p + ".self_attn_layer_norm")
+        mlp(p)
+        ln(p + ".final_layer_norm")
+    ln("encoder.layer_norm")
+    rn("decoder.embed_tokens.weight", cfg.n_vocab, d, std=0.05)
+    rn("decoder.embed_positions.weight", cfg.n_text_ctx, d, std=0.02)
+    for i in range(cfg.dec_layers):
+        p = f"decoder.layers.{i}"
+        attn(p + ".self_attn")
+        ln(p + ".self_attn_layer_norm")
+        attn(p + ".encoder_attn")
+        ln(p + ".encoder_attn_layer_norm")
+        mlp(p)
+        ln(p + ".final_layer_norm")
+    ln("decoder.layer_norm")
+    return W
+
+
+def load_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
+    path = os.environ.get("JANUS_WHISPER_DIR")
+    if path and os.path.exists(os.path.join(path, "model.safetensors")):
+        from safetensors.numpy import load_file
+        raw = load_file(os.path.join(path, "model.safetensors"))
+        return {k[len("model."):] if k.startswith("model.") else k: v.astype(np.float32)
+                for k, v in raw.items()}
+    return synthetic_weights(cfg, seed)
+
+
+# --------------------------------------------------------------------- engine
+class WhisperEngine:
+    """One janus_whisper context on the current GPU (thread-safe per call in C++)."""
+
+    def __init__(self, cfg: WhisperConfig, weights: dict = None, seed: int = 0):
+        self.device = nat.require_gpu()
+        self.cfg = cfg
+        self.tokenizer = tok.load_tokenizer()
+        c = janus_whisper_config(cfg.n_mels, cfg.n_audio_ctx, cfg.d_model, cfg.n_heads,
+                                 cfg.enc_layers, cfg.dec_layers, cfg.n_vocab, cfg.n_text_ctx)
+        h = ctypes.c_void_p()
+        nat.call("janus_whisper_create", ctypes.addressof(c), ctypes.addressof(h))
+        self._h = h
+        weights = weights if weights is not None else load_weights(cfg, seed)
+        basis, filt = mel_constants()
+        weights = dict(weights)
+        weights["mel.basis"] = basis
+        weights["mel.filters"] = filt
+        for name, arr in weights.items():
+            a = np.ascontiguousarray(arr, dtype=np.float32)
+            nat.call("janus_whisper_set_tensor", self._h, name.encode(), a.ctypes.data, a.size)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                nat.lib().janus_whisper_destroy(h)
+            except Exception:
+                pass
+
+    # ---- stages (device tensors in/out, current stream)
+    def logmel(self, pcm: torch.Tensor, offsets: torch.Tensor, batch: int, decim: int,
+               want_raw: bool = False):
+        frames = 2 * self.cfg.n_audio_ctx
+        mel = torch.empty(batch, frames, 80, dtype=torch.float16, device=self.device)
+        raw = torch.empty(batch, frames, 80, dtype=torch.float32, device=self.device) if want_raw else None
+        nat.call("janus_whisper_logmel", self._h, pcm.data_ptr(), offsets.data_ptr(), batch, decim,
+                 raw.data_ptr() if raw is not None else None, mel.data_ptr(), nat.stream_ptr())
+        return (mel, raw) if want_raw else mel
+
+    def encode(self, mel: torch.Tensor) -> torch.Tensor:
+        B = mel.shape[0]
+        assert mel.dtype == torch.float16 and mel.is_contiguous()
+        enc = torch.empty(B, self.cfg.n_audio_ctx, self.cfg.d_model, dtype=torch.float16,
+                          device=self.device)
+        nat.call("janus_whisper_encode", self._h, mel.data_ptr(), B, enc.data_ptr(), nat.stream_ptr())
+        return enc
+
+    def decode_options(self, max_length: int = 448, check_every: int = 16,
+                       timestamps: bool = True):
+        t = self.tokenizer
+        prompt = np.array(t.sot_sequence, np.int32)
+        supp = np.array(t.suppress_tokens(), np.int32)
+        opt = janus_decode_options()
+        opt.prompt = prompt.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        opt.prompt_len = len(prompt)
+        opt.max_length = max_length
+        opt.eot = t.eot
+        opt.suppress = supp.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        opt.n_suppress = len(supp)
+        opt.suppress_blank = 1
+        opt.blank_token = t.blank
+        opt.timestamp_begin = t.timestamp_begin if timestamps else -1
+        opt.no_timestamps = t.no_timestamps
+        opt.max_initial_timestamp_index = 50
+        opt.check_every = check_every
+        return opt, (prompt, supp)
+
+    def decode(self, enc: torch.Tensor, max_length: int = 448, check_every: int = 16,
+               timestamps: bool = True):
+        B = enc.shape[0]
+        opt, keep = self.decode_options(max_length, check_every, timestamps)
+        tokens = torch.empty(B, max_length, dtype=torch.int32, device=self.device)
+        ntok = torch.empty(B, dtype=torch.int32, device=self.device)
+        slp = torch.empty(B, dtype=torch.float32, device=self.device)
+        nat.call("janus_whisper_decode_greedy", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
+                 tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(), nat.stream_ptr())
+        del keep
+        return tokens, ntok, slp
+
+    def texts(self, tokens: torch.Tensor):
+        """Host-side detokenisation of decoded rows (after the prompt)."""
+        t = tokens.cpu().numpy()
+        plen = len(self.tokenizer.sot_sequence)
+        return [self.tokenizer.transcript(row[plen:]) for row in t]

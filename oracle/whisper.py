@@ -1,0 +1,160 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+fp32/fp64 CPU restatement of the reference's STT path (transcriber.py:29-64 ->
+faster-whisper WhisperModel.transcribe(audio[::3], beam_size=1, language='en')):
+
+* ``logmel``: faster-whisper FeatureExtractor (numpy STFT, n_fft 400, hop 160,
+  periodic Hann, center/reflect, 30 s of right zero padding, |rfft|^2, slaney mel,
+  log10 clamp, global-max - 8, (x+4)/4), float64 FFT. Pinned against the third-party
+  transformers WhisperFeatureExtractor (tests/test_oracle_whisper.py).
+* ``encoder`` / ``decoder_logits``: Whisper encoder and decoder forward in fp32 torch,
+  pinned against transformers' WhisperModel loaded with the same weights.
+* ``greedy``: temperature-0 decoding with OpenAI's SuppressBlank, SuppressTokens and
+  ApplyTimestampRules (incl. max_initial_timestamp 1.0 s) that CTranslate2 applies for
+  faster-whisper; parity unpinned against faster-whisper itself (not installed, no
+  weights offline) — its rule code is restated from openai/whisper decoding.py.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def logmel(x, decim=3, filters=None, n_frames=3000):
+    """float32 [n_frames][80]; ``filters`` is [201][80] (janus_amd.whisper.mel_filters)."""
+    x16 = np.asarray(x, np.float32)[::decim].astype(np.float64)
+    n_samples = 480000
+    padded = np.pad(x16, (0, n_samples))               # faster-whisper: padding=30 s
+    y = np.pad(padded, (200, 200), mode="reflect")     # center=True
+    nfr = 1 + (len(y) - 400) // 160
+    idx = np.arange(400)[None, :] + 160 * np.arange(nfr)[:, None]
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(400) / 400)
+    spec = np.fft.rfft(y[idx] * win[None, :], axis=1)
+    power = np.abs(spec[:-1]) ** 2                       # drop last frame
+    mel = power @ filters.astype(np.float64)
+    lg = np.log10(np.maximum(mel, 1e-10))
+    lg = np.maximum(lg, lg.max() - 8.0)
+    lg = (lg + 4.0) / 4.0
+    return lg[:n_frames].astype(np.float32)
+
+
+def _t(W, name):
+    return torch.from_numpy(np.asarray(W[name], np.float32))
+
+
+def _ln(x, W, p):
+    return F.layer_norm(x, (x.shape[-1],), _t(W, p + ".weight"), _t(W, p + ".bias"), 1e-5)
+
+
+def _lin(x, W, p, bias=True):
+    b = _t(W, p + ".bias") if (bias and (p + ".bias") in W) else None
+    return F.linear(x, _t(W, p + ".weight"), b)
+
+
+def _mha(xq, xkv, W, p, n_heads, mask=None):
+    q = _lin(xq, W, p + ".q_proj")
+    k = _lin(xkv, W, p + ".k_proj", bias=False)
+    v = _lin(xkv, W, p + ".v_proj")
+    B, Tq, d = q.shape
+    Tk = k.shape[1]
+    hd = d // n_heads
+    q = q.view(B, Tq, n_heads, hd).transpose(1, 2)
+    k = k.view(B, Tk, n_heads, hd).transpose(1, 2)
+    v = v.view(B, Tk, n_heads, hd).transpose(1, 2)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+    if mask is not None:
+        s = s + mask
+    o = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, Tq, d)
+    return _lin(o, W, p + ".out_proj")
+
+
+@torch.no_grad()
+def encoder(mel, W, cfg):
+    """mel: [B][3000][80] -> [B][1500][d] (fp32)."""
+    x = torch.as_tensor(np.asarray(mel, np.float32)).transpose(1, 2)  # [B][80][3000]
+    x = F.gelu(F.conv1d(x, _t(W, "encoder.conv1.weight"), _t(W, "encoder.conv1.bias"), padding=1))
+    x = F.gelu(F.conv1d(x, _t(W, "encoder.conv2.weight"), _t(W, "encoder.conv2.bias"), stride=2,
+                        padding=1))
+    x = x.transpose(1, 2) + _t(W, "encoder.embed_positions.weight")
+    for i in range(cfg.enc_layers):
+        p = f"encoder.layers.{i}"
+        x = x + _mha(_ln(x, W, p + ".self_attn_layer_norm"), _ln(x, W, p + ".self_attn_layer_norm"),
+                     W, p + ".self_attn", cfg.n_heads)
+        h = _ln(x, W, p + ".final_layer_norm")
+        x = x + _lin(F.gelu(_lin(h, W, p + ".fc1")), W, p + ".fc2")
+    return _ln(x, W, "encoder.layer_norm")
+
+
+@torch.no_grad()
+def decoder_logits(tokens, enc, W, cfg):
+    """Full-sequence decoder forward: tokens [B][T] -> logits [B][T][V] (fp32)."""
+    tokens = torch.as_tensor(np.asarray(tokens, np.int64))
+    enc = torch.as_tensor(enc, dtype=torch.float32)
+    B, T = tokens.shape
+    x = _t(W, "decoder.embed_tokens.weight")[tokens] + _t(W, "decoder.embed_positions.weight")[:T]
+    mask = torch.full((T, T), float("-inf")).triu(1)
+    for i in range(cfg.dec_layers):
+        p = f"decoder.layers.{i}"
+        h = _ln(x, W, p + ".self_attn_layer_norm")
+        x = x + _mha(h, h, W, p + ".self_attn", cfg.n_heads, mask)
+        h = _ln(x, W, p + ".encoder_attn_layer_norm")
+        x = x + _mha(h, enc, W, p + ".encoder_attn", cfg.n_heads)
+        h = _ln(x, W, p + ".final_layer_norm")
+        x = x + _lin(F.gelu(_lin(h, W, p + ".fc1")), W, p + ".fc2")
+    x = _ln(x, W, "decoder.layer_norm")
+    return x @ _t(W, "decoder.embed_tokens.weight").T
+
+
+def apply_rules(logits, sampled, tk, suppress, max_initial=50, timestamps=True):
+    """OpenAI decoding filters on one row of logits (numpy f64, modified copy) given the
+    tokens sampled so far (after the prompt). Returns (filtered logits, log-probs)."""
+    L = np.array(logits, np.float64)
+    L[list(suppress)] = -np.inf
+    if len(sampled) == 0:                     # SuppressBlank
+        L[[tk.blank, tk.eot]] = -np.inf
+    if timestamps:
+        tb = tk.timestamp_begin
+        L[tk.no_timestamps] = -np.inf
+        last_ts = len(sampled) >= 1 and sampled[-1] >= tb
+        pen_ts = len(sampled) < 2 or sampled[-2] >= tb
+        if last_ts:
+            if pen_ts:
+                L[tb:] = -np.inf
+            else:
+                L[:tk.eot] = -np.inf
+        stamps = [t for t in sampled if t >= tb]
+        if stamps:
+            last = stamps[-1] if (last_ts and not pen_ts) else stamps[-1] + 1
+            L[tb:last] = -np.inf
+        if len(sampled) == 0:
+            L[:tb] = -np.inf
+            if max_initial is not None:
+                L[tb + max_initial + 1:] = -np.inf
+        m = L.max()
+        lp = L - (m + np.log(np.exp(L - m).sum()))
+        ts_lp = np.logaddexp.reduce(lp[tb:])
+        text_max = lp[:tb].max()
+        if ts_lp > text_max:
+            L[:tb] = -np.inf
+    m = L.max()
+    lp = L - (m + np.log(np.exp(L - m).sum()))
+    return L, lp
+
+
+@torch.no_grad()
+def greedy(enc, W, cfg, tk, max_length=448, timestamps=True):
+    """Greedy decode of one utterance (enc [1500][d]); returns sampled tokens incl. eot."""
+    suppress = tk.suppress_tokens()
+    seq = list(tk.sot_sequence)
+    sampled = []
+    enc = torch.as_tensor(enc, dtype=torch.float32)[None]
+    while len(seq) < max_length:
+        logits = decoder_logits(np.array([seq]), enc, W, cfg)[0, -1].numpy()
+        L, lp = apply_rules(logits, sampled, tk, suppress, timestamps=timestamps)
+        nxt = int(np.argmax(L))
+        seq.append(nxt)
+        sampled.append(nxt)
+        if nxt == tk.eot:
+            break
+    return sampled

@@ -1,0 +1,138 @@
+"""GPU parity of the kernel-level ABI (include/janus_kernels.h) against PyTorch fp32/fp64
+CPU references of the same ops on the same fp16-rounded inputs."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from janus_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def rel_err(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 64), (64, 1536, 512), (1, 24, 8), (1500, 512, 2048),
+                                   (129, 130, 136)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm(gpu, M, N, K, epi):
+    g = torch.Generator().manual_seed(M * 7 + N + K + epi)
+    A = (torch.randn(M, K, generator=g)).half()
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).half()
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    ref = A.double() @ W.double().T + bias.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = ref + R.double()
+    dA, dW, db = A.to(gpu), W.to(gpu), bias.to(gpu)
+    out_dtype = torch.float16 if epi in (0, 1) else torch.float32
+    C = R.to(gpu).clone() if epi == 2 else torch.empty(M, N, dtype=out_dtype, device=gpu)
+    nat.call("janus_gemm_f16", epi, dA.data_ptr(), K, dW.data_ptr(), K, db.data_ptr(), C.data_ptr(),
+             N, C.data_ptr() if epi == 2 else None, N, M, N, K, stream())
+    torch.cuda.synchronize()
+    err = rel_err(C, ref)
+    assert err < (2e-3 if out_dtype == torch.float16 else 1e-4), err
+
+
+def test_layernorm(gpu):
+    g = torch.Generator().manual_seed(1)
+    for d in (384, 512, 768):
+        x = torch.randn(333, d, generator=g) * 3 + 1
+        gam, bet = torch.randn(d, generator=g), torch.randn(d, generator=g)
+        ref = F.layer_norm(x.double(), (d,), gam.double(), bet.double(), 1e-5)
+        out = torch.empty(333, d, dtype=torch.float16, device=gpu)
+        nat.call("janus_layernorm_f16", x.to(gpu).data_ptr(), gam.to(gpu).data_ptr(),
+                 bet.to(gpu).data_ptr(), out.data_ptr(), 333, d, 1e-5, stream())
+        torch.cuda.synchronize()
+        assert rel_err(out, ref) < 1e-3
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 100, 2), (1, 1500, 6), (3, 65, 8)])
+def test_attention(gpu, B, T, H):
+    g = torch.Generator().manual_seed(T + H)
+    d = H * 64
+    qkv = (torch.randn(B, T, 3 * d, generator=g) * 1.5).half()
+    q, k, v = qkv.double().split(d, dim=-1)
+    q = q.view(B, T, H, 64).transpose(1, 2)
+    k = k.view(B, T, H, 64).transpose(1, 2)
+    v = v.view(B, T, H, 64).transpose(1, 2)
+    ref = ((q @ k.transpose(-1, -2)) / 8.0).softmax(-1) @ v
+    ref = ref.transpose(1, 2).reshape(B, T, d)
+    out = torch.empty(B, T, d, dtype=torch.float16, device=gpu)
+    nat.call("janus_attention_f16", qkv.to(gpu).data_ptr(), out.data_ptr(), B, T, H, 0.125, stream())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 3e-3
+
+
+def act(x, a):
+    return {0: lambda t: t, 1: F.silu, 2: F.gelu, 3: torch.tanh}[a](x)
+
+
+CONV_CASES = [
+    # Cin, Cout, taps, stride, pad, dil, transposed, pre, post, res, scale, acc, T_in
+    (80, 384, 3, 1, 1, 1, 0, 0, 2, False, 1.0, 0, 300),      # whisper conv1
+    (384, 384, 3, 2, 1, 1, 0, 0, 2, True, 1.0, 0, 300),      # whisper conv2 (+pos)
+    (512, 512, 13, 1, 6, 1, 0, 0, 0, False, 1.0, 0, 70),     # firefly conv_pre
+    (256, 256, 11, 1, 25, 5, 0, 1, 1, False, 1.0, 0, 300),   # resblock c1 (pre/post SiLU)
+    (128, 128, 7, 1, 9, 3, 0, 0, 0, True, 1.0, 0, 500),      # resblock c2 (+residual)
+    (64, 64, 3, 1, 1, 1, 0, 1, 1, False, 1.0, 0, 700),
+    (32, 32, 11, 1, 25, 5, 0, 0, 0, True, 1 / 3, 1, 900),    # parallel-block mean accumulate
+    (16, 16, 7, 1, 9, 3, 0, 1, 1, False, 1.0, 0, 1000),
+    (512, 256, 0, 8, 4, 1, 1, 1, 0, False, 1.0, 0, 40),      # ConvTranspose u=8 k=16
+    (256, 128, 0, 8, 4, 1, 1, 1, 0, False, 1.0, 0, 50),
+    (32, 16, 0, 2, 1, 1, 1, 1, 0, False, 1.0, 0, 333),       # ConvTranspose u=2 k=4
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv1d(gpu, case):
+    Cin, Cout, taps, stride, pad, dil, tr, pre, post, use_res, scale, acc, T_in = case
+    B = 2
+    g = torch.Generator().manual_seed(Cin + Cout + taps + stride)
+    x = torch.randn(B, T_in, Cin, generator=g).half()
+    if tr:
+        k = 2 * stride
+        w = torch.randn(Cin, Cout, k, generator=g) / math.sqrt(Cin * 2)
+        T_out = (T_in - 1) * stride - 2 * pad + k
+    else:
+        w = torch.randn(Cout, Cin, taps, generator=g) / math.sqrt(Cin * taps)
+        T_out = (T_in + 2 * pad - dil * (taps - 1) - 1) // stride + 1
+    bias = torch.randn(Cout, generator=g) * 0.1
+    xin = act(x.double(), pre).half().double()  # kernel rounds pre-activated input to fp16
+    xin = xin.transpose(1, 2)
+    wq = w.half().double()
+    if tr:
+        ref = F.conv_transpose1d(xin, wq, bias.double(), stride=stride, padding=pad)
+    else:
+        ref = F.conv1d(xin, wq, bias.double(), stride=stride, padding=pad, dilation=dil)
+    ref = act(ref, post).transpose(1, 2)
+    res = torch.randn(B, T_out, Cout, generator=g).half() if use_res else None
+    if res is not None:
+        ref = ref + res.double()
+    prev = torch.randn(B, T_out, Cout, generator=g).half()
+    ref = ref * scale + (prev.double() if acc else 0)
+    n_packed = nat.lib().janus_conv1d_packed_size(Cin, Cout, taps, tr, stride)
+    packed = torch.empty(n_packed, dtype=torch.float16, device=gpu)
+    dw = w.float().contiguous().to(gpu)
+    nat.call("janus_conv1d_pack", dw.data_ptr(), packed.data_ptr(), Cin, Cout, taps, tr, stride, stream())
+    out = prev.to(gpu).clone()
+    dres = res.to(gpu) if res is not None else None
+    nat.call("janus_conv1d_f16", x.to(gpu).data_ptr(), B, T_in, Cin, packed.data_ptr(),
+             bias.to(gpu).data_ptr(), out.data_ptr(), T_out, Cout, taps, stride, pad, dil, tr, pre,
+             post, dres.data_ptr() if dres is not None else None, T_out * Cout, scale, acc, stream())
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    err = rel_err(out, ref)
+    assert err < 2e-3, err

@@ -1,0 +1,98 @@
+"""Oracle pinning for the STT path (CPU): the log-mel and encoder/decoder restatements
+agree with the third-party transformers Whisper implementation on the same inputs and
+seeded weights (the reference's own tests mock WhisperModel, test_input_processing.py:73-90,
+so transformers is the available pin)."""
+import numpy as np
+import pytest
+import torch
+
+from janus_amd import tokenizer as tkz
+from janus_amd.whisper import WhisperConfig, mel_filters, synthetic_weights
+from janus_amd.workload import synth_speech
+from oracle import whisper as ow
+
+
+def test_logmel_matches_transformers():
+    from transformers import WhisperFeatureExtractor
+    x16 = synth_speech(11, 12.0, sr=16000)
+    ref = WhisperFeatureExtractor(feature_size=80)(x16, sampling_rate=16000,
+                                                  return_tensors="np").input_features[0]
+    ours = ow.logmel(x16, decim=1, filters=mel_filters())
+    assert ours.shape == (3000, 80)
+    assert np.abs(ours - ref.T).max() < 1e-4
+
+
+def test_decimation_matches_slicing():
+    x48 = synth_speech(12, 3.0)
+    a = ow.logmel(x48, decim=3, filters=mel_filters())
+    b = ow.logmel(x48[::3], decim=1, filters=mel_filters())
+    assert np.array_equal(a, b)
+
+
+SMALL = WhisperConfig("pin", d_model=128, n_heads=2, enc_layers=2, dec_layers=2, n_vocab=51864)
+
+
+def _hf_model(W, cfg):
+    from transformers import WhisperConfig as HC, WhisperModel
+    hc = HC(vocab_size=cfg.n_vocab, num_mel_bins=80, encoder_layers=cfg.enc_layers,
+            encoder_attention_heads=cfg.n_heads, decoder_layers=cfg.dec_layers,
+            decoder_attention_heads=cfg.n_heads, d_model=cfg.d_model,
+            encoder_ffn_dim=4 * cfg.d_model, decoder_ffn_dim=4 * cfg.d_model,
+            max_source_positions=1500, max_target_positions=448, activation_function="gelu")
+    m = WhisperModel(hc).eval()
+    sd = {k: torch.from_numpy(v) for k, v in W.items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("k_proj.bias" in k for k in missing), missing
+    return m
+
+
+def test_encoder_decoder_match_transformers():
+    W = synthetic_weights(SMALL, seed=3)
+    m = _hf_model(W, SMALL)
+    mel = ow.logmel(synth_speech(13, 5.0), decim=3, filters=mel_filters())[None]
+    with torch.no_grad():
+        ref_enc = m.encoder(torch.from_numpy(mel).transpose(1, 2)).last_hidden_state
+    enc = ow.encoder(mel, W, SMALL)
+    assert torch.allclose(enc, ref_enc, atol=2e-4, rtol=1e-4)
+    toks = np.array([[tkz.SOT, tkz.TIMESTAMP_BEGIN, 400, 1234, 77]])
+    with torch.no_grad():
+        h = m.decoder(input_ids=torch.from_numpy(toks), encoder_hidden_states=ref_enc).last_hidden_state
+        ref_logits = h @ torch.from_numpy(W["decoder.embed_tokens.weight"]).T
+    logits = ow.decoder_logits(toks, enc, W, SMALL)
+    assert torch.allclose(logits, ref_logits, atol=1e-3, rtol=1e-4)
+
+
+def test_timestamp_rules():
+    tk = tkz.WhisperTokenizer()
+    V = tkz.N_VOCAB_EN
+    rng = np.random.default_rng(0)
+    logits = rng.standard_normal(V)
+    supp = tk.suppress_tokens()
+    # first step: only timestamps <= 1.0 s allowed
+    L, _ = ow.apply_rules(logits, [], tk, supp)
+    allowed = np.nonzero(np.isfinite(L))[0]
+    assert allowed.min() >= tk.timestamp_begin and allowed.max() <= tk.timestamp_begin + 50
+    # after <|0.00|> text: timestamps below the last one are banned
+    L, _ = ow.apply_rules(logits, [tk.timestamp_begin + 10, 500], tk, supp)
+    assert np.all(~np.isfinite(L[tk.timestamp_begin:tk.timestamp_begin + 11]))
+    # after a pair of timestamps: no timestamp may follow
+    L, _ = ow.apply_rules(logits, [tk.timestamp_begin, 500, tk.timestamp_begin + 3, tk.timestamp_begin + 3],
+                          tk, supp)
+    assert np.all(~np.isfinite(L[tk.timestamp_begin:]))
+    # single timestamp after text: only timestamps or eot
+    L, _ = ow.apply_rules(logits, [tk.timestamp_begin, 500, tk.timestamp_begin + 7], tk, supp)
+    assert np.all(~np.isfinite(L[:tk.eot]))
+    for s in supp:
+        assert not np.isfinite(L[s])
+
+
+def test_segments_and_transcript():
+    tk = tkz.WhisperTokenizer()
+    tb = tk.timestamp_begin
+    words = tk.encode_text(" hello world")
+    seq = [tb] + words + [tb + 50, tb + 50] + tk.encode_text(" again") + [tb + 90, tk.eot]
+    segs = tk.segments(seq)
+    assert [s[2] for s in segs] == [" hello world", " again"]
+    assert tk.transcript(seq) == "hello world again"
+    assert tk.transcript([tk.eot]) == ""
