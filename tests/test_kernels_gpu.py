@@ -53,8 +53,9 @@ def test_layernorm(gpu):
         gam, bet = torch.randn(d, generator=g), torch.randn(d, generator=g)
         ref = F.layer_norm(x.double(), (d,), gam.double(), bet.double(), 1e-5)
         out = torch.empty(333, d, dtype=torch.float16, device=gpu)
-        nat.call("janus_layernorm_f16", x.to(gpu).data_ptr(), gam.to(gpu).data_ptr(),
-                 bet.to(gpu).data_ptr(), out.data_ptr(), 333, d, 1e-5, stream())
+        dx, dg, db = x.to(gpu), gam.to(gpu), bet.to(gpu)  # keep device copies alive
+        nat.call("janus_layernorm_f16", dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                 out.data_ptr(), 333, d, 1e-5, stream())
         torch.cuda.synchronize()
         assert rel_err(out, ref) < 1e-3
 
@@ -71,7 +72,8 @@ def test_attention(gpu, B, T, H):
     ref = ((q @ k.transpose(-1, -2)) / 8.0).softmax(-1) @ v
     ref = ref.transpose(1, 2).reshape(B, T, d)
     out = torch.empty(B, T, d, dtype=torch.float16, device=gpu)
-    nat.call("janus_attention_f16", qkv.to(gpu).data_ptr(), out.data_ptr(), B, T, H, 0.125, stream())
+    dqkv = qkv.to(gpu)
+    nat.call("janus_attention_f16", dqkv.data_ptr(), out.data_ptr(), B, T, H, 0.125, stream())
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 3e-3
 
@@ -129,8 +131,9 @@ def test_conv1d(gpu, case):
     nat.call("janus_conv1d_pack", dw.data_ptr(), packed.data_ptr(), Cin, Cout, taps, tr, stride, stream())
     out = prev.to(gpu).clone()
     dres = res.to(gpu) if res is not None else None
-    nat.call("janus_conv1d_f16", x.to(gpu).data_ptr(), B, T_in, Cin, packed.data_ptr(),
-             bias.to(gpu).data_ptr(), out.data_ptr(), T_out, Cout, taps, stride, pad, dil, tr, pre,
+    dx, dbias = x.to(gpu), bias.to(gpu)
+    nat.call("janus_conv1d_f16", dx.data_ptr(), B, T_in, Cin, packed.data_ptr(),
+             dbias.data_ptr(), out.data_ptr(), T_out, Cout, taps, stride, pad, dil, tr, pre,
              post, dres.data_ptr() if dres is not None else None, T_out * Cout, scale, acc, stream())
     torch.cuda.synchronize()
     assert out.shape == ref.shape
