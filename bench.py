@@ -1,0 +1,224 @@
+"""Janus hot-path benchmark: end-to-end encode + decode xRT on MI355X.
+
+Workload (BASELINE.json metric "xRT (audio-s/wall-s) per GPU, 30s clips batch=64"):
+per GPU, 64 seeded synthetic 30 s utterances at 48 kHz (janus_amd/workload.py) already
+resident in HBM. One step = the whole batch through
+  encode: log-mel([::3]) -> Whisper base.en encoder -> greedy decoder (<= 448 tokens,
+          timestamp rules) -> detokenize -> YIN + RMS prosody -> MessagePack packets
+  decode: unpack -> "(emotion) text" prompt -> front end -> Firefly-GAN vocoder
+          (30 s = 2584 latent frames -> 1 323 008 samples @ 44.1 kHz, f32 + int16)
+Weights are seeded synthetic tensors of the real shapes (no checkpoints offline).
+Multi-GPU: one process per GPU, utterances sharded with no data-path collective; packet
+bytes and per-utterance stats are gathered to rank 0 once per step (RCCL).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a
+``roofline`` object for the dominant kernel (the vocoder's implicit-GEMM MFMA conv,
+timed live with HIP events on its stream) and a ``cpu_baseline`` object (the oracle's
+CPU restatement on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MFMA_F16_PEAK_TFLOPS = 2500.0   # dense fp16 MFMA, MI355X_MICROARCH.md
+AUDIO_SECONDS = 30.0
+FRAMES_30S = 2584               # 30 s * 44100 / 512 (rounded up)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
+    ap.add_argument("--seconds", type=float, default=AUDIO_SECONDS)
+    ap.add_argument("--model", default="base.en")
+    ap.add_argument("--max-length", type=int, default=448)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(model: str, tokens_per_utt: float):
+    """Oracle (CPU restatement) time for one 30 s utterance, from bounded samples:
+    log-mel of one 30 s clip, the encoder on one window, 32 decoder positions
+    (scaled to the tokens the GPU emitted), 5 s of YIN (scaled x6) and 1 s of vocoder
+    output (scaled x30). ~10-30 s of CPU work."""
+    from janus_amd import vocoder as jv
+    from janus_amd import whisper as jw
+    from janus_amd.workload import synth_speech
+    from oracle import prosody as op
+    from oracle import vocoder as ov
+    from oracle import whisper as ow
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    cfg = jw.CONFIGS[model]
+    W = jw.synthetic_weights(cfg, 0)
+    x = synth_speech(999, AUDIO_SECONDS)
+    t = {}
+    t0 = time.perf_counter()
+    mel = ow.logmel(x, 3, jw.mel_filters())
+    t["mel"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    enc = ow.encoder(mel[None], W, cfg)
+    t["encoder"] = time.perf_counter() - t0
+    toks = np.full((1, 32), 220)
+    toks[0, 0] = 50257
+    t0 = time.perf_counter()
+    ow.decoder_logits(toks, enc, W, cfg)
+    t["decoder"] = (time.perf_counter() - t0) / 32 * tokens_per_utt
+    t0 = time.perf_counter()
+    op.yin_stream(x[: 5 * 48000])
+    t["prosody"] = (time.perf_counter() - t0) * AUDIO_SECONDS / 5.0
+    vc = jv.FireflyConfig()
+    VW = jv.synthetic_weights(vc, 0)
+    lat = ov.frontend([b"(auto) sample"], [jv.emotion_id("auto")], 87, VW)
+    t0 = time.perf_counter()
+    ov.generator(lat, VW, vc)
+    t["vocoder"] = (time.perf_counter() - t0) * AUDIO_SECONDS / (87 * 512 / 44100)
+    total = sum(t.values())
+    return {
+        "value": AUDIO_SECONDS / total,
+        "unit": "xRT (audio-s/wall-s)",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": ("oracle CPU restatement (numpy/torch fp32 + C YIN), one 30 s utterance: "
+                   f"mel 30 s, encoder 1 window, decoder 32 positions scaled to {tokens_per_utt:.0f} "
+                   "tokens, YIN 5 s x6 (1 thread), vocoder 1 s x30"),
+        "stage_seconds": {k: round(v, 3) for k, v in t.items()},
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from janus_amd.pipeline import JanusPipeline
+    from janus_amd.workload import synth_speech
+
+    dev = torch.device("cuda", local)
+    B = args.batch
+    # rank r owns utterances [r*B, (r+1)*B) of the job (seed = 1000*config + index, config 4)
+    utts = [synth_speech(4000 + rank * B + i, args.seconds) for i in range(B)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
+    frames = int(np.ceil(args.seconds * 44100 / 512))
+    pipe = JanusPipeline(args.model, max_length=args.max_length)
+    torch.cuda.synchronize()
+
+    def step():
+        enc, wav, pcm16 = pipe.step(pcm, offs, lengths, frames)
+        return enc
+
+    for _ in range(args.warmup):
+        enc = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    pipe.vocoder.conv_stats(reset=True)
+    pipe.vocoder.set_timing(True)
+    times = []
+    tok_counts = []
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        enc = step()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        tok_counts.append(float(enc.n_tokens.float().mean().item()))
+    pipe.vocoder.set_timing(False)
+    flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
+    # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
+    total_t = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(total_t, op=dist.ReduceOp.MAX)
+        nbytes = torch.tensor([sum(len(p or b"") for p in enc.packets)], dtype=torch.int64, device=dev)
+        gathered = [torch.zeros_like(nbytes) for _ in range(world)]
+        dist.all_gather(gathered, nbytes)
+    wall = float(total_t.item())
+    ms_per_step = wall / args.steps * 1000.0
+    audio_s = world * B * args.seconds
+    value = audio_s / (wall / args.steps)
+    achieved = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
+    out = None
+    if rank == 0:
+        traffic = None
+        try:
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+        out = {
+            "metric": "xRT (audio-s/wall-s) per GPU, 30s clips batch=64; p50 encode+decode latency",
+            "value": round(value, 2),
+            "unit": "xRT (audio-s/wall-s)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp16",
+            "data": "synthetic (seeded source-filter speech, 48 kHz int16 grid; seeded synthetic weights)",
+            "config": {"workload": "e2e encode+decode, Whisper base.en + Firefly-GAN vocoder, "
+                                   f"{B} x {args.seconds:g} s utterances per GPU",
+                       "model": args.model, "global_batch": world * B, "seq_len": 1500,
+                       "parallelism": f"dp{world}", "max_length": args.max_length},
+            "xrt_per_gpu": round(value / world, 2),
+            "p50_latency_ms": round(float(np.median(times)) * 1000.0, 2),
+            "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
+            "roofline": {
+                "kernel": "conv1d implicit-GEMM (vocoder, v_mfma_f32_16x16x32_f16)",
+                "bound": "mfma",
+                "achieved": round(achieved, 2),
+                "peak": MFMA_F16_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / MFMA_F16_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "launches": int(launches),
+                "avg_launch_ms": round(kms / max(launches, 1), 4),
+                "flops_per_launch": flops / max(launches, 1),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.model, float(np.mean(tok_counts)))
+            except Exception as e:  # reported, never fatal to the bench line
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

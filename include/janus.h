@@ -175,6 +175,62 @@ int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc, int batch
                                 const janus_decode_options* opt, int32_t* tokens,
                                 int32_t* n_tokens, float* sum_logprob, void* stream);
 
+/* ------------------------------------------------------------ vocoder --- */
+/*
+ * Local Firefly-GAN decoder (fish-speech HiFiGANGenerator architecture) replacing the
+ * Fish Audio cloud TTS call client.tts.convert(text=prompt, format="wav", ...)
+ * (backend/services/synthesizer.py:179-203, :235-255). Conditioning is the same
+ * "(emotion) text" prompt the reference sends (synthesizer.py:151-177).
+ */
+typedef struct {
+  int latent_dim;       /* 512 */
+  int channels;         /* upsample_initial_channel, 512 */
+  int n_ups;            /* 5 */
+  int up_rates[8];      /* 8, 8, 2, 2, 2 (kernel 2u, padding u/2) */
+  int n_kernels;        /* 3 */
+  int rb_kernels[4];    /* 3, 7, 11 */
+  int n_dilations;      /* 3 */
+  int rb_dilations[4];  /* 1, 3, 5 */
+  int pre_kernel;       /* 13 */
+  int post_kernel;      /* 13 */
+  int n_emotions;       /* rows of frontend.emotion_embed */
+} janus_vocoder_config;
+
+typedef struct janus_vocoder janus_vocoder;
+
+int janus_vocoder_create(const janus_vocoder_config* cfg, janus_vocoder** out);
+int janus_vocoder_destroy(janus_vocoder* v);
+/*
+ * fp32 [host] parameters by fish-speech generator name (weight norm folded):
+ * conv_pre.{weight,bias}, ups.{i}.{weight,bias} ([Cin][Cout][2u]),
+ * resblocks.{i}.blocks.{j}.convs{1,2}.{m}.{weight,bias}, conv_post.{weight,bias},
+ * plus the front end: frontend.text_embed [256][latent], frontend.emotion_embed
+ * [n_emotions][latent].
+ */
+int janus_vocoder_set_tensor(janus_vocoder* v, const char* name, const float* host,
+                             int64_t numel);
+/*
+ * Prompt -> latents: latents [device] fp16 [B][frames][latent] with frame f of row b =
+ * text_embed[prompt byte floor(f*n_b/frames)] + emotion_embed[emotion_ids[b]].
+ * bytes [device] u8 prompts back to back, byte_offsets [device] int64[B+1],
+ * emotion_ids [device] int32[B].
+ */
+int janus_vocoder_frontend(janus_vocoder* v, const uint8_t* bytes, const int64_t* byte_offsets,
+                           const int32_t* emotion_ids, int batch, int frames, uint16_t* latents,
+                           void* stream);
+/*
+ * Generator forward: latents [device] fp16 [B][frames][latent] -> wav [device] f32
+ * [B][frames*prod(up_rates)] in [-1, 1] and, if pcm != NULL, int16 [B][...]
+ * (clip(round(32767*y))).
+ */
+int janus_vocoder_forward(janus_vocoder* v, const uint16_t* latents, int batch, int frames,
+                          float* wav, int16_t* pcm, void* stream);
+/* HIP-event timing of every conv launch (for roofline accounting). */
+int janus_vocoder_set_timing(janus_vocoder* v, int on);
+/* Accumulated conv FLOPs (2*Cin*Cout*taps*rows), kernel milliseconds and launches. */
+int janus_vocoder_conv_stats(janus_vocoder* v, double* flops, double* ms, int64_t* launches,
+                             int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,13 @@ SIGNATURES = {
     "janus_whisper_logmel": [_P, _P, _P, _I32, _I32, _P, _P, _P],
     "janus_whisper_encode": [_P, _P, _I32, _P, _P],
     "janus_whisper_decode_greedy": [_P, _P, _I32, _P, _P, _P, _P, _P],
+    "janus_vocoder_create": [_P, _P],
+    "janus_vocoder_destroy": [_P],
+    "janus_vocoder_set_tensor": [_P, ctypes.c_char_p, _P, _I64],
+    "janus_vocoder_frontend": [_P, _P, _P, _P, _I32, _I32, _P, _P],
+    "janus_vocoder_forward": [_P, _P, _I32, _I32, _P, _P, _P],
+    "janus_vocoder_set_timing": [_P, _I32],
+    "janus_vocoder_conv_stats": [_P, _P, _P, _P, _I32],
     # include/janus_kernels.h
     "janus_gemm_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
     "janus_layernorm_f16": [_P, _P, _P, _P, _I32, _I32, _F32, _P],

@@ -1,0 +1,90 @@
+"""Batched Janus encode/decode on one GPU (the hot path of SURVEY.md §8, rows a1-a14).
+
+Encode mirrors the engine glue ``process_audio_blocking`` / ``transmit_packet_blocking``
+(backend/services/engine.py:510-552): per utterance transcribe (Whisper on the 48 kHz
+buffer's ``[::3]``), prosody (YIN + RMS at 48 kHz, fallback Normal/Normal on error), and
+— only if the text is non-empty (engine.py:536) — a ``JanusPacket(text, mode, prosody,
+override_emotion=control_state.emotion_override)`` serialised to MessagePack bytes. The
+engine's override is the str-enum ``"auto"``, so its packets carry ``'o': 'auto'``.
+
+Decode mirrors the receiver (engine.py:220-280 -> Synthesizer.synthesize): deserialize,
+build the "(emotion) text" prompt (synthesizer.py:149-177), then the GPU front end and
+Firefly-GAN vocoder produce f32 audio and int16 PCM for all packets in one batch.
+Morse packets stay on the host (synthesizer.py:257-326).
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .common.protocol import JanusMode, JanusPacket
+from .services.prosody import prosody_launch
+from .services.synthesizer import emotion_prompt
+from .vocoder import FireflyConfig, VocoderEngine, emotion_id
+from .whisper import CONFIGS, WhisperEngine
+
+CAPTURE_RATE = 48000
+
+
+class EncodeResult:
+    def __init__(self, texts, tags, packets, tokens, n_tokens):
+        self.texts, self.tags, self.packets = texts, tags, packets
+        self.tokens, self.n_tokens = tokens, n_tokens
+
+
+class JanusPipeline:
+    def __init__(self, model: str = "base.en", whisper_seed: int = 0, vocoder_seed: int = 0,
+                 max_length: int = 448, vocoder_cfg: FireflyConfig = FireflyConfig()):
+        self.device = nat.require_gpu()
+        self.whisper = WhisperEngine(CONFIGS[model], seed=whisper_seed)
+        self.vocoder = VocoderEngine(vocoder_cfg, seed=vocoder_seed)
+        self.max_length = max_length
+
+    # ------------------------------------------------------------------ encode
+    def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
+               override="auto", timestamp=None) -> EncodeResult:
+        B = len(lengths)
+        w = self.whisper
+        mel = w.logmel(pcm, offsets, B, 3)
+        enc = w.encode(mel)
+        tokens, ntok, _ = w.decode(enc, self.max_length)
+        try:
+            tags = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512).tags()
+        except Exception:  # engine.py:520-525
+            tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
+        texts = w.texts(tokens)
+        ts = time.time() if timestamp is None else timestamp
+        packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
+                   for t, g in zip(texts, tags)]
+        return EncodeResult(texts, tags, packets, tokens, ntok)
+
+    # ------------------------------------------------------------------ decode
+    def decode(self, packets, frames: int):
+        """packets: MessagePack bytes (None entries skipped). Returns (wav, pcm, prompts)
+        for the SEMANTIC / TEXT_ONLY packets, all rendered to `frames` latent frames."""
+        prompts, emos = [], []
+        for p in packets:
+            if p is None:
+                continue
+            pkt = JanusPacket.deserialize(p)
+            if pkt.mode == JanusMode.MORSE_CODE:
+                continue
+            if pkt.mode == JanusMode.TEXT_ONLY:
+                emo = pkt.override_emotion
+                prompt, tag = ((f"({emo}) {pkt.text}", str(emo)) if emo and emo != "Auto"
+                               else (pkt.text, "relaxed"))
+            else:
+                prompt, tag = emotion_prompt(pkt)
+            prompts.append(prompt.encode("utf-8"))
+            emos.append(emotion_id(tag, self.vocoder.cfg.n_emotions))
+        if not prompts:
+            return None, None, []
+        lat = self.vocoder.frontend(prompts, emos, frames)
+        wav, pcm = self.vocoder.forward(lat)
+        return wav, pcm, prompts
+
+    def step(self, pcm, offsets, lengths, frames):
+        enc = self.encode(pcm, offsets, lengths)
+        wav, pcm16, _ = self.decode(enc.packets, frames)
+        return enc, wav, pcm16

@@ -1,0 +1,64 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+fp32 torch CPU restatement of the decode path that replaces the reference's cloud TTS
+(synthesizer.py:133-207): the build-defined prompt front end (janus_amd/vocoder.py
+docstring) and the fish-speech Firefly-GAN HiFiGANGenerator forward (conv_pre ->
+[SiLU, ConvTranspose1d, ParallelBlock(ResBlock1 x 3)] x 5 -> SiLU -> conv_post ->
+tanh), written from the public architecture. No reference implementation exists in
+/root/reference (its TTS is remote), so vocoder parity is GPU-vs-this-oracle only
+("parity unpinned" against any external vocoder).
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _t(W, name):
+    return torch.from_numpy(np.asarray(W[name], np.float32))
+
+
+def frontend(prompts_bytes, emotion_ids, frames, W):
+    """latents [B][frames][latent] fp32."""
+    te, ee = _t(W, "frontend.text_embed"), _t(W, "frontend.emotion_embed")
+    out = []
+    for pb, e in zip(prompts_bytes, emotion_ids):
+        n = len(pb)
+        if n:
+            idx = (np.arange(frames, dtype=np.int64) * n) // frames
+            tx = te[torch.from_numpy(np.frombuffer(pb, np.uint8)[idx].astype(np.int64))]
+        else:
+            tx = torch.zeros(frames, te.shape[1])
+        out.append(tx + ee[e])
+    return torch.stack(out)
+
+
+@torch.no_grad()
+def generator(lat, W, cfg):
+    """lat [B][F][latent] -> wav [B][F*prod(rates)] (fp32)."""
+    x = torch.as_tensor(lat, dtype=torch.float32).transpose(1, 2)
+    x = F.conv1d(x, _t(W, "conv_pre.weight"), _t(W, "conv_pre.bias"), padding=(cfg.pre_kernel - 1) // 2)
+    for i, u in enumerate(cfg.up_rates):
+        x = F.silu(x)
+        x = F.conv_transpose1d(x, _t(W, f"ups.{i}.weight"), _t(W, f"ups.{i}.bias"), stride=u,
+                               padding=u // 2)
+        outs = []
+        for j, k in enumerate(cfg.rb_kernels):
+            y = x
+            p = f"resblocks.{i}.blocks.{j}"
+            for m, d in enumerate(cfg.rb_dilations):
+                xt = F.silu(y)
+                xt = F.conv1d(xt, _t(W, f"{p}.convs1.{m}.weight"), _t(W, f"{p}.convs1.{m}.bias"),
+                              padding=d * (k - 1) // 2, dilation=d)
+                xt = F.silu(xt)
+                xt = F.conv1d(xt, _t(W, f"{p}.convs2.{m}.weight"), _t(W, f"{p}.convs2.{m}.bias"),
+                              padding=(k - 1) // 2)
+                y = xt + y
+            outs.append(y)
+        x = torch.stack(outs, 0).mean(0)
+    x = F.silu(x)
+    x = F.conv1d(x, _t(W, "conv_post.weight"), _t(W, "conv_post.bias"), padding=(cfg.post_kernel - 1) // 2)
+    return torch.tanh(x)[:, 0]
+
+
+def pcm16(wav):
+    return np.clip(np.rint(np.asarray(wav, np.float32) * 32767.0), -32768, 32767).astype(np.int16)

@@ -1,0 +1,49 @@
+"""End-to-end batched encode/decode on the GPU (engine.py:510-552 -> receiver):
+packet bytes bit-identical to the oracle packer given the GPU's text and the oracle's
+prosody tags; drop-in Transcriber on a 16 kHz WAV (BASELINE config 1)."""
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+from janus_amd.pipeline import JanusPipeline
+from janus_amd.workload import synth_speech
+from oracle import packet as opk
+from oracle.prosody import OracleProsody
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pipeline_small(gpu):
+    pipe = JanusPipeline("tiny.en", max_length=12)
+    utts = [synth_speech(77 + k, 2.0 + k) for k in range(3)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+    res = pipe.encode(pcm, offs, lengths, timestamp=1700000000.5)
+    for b, u in enumerate(utts):
+        tags = OracleProsody(48000).analyze_buffer(u)[0]
+        assert res.tags[b] == tags
+        if res.texts[b].strip():
+            assert res.packets[b] == opk.serialize(res.texts[b], 0, tags, "auto", 1700000000.5)
+        else:
+            assert res.packets[b] is None
+    wav, pcm16, prompts = pipe.decode(res.packets, 20)
+    assert wav.shape[1] == 20 * 512 and len(prompts) == sum(p is not None for p in res.packets)
+    assert torch.isfinite(wav).all()
+
+
+def test_transcriber_wav(gpu, tmp_path):
+    from janus_amd.services.transcriber import Transcriber
+    x = synth_speech(5, 5.0, sr=16000)
+    path = tmp_path / "a.wav"
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes((x * 32768).astype("<i2").tobytes())
+    tr = Transcriber("tiny.en")
+    t1 = tr.transcribe_file(str(path))
+    t2 = tr.transcribe_buffer(np.repeat(x, 3))  # 48 kHz buffer whose [::3] is x
+    assert isinstance(t1, str) and t1 == t2
