@@ -228,4 +228,128 @@ void decode_attention_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
   JANUS_LAUNCH_CHECK();
 }
 
+
+// ------------------------------------------------------- split-key decode
+// Flash-decoding for one query per (b, h): a block owns (b, key split) for ALL heads, so
+// every cached key/value row (H*64 fp16 = 1 KB at d = 512) is read by one wave as one
+// 16-byte-per-lane coalesced load; lane l holds dims 8l..8l+7 (head l/8). Partial
+// (max, sum, unnormalised P·V) per split go to a small fp32 workspace and a second
+// kernel combines the splits. HBM-bound on the K/V stream.
+constexpr int kSplitKeys = 64;   // keys per split (target)
+constexpr int kMaxHeads = 8;     // d <= 512
+
+__global__ __launch_bounds__(256) void decode_split_kernel(
+    const _Float16* __restrict__ q, int64_t q_bs, const _Float16* __restrict__ k,
+    const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv, int H, int chunk,
+    float scale_log2, float* __restrict__ part_o, float* __restrict__ part_ml) {
+  __shared__ float sc[kSplitKeys * 2][kMaxHeads];
+  __shared__ float acc_s[4][kMaxHeads * kHd];
+  __shared__ float mh[kMaxHeads], lh[kMaxHeads];
+  const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int d = H * kHd;
+  const bool active = lane * 8 < d;
+  const int head = lane >> 3;
+  const int t0 = s * chunk, t1 = min(Tkv, t0 + chunk);
+  float qv[8];
+  {
+    uint4 u = active ? *reinterpret_cast<const uint4*>(q + (int64_t)b * q_bs + lane * 8) : make_uint4(0, 0, 0, 0);
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = (float)h8[j] * scale_log2;
+  }
+  const _Float16* kb = k + (int64_t)b * kv_bs;
+  const _Float16* vb = v + (int64_t)b * kv_bs;
+  for (int t = t0 + w; t < t1; t += 4) {
+    uint4 u = active ? *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs + lane * 8) : make_uint4(0, 0, 0, 0);
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dot += (float)h8[j] * qv[j];
+    dot += __shfl_xor(dot, 1);
+    dot += __shfl_xor(dot, 2);
+    dot += __shfl_xor(dot, 4);
+    if ((lane & 7) == 0 && active) sc[t - t0][head] = dot;
+  }
+  __syncthreads();
+  // per-head max / exp / sum over this split: wave w handles heads w, w+4
+  const int nk = t1 - t0;
+  for (int h = w; h < H; h += 4) {
+    float m = -INFINITY;
+    for (int t = lane; t < nk; t += 64) m = fmaxf(m, sc[t][h]);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float l = 0.f;
+    for (int t = lane; t < nk; t += 64) {
+      const float p = exp2f(sc[t][h] - m);
+      sc[t][h] = p;
+      l += p;
+    }
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    if (lane == 0) { mh[h] = m; lh[h] = l; }
+  }
+  __syncthreads();
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  for (int t = t0 + w; t < t1; t += 4) {
+    uint4 u = active ? *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs + lane * 8) : make_uint4(0, 0, 0, 0);
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
+    const float p = active ? sc[t - t0][head] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += p * (float)h8[j];
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc_s[w][lane * 8 + j] = a[j];
+  }
+  __syncthreads();
+  float* po = part_o + ((int64_t)b * nsplit + s) * d;
+  for (int i = tid; i < d; i += 256) po[i] = acc_s[0][i] + acc_s[1][i] + acc_s[2][i] + acc_s[3][i];
+  if (tid < H) {
+    float* pm = part_ml + (((int64_t)b * nsplit + s) * H + tid) * 2;
+    pm[0] = nk > 0 ? mh[tid] : -INFINITY;
+    pm[1] = nk > 0 ? lh[tid] : 0.f;
+  }
+}
+
+__global__ void decode_combine_kernel(const float* __restrict__ part_o,
+                                      const float* __restrict__ part_ml, int nsplit, int H,
+                                      _Float16* __restrict__ out, int64_t o_bs) {
+  const int b = blockIdx.x, i = threadIdx.x;  // i < d
+  const int d = H * kHd;
+  if (i >= d) return;
+  const int h = i / kHd;
+  float m = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, part_ml[(((int64_t)b * nsplit + s) * H + h) * 2]);
+  float l = 0.f, o = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float* pm = part_ml + (((int64_t)b * nsplit + s) * H + h) * 2;
+    const float f = exp2f(pm[0] - m);
+    l += pm[1] * f;
+    o += part_o[((int64_t)b * nsplit + s) * d + i] * f;
+  }
+  out[(int64_t)b * o_bs + i] = (_Float16)(o / l);
+}
+
+int decode_split_count(int Tkv) {
+  int n = (Tkv + kSplitKeys - 1) / kSplitKeys;
+  return n < 1 ? 1 : n;
+}
+
+void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
+                                   const _Float16* v, int64_t kv_bs, int64_t kv_rs, int Tkv,
+                                   _Float16* out, int64_t o_bs, int B, int H, float scale,
+                                   float* part_o, float* part_ml, hipStream_t s) {
+  JANUS_CHECK(H <= kMaxHeads, "split decode attention: at most 8 heads (d <= 512)");
+  if (B <= 0 || Tkv <= 0) return;
+  const int nsplit = decode_split_count(Tkv);
+  const int chunk = (Tkv + nsplit - 1) / nsplit;
+  JANUS_CHECK(chunk <= 2 * kSplitKeys, "split decode attention: chunk too large");
+  decode_split_kernel<<<dim3(nsplit, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, H, chunk,
+                                                      scale * 1.4426950408889634f, part_o, part_ml);
+  JANUS_LAUNCH_CHECK();
+  decode_combine_kernel<<<B, H * kHd, 0, s>>>(part_o, part_ml, nsplit, H, out, o_bs);
+  JANUS_LAUNCH_CHECK();
+}
+
 }  // namespace janus

@@ -139,8 +139,18 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
     if (tid == 0) row_tok[pos + 1] = R.eot;
     return;
   }
+  __shared__ int last_ts_pos;
+  const int nsamp = pos + 1 - sample_begin_pos;  // tokens sampled so far
+  if (tid == 0) { last_ts_pos = -1; best = 0ull; }
+  __syncthreads();
+  if (R.ts_begin >= 0) {
+    int lp = -1;
+    for (int i = sample_begin_pos + tid; i <= pos; i += blockDim.x)
+      if (row_tok[i] >= R.ts_begin) lp = i;
+    if (lp >= 0) atomicMax(&last_ts_pos, lp);
+  }
+  __syncthreads();
   if (tid == 0) {
-    const int nsamp = pos + 1 - sample_begin_pos;  // tokens sampled so far
     rr.sample_begin = nsamp == 0;
     rr.suppress_all_ts = rr.suppress_text = 0;
     rr.ts_floor = -1;
@@ -151,12 +161,11 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
         if (pen_ts) rr.suppress_all_ts = 1;
         else rr.suppress_text = 1;
       }
-      int last_stamp = -1;
-      for (int i = sample_begin_pos; i <= pos; ++i)
-        if (row_tok[i] >= R.ts_begin) last_stamp = row_tok[i];
-      if (last_stamp >= 0) rr.ts_floor = (last_ts && !pen_ts) ? last_stamp : last_stamp + 1;
+      if (last_ts_pos >= 0) {
+        const int last_stamp = row_tok[last_ts_pos];
+        rr.ts_floor = (last_ts && !pen_ts) ? last_stamp : last_stamp + 1;
+      }
     }
-    best = 0ull;
   }
   __syncthreads();
   const RowRules rl = rr;

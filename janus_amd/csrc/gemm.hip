@@ -138,11 +138,77 @@ static void launch_cfg(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
+
+// ---------------------------------------------------------------- skinny M
+// M <= 64 (decoder steps: one row per utterance). Block = all 64 rows x 16 columns;
+// the 4 waves split K and reduce through LDS, so an N = 512 projection still spreads
+// over 32 blocks and every weight byte is read once per step (weight-streaming bound).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
+  __shared__ float red[4][64][17];
+  const int M = p.M, N = p.N, K = p.K;
+  const int col0 = blockIdx.x * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kq = ((K + 3) / 4 + 31) / 32 * 32;  // per-wave K slice, multiple of 32
+  const int kbeg = w * kq, kend = min(K, kbeg + kq);
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+  const int bcol = col0 + (lane & 15);
+  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
+#pragma unroll 2
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    const int kk = k0 + 8 * (lane >> 4);
+    const bool kok = kk < kend;
+    const half8 b = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+    half8 a[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int r = m * 16 + (lane & 15);
+      a[m] = (kok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kk) : zero_half8();
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
+  __syncthreads();
+  for (int i = tid; i < 64 * 16; i += 256) {
+    const int row = i >> 4, c = i & 15, col = col0 + c;
+    if (row >= M || col >= N) continue;
+    float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
+    v += p.bias ? p.bias[col] : 0.0f;
+    if constexpr (EPI == EPI_F16) {
+      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+    } else if constexpr (EPI == EPI_GELU_F16) {
+      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
+    } else if constexpr (EPI == EPI_RESID_F32) {
+      static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = p.R[(int64_t)row * p.ldr + col] + v;
+    } else {
+      static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
+    }
+  }
+}
+
+static void launch_skinny(int epi, const GemmArgs& p, hipStream_t s) {
+  const int blocks = (p.N + 15) / 16;
+  switch (epi) {
+    case EPI_F16: gemm_skinny_kernel<EPI_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_RESID_F32: gemm_skinny_kernel<EPI_RESID_F32><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_F32: gemm_skinny_kernel<EPI_F32><<<blocks, 256, 0, s>>>(p); break;
+    default: throw Error("bad gemm epilogue");
+  }
+  JANUS_LAUNCH_CHECK();
+}
+
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
   JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");
   if (p.M <= 0 || p.N <= 0) return;
-  if (p.M <= 64) launch_cfg<64, 64, 4, 1>(epi, p, s);
+  if (p.M <= 64) launch_skinny(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }
 

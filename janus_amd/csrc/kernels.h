@@ -38,6 +38,14 @@ void decode_attention_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
                              _Float16* out, int64_t o_bs, int B, int H, float scale,
                              hipStream_t s);
 
+// Split-key (flash-decoding) variant for d <= 512: all heads of a row per block.
+// part_o: f32 [B][splits][d], part_ml: f32 [B][splits][H][2] workspaces.
+int decode_split_count(int Tkv);
+void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
+                                   const _Float16* v, int64_t kv_bs, int64_t kv_rs, int Tkv,
+                                   _Float16* out, int64_t o_bs, int B, int H, float scale,
+                                   float* part_o, float* part_ml, hipStream_t s);
+
 // ----------------------------------------------------------------- conv
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };
 

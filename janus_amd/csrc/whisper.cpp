@@ -6,6 +6,7 @@
 // Weights arrive by name (HF Whisper checkpoint naming) as fp32 and are re-laid out
 // on the device: fused fp16 QKV, packed conv weights, fp16 embeddings; the residual
 // stream stays fp32, GEMM/attention operands are fp16 on MFMA with fp32 accumulation.
+#include <algorithm>
 #include <mutex>
 #include <cstring>
 #include "devmem.h"
@@ -39,7 +40,7 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch;
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml;
 };
 
 namespace janus {
@@ -219,6 +220,11 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
   w->d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
   w->d_smask.ensure(V);
+  const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
+  w->d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
+  w->d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
+  float* part_o = w->d_part_o.as<float>();
+  float* part_ml = w->d_part_ml.as<float>();
   w->d_done.ensure(sizeof(int32_t) * B);
   w->d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
   w->d_supp.ensure(sizeof(int32_t) * (opt->n_suppress > 0 ? opt->n_suppress : 1));
@@ -268,11 +274,13 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
       gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
       kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
-      decode_attention_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, nullptr, o, d, B, H, scale, s);
+      decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
+                                    part_o, part_ml, s);
       gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, x, d, B, d, d, x, d), s);
       layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
       gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
-      decode_attention_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, nullptr, o, d, B, H, scale, s);
+      decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
+                                    part_ml, s);
       gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo_c.as<_Float16>(), d, L.bo_c, x, d, B, d, d, x, d), s);
       layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
       gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
