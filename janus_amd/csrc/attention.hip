@@ -312,21 +312,31 @@ __global__ __launch_bounds__(256) void decode_split_kernel(
   }
 }
 
-__global__ void decode_combine_kernel(const float* __restrict__ part_o,
-                                      const float* __restrict__ part_ml, int nsplit, int H,
-                                      _Float16* __restrict__ out, int64_t o_bs) {
+__global__ __launch_bounds__(512) void decode_combine_kernel(const float* __restrict__ part_o,
+                                                             const float* __restrict__ part_ml,
+                                                             int nsplit, int H,
+                                                             _Float16* __restrict__ out,
+                                                             int64_t o_bs) {
+  __shared__ float sm[64][kMaxHeads], sl[64][kMaxHeads];
   const int b = blockIdx.x, i = threadIdx.x;  // i < d
   const int d = H * kHd;
+  const float* pml = part_ml + (int64_t)b * nsplit * H * 2;
+  for (int j = i; j < nsplit * H; j += blockDim.x) {
+    sm[j / H][j % H] = pml[2 * j];
+    sl[j / H][j % H] = pml[2 * j + 1];
+  }
+  __syncthreads();
   if (i >= d) return;
   const int h = i / kHd;
   float m = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, part_ml[(((int64_t)b * nsplit + s) * H + h) * 2]);
+  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, sm[s][h]);
   float l = 0.f, o = 0.f;
+  const float* po = part_o + (int64_t)b * nsplit * d + i;
+#pragma unroll 8
   for (int s = 0; s < nsplit; ++s) {
-    const float* pm = part_ml + (((int64_t)b * nsplit + s) * H + h) * 2;
-    const float f = exp2f(pm[0] - m);
-    l += pm[1] * f;
-    o += part_o[((int64_t)b * nsplit + s) * d + i] * f;
+    const float f = exp2f(sm[s][h] - m);
+    l += sl[s][h] * f;
+    o += po[(int64_t)s * d] * f;
   }
   out[(int64_t)b * o_bs + i] = (_Float16)(o / l);
 }
@@ -344,7 +354,7 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
   if (B <= 0 || Tkv <= 0) return;
   const int nsplit = decode_split_count(Tkv);
   const int chunk = (Tkv + nsplit - 1) / nsplit;
-  JANUS_CHECK(chunk <= 2 * kSplitKeys, "split decode attention: chunk too large");
+  JANUS_CHECK(chunk <= 2 * kSplitKeys && nsplit <= 64, "split decode attention: too many keys");
   decode_split_kernel<<<dim3(nsplit, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, H, chunk,
                                                       scale * 1.4426950408889634f, part_o, part_ml);
   JANUS_LAUNCH_CHECK();

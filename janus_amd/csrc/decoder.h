@@ -12,6 +12,26 @@ struct DecodeRules {
   int max_initial_ts;            // max_initial_timestamp index (-1: none)
 };
 
+// Per-row rule state carried across steps (computed by the selector for the next step).
+struct RowRules {
+  int sample_begin;       // no token sampled yet
+  int suppress_all_ts;    // last two sampled were timestamps
+  int suppress_text;      // last was a timestamp, penultimate was not: text (< eot) banned
+  int ts_floor;           // timestamps < ts_floor banned (-1: none)
+  int last_stamp;         // last sampled timestamp token (-1: none)
+  int pad[3];
+};
+
+// Per (row, 16-column block) partial statistics of the rule-filtered logits.
+struct LogitPart {
+  float m_all, s_all;     // max / sum exp(v - m_all) over allowed tokens
+  float m_text;           // max over allowed text tokens (< ts_begin)
+  float m_ts, s_ts;       // max / sum exp over allowed timestamp tokens
+  float b_all_v; int b_all_i;  // argmax over allowed (first index on ties)
+  float b_ts_v; int b_ts_i;    // argmax over allowed timestamps
+  float pad;
+};
+
 void cast_f16_f32_launch(const _Float16* in, float* out, int64_t n, hipStream_t s);
 void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t s);
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
@@ -23,6 +43,16 @@ void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen
 void select_launch(const float* logits, int V, const DecodeRules& R, const uint8_t* smask,
                    int32_t* tokens, int ld, int pos, int sample_begin_pos, int32_t* done,
                    float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
+void rules_init_launch(RowRules* rules, int B, hipStream_t s);
+// logits = A[B][K] . W[V][K]^T computed block-wise with the filtered statistics reduced
+// in the epilogue (no logits in HBM); nblk = ceil(V/16) partials per row.
+int logits_partial_blocks(int V);
+void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
+                           const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
+                           LogitPart* parts, hipStream_t s);
+void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
+                            RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
+                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s);
 
 }  // namespace janus

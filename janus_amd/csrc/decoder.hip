@@ -87,13 +87,6 @@ void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen
 }
 
 // ------------------------------------------------------------------ select
-struct RowRules {
-  int sample_begin;       // no token sampled yet
-  int suppress_all_ts;    // last two sampled were timestamps
-  int suppress_text;      // last was a timestamp, penultimate was not: text (< eot) banned
-  int ts_floor;           // timestamps < ts_floor banned (-1: none)
-};
-
 __device__ __forceinline__ bool allowed(int t, const uint8_t* smask, const DecodeRules& R,
                                         const RowRules& rr, bool ban_all_text) {
   if (smask[t]) return false;
@@ -154,6 +147,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ l
     rr.sample_begin = nsamp == 0;
     rr.suppress_all_ts = rr.suppress_text = 0;
     rr.ts_floor = -1;
+    rr.last_stamp = -1;
     if (R.ts_begin >= 0 && nsamp > 0) {
       const bool last_ts = row_tok[pos] >= R.ts_begin;
       const bool pen_ts = nsamp < 2 || row_tok[pos - 1] >= R.ts_begin;
@@ -242,6 +236,232 @@ __global__ void build_mask_kernel(const int32_t* __restrict__ list, int n, uint8
                                   int V) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && list[i] >= 0 && list[i] < V) mask[list[i]] = 1;
+}
+
+
+// ------------------------------------------------------- fused logits path
+__global__ void rules_init_kernel(RowRules* rules, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  RowRules r;
+  r.sample_begin = 1;
+  r.suppress_all_ts = r.suppress_text = 0;
+  r.ts_floor = -1;
+  r.last_stamp = -1;
+  r.pad[0] = r.pad[1] = r.pad[2] = 0;
+  rules[b] = r;
+}
+
+void rules_init_launch(RowRules* rules, int B, hipStream_t s) {
+  rules_init_kernel<<<(B + 63) / 64, 64, 0, s>>>(rules, B);
+  JANUS_LAUNCH_CHECK();
+}
+
+int logits_partial_blocks(int V) { return (V + 15) / 16; }
+
+__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+  return v > bv || (v == bv && i < bi);
+}
+
+// grid (ceil(V/16), ceil(B/64)); each block: 16 vocab columns x 64 rows, K split over
+// the 4 waves (skinny MFMA GEMM), then rule-filtered statistics per row.
+__global__ __launch_bounds__(256) void logits_partial_kernel(
+    const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int K, int V, int B,
+    DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
+    LogitPart* __restrict__ parts) {
+  __shared__ float red[4][64][17];
+  const int nblk = gridDim.x;
+  const int col0 = blockIdx.x * 16, row0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kq = ((K + 3) / 4 + 31) / 32 * 32;
+  const int kbeg = w * kq, kend = min(K, kbeg + kq);
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+  const int bcol = col0 + (lane & 15);
+  const _Float16* wrow = W + (int64_t)min(bcol, V - 1) * K;
+
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    const int kk = k0 + 8 * (lane >> 4);
+    const bool kok = kk < kend;
+    const half8 b = (kok && bcol < V) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+    half8 a[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int r = row0 + m * 16 + (lane & 15);
+      a[m] = (kok && r < B) ? *reinterpret_cast<const half8*>(A + (int64_t)r * lda + kk) : zero_half8();
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
+  __syncthreads();
+  // thread -> (row = tid/4, 4 columns); rows reduce over 4 adjacent lanes
+  const int rl = tid >> 2, cq = (tid & 3) * 4;
+  const int row = row0 + rl;
+  RowRules rr;
+  if (row < B) rr = rules[row];
+  else { rr.sample_begin = 0; rr.suppress_all_ts = rr.suppress_text = 0; rr.ts_floor = -1; }
+  float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
+  float vals[4];
+  bool ok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = cq + j, t = col0 + c;
+    const float v = red[0][rl][c] + red[1][rl][c] + red[2][rl][c] + red[3][rl][c];
+    ok[j] = row < B && t < V && allowed(t, smask, R, rr, false);
+    vals[j] = v;
+    if (ok[j]) {
+      m_all = fmaxf(m_all, v);
+      if (R.ts_begin >= 0 && t >= R.ts_begin) m_ts = fmaxf(m_ts, v);
+      else m_text = fmaxf(m_text, v);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    m_all = fmaxf(m_all, __shfl_xor(m_all, o));
+    m_text = fmaxf(m_text, __shfl_xor(m_text, o));
+    m_ts = fmaxf(m_ts, __shfl_xor(m_ts, o));
+  }
+  float s_all = 0.f, s_ts = 0.f, ba_v = -INFINITY, bt_v = -INFINITY;
+  int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!ok[j]) continue;
+    const int t = col0 + cq + j;
+    const float v = vals[j];
+    s_all += __expf(v - m_all);
+    if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
+    if (R.ts_begin >= 0 && t >= R.ts_begin) {
+      s_ts += __expf(v - m_ts);
+      if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    s_all += __shfl_xor(s_all, o);
+    s_ts += __shfl_xor(s_ts, o);
+    const float ov = __shfl_xor(ba_v, o);
+    const int oi = __shfl_xor(ba_i, o);
+    if (better(ov, oi, ba_v, ba_i)) { ba_v = ov; ba_i = oi; }
+    const float tv = __shfl_xor(bt_v, o);
+    const int ti = __shfl_xor(bt_i, o);
+    if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; }
+  }
+  if ((tid & 3) == 0 && row < B) {
+    LogitPart p;
+    p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
+    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
+    parts[(int64_t)row * nblk + blockIdx.x] = p;
+  }
+}
+
+void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
+                           const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
+                           LogitPart* parts, hipStream_t s) {
+  JANUS_CHECK(K % 8 == 0, "logits: K must be a multiple of 8");
+  dim3 grid(logits_partial_blocks(V), (B + 63) / 64);
+  logits_partial_kernel<<<grid, 256, 0, s>>>(A, lda, W, K, V, B, R, smask, rules, parts);
+  JANUS_LAUNCH_CHECK();
+}
+
+__device__ __forceinline__ float lse_merge(float m1, float s1, float m2, float s2, float* mo) {
+  const float m = fmaxf(m1, m2);
+  *mo = m;
+  if (m == -INFINITY) return 0.f;
+  return s1 * __expf(m1 - m) + s2 * __expf(m2 - m);
+}
+
+// One block per row: reduce the partials, apply the timestamp-probability rule, pick
+// the token, accumulate its log-probability and derive the next step's row rules.
+__global__ __launch_bounds__(256) void select_partials_kernel(
+    const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
+    int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
+    float* __restrict__ sum_lp, int32_t* __restrict__ n_tok) {
+  __shared__ LogitPart sh[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int32_t* row_tok = tokens + (int64_t)b * ld;
+  if (done[b]) {
+    if (tid == 0) row_tok[pos + 1] = R.eot;
+    return;
+  }
+  float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
+  float ba_v = -INFINITY, bt_v = -INFINITY;
+  int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+  const LogitPart* pr = parts + (int64_t)b * nblk;
+  for (int i = tid; i < nblk; i += 256) {
+    const LogitPart p = pr[i];
+    float mo;
+    s_all = lse_merge(m_all, s_all, p.m_all, p.s_all, &mo); m_all = mo;
+    s_ts = lse_merge(m_ts, s_ts, p.m_ts, p.s_ts, &mo); m_ts = mo;
+    m_text = fmaxf(m_text, p.m_text);
+    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
+    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    float mo;
+    const float om = __shfl_xor(m_all, o), os = __shfl_xor(s_all, o);
+    s_all = lse_merge(m_all, s_all, om, os, &mo); m_all = mo;
+    const float tm = __shfl_xor(m_ts, o), ts = __shfl_xor(s_ts, o);
+    s_ts = lse_merge(m_ts, s_ts, tm, ts, &mo); m_ts = mo;
+    m_text = fmaxf(m_text, __shfl_xor(m_text, o));
+    const float av = __shfl_xor(ba_v, o); const int ai = __shfl_xor(ba_i, o);
+    if (better(av, ai, ba_v, ba_i)) { ba_v = av; ba_i = ai; }
+    const float tv = __shfl_xor(bt_v, o); const int ti = __shfl_xor(bt_i, o);
+    if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; }
+  }
+  if (lane == 0) {
+    LogitPart p;
+    p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
+    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i;
+    sh[w] = p;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int k = 1; k < 4; ++k) {
+    const LogitPart& p = sh[k];
+    float mo;
+    s_all = lse_merge(m_all, s_all, p.m_all, p.s_all, &mo); m_all = mo;
+    s_ts = lse_merge(m_ts, s_ts, p.m_ts, p.s_ts, &mo); m_ts = mo;
+    m_text = fmaxf(m_text, p.m_text);
+    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
+    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
+  }
+  const float lse_all = m_all + __logf(s_all);
+  int next = ba_i;
+  float lp = ba_v - lse_all;
+  if (R.ts_begin >= 0 && m_ts > -INFINITY) {
+    const float lse_ts = m_ts + __logf(s_ts);
+    if (lse_ts - lse_all > m_text - lse_all) {  // timestamp mass beats every text token
+      next = bt_i;
+      lp = bt_v - lse_ts;
+    }
+  }
+  row_tok[pos + 1] = next;
+  sum_lp[b] += lp;
+  n_tok[b] += 1;
+  if (next == R.eot) done[b] = 1;
+  // rules for the next step
+  RowRules r = rules[b];
+  const bool last_ts = R.ts_begin >= 0 && next >= R.ts_begin;
+  const bool pen_ts = r.sample_begin || (R.ts_begin >= 0 && row_tok[pos] >= R.ts_begin);
+  r.sample_begin = 0;
+  r.suppress_all_ts = last_ts && pen_ts;
+  r.suppress_text = last_ts && !pen_ts;
+  if (last_ts) r.last_stamp = next;
+  r.ts_floor = r.last_stamp >= 0 ? ((last_ts && !pen_ts) ? r.last_stamp : r.last_stamp + 1) : -1;
+  rules[b] = r;
+}
+
+void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
+                            RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
+                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s) {
+  select_partials_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp,
+                                           n_tok);
+  JANUS_LAUNCH_CHECK();
 }
 
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s) {

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
   for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
   const int bcol = col0 + (lane & 15);
   const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
-#pragma unroll 2
+
   for (int k0 = kbeg; k0 < kend; k0 += 32) {
     const int kk = k0 + 8 * (lane >> 4);
     const bool kok = kk < kend;

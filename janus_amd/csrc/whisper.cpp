@@ -40,7 +40,7 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml;
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules;
 };
 
 namespace janus {
@@ -214,7 +214,6 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   w->d_o.ensure(sizeof(_Float16) * B * d);
   w->d_q2.ensure(sizeof(_Float16) * B * d);
   w->d_f.ensure(sizeof(_Float16) * B * 4 * d);
-  w->d_logits.ensure(sizeof(float) * (int64_t)B * V);
   w->d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
   w->d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
   w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
@@ -223,6 +222,9 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   w->d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
   w->d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
+  const int nblk = logits_partial_blocks(V);
+  w->d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
+  w->d_rules.ensure(sizeof(RowRules) * B);
   float* part_o = w->d_part_o.as<float>();
   float* part_ml = w->d_part_ml.as<float>();
   w->d_done.ensure(sizeof(int32_t) * B);
@@ -231,7 +233,6 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   float* x = w->d_x.as<float>();
   _Float16 *a = w->d_a.as<_Float16>(), *qkv = w->d_qkv.as<_Float16>(), *o = w->d_o.as<_Float16>(),
            *q2 = w->d_q2.as<_Float16>(), *f = w->d_f.as<_Float16>();
-  float* logits = w->d_logits.as<float>();
   int32_t* done = w->d_done.as<int32_t>();
 
   JANUS_HIP(hipMemcpyAsync(w->d_prompt.p, opt->prompt, sizeof(int32_t) * opt->prompt_len,
@@ -242,6 +243,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   build_mask_launch(w->d_supp.as<int32_t>(), opt->n_suppress, w->d_smask.as<uint8_t>(), V, s);
   init_tokens_launch(tokens, maxlen, w->d_prompt.as<int32_t>(), opt->prompt_len, done, sum_lp,
                      n_tokens, B, s);
+  rules_init_launch(w->d_rules.as<RowRules>(), B, s);
 
   // cross-attention keys/values, once per window
   for (int l = 0; l < nl; ++l) {
@@ -289,9 +291,10 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
     if (pos + 1 < sample_begin) continue;  // still inside the prompt
     layernorm_launch(x, w->params.get("decoder.layer_norm.weight", d),
                      w->params.get("decoder.layer_norm.bias", d), a, B, d, 1e-5f, s);
-    gemm_launch(EPI_F32, gargs(a, d, w->tok16.as<_Float16>(), d, nullptr, logits, V, B, V, d), s);
-    select_launch(logits, V, R, w->d_smask.as<uint8_t>(), tokens, maxlen, pos, sample_begin, done,
-                  sum_lp, n_tokens, B, s);
+    logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, w->d_smask.as<uint8_t>(),
+                          w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s);
+    select_partials_launch(w->d_parts.as<LogitPart>(), nblk, R, w->d_rules.as<RowRules>(), tokens,
+                           maxlen, pos, done, sum_lp, n_tokens, B, s);
     if (opt->check_every > 0 && ((pos + 1 - sample_begin) % opt->check_every) == opt->check_every - 1) {
       JANUS_HIP(hipMemcpyAsync(h_done.data(), done, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
       JANUS_HIP(hipStreamSynchronize(s));
