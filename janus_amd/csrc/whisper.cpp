@@ -7,6 +7,8 @@
 // on the device: fused fp16 QKV, packed conv weights, fp16 embeddings; the residual
 // stream stays fp32, GEMM/attention operands are fp16 on MFMA with fp32 accumulation.
 #include <algorithm>
+#include <cstdlib>
+#include <map>
 #include <mutex>
 #include <cstring>
 #include "devmem.h"
@@ -40,7 +42,16 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules;
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp;
+  std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
+  hipStream_t side = nullptr;  // graph capture needs a non-null stream
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  ~janus_whisper() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    if (side) (void)hipStreamDestroy(side);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+  }
 };
 
 namespace janus {
@@ -200,7 +211,8 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
 }
 
 static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const janus_decode_options* opt,
-                          int32_t* tokens, int32_t* n_tokens, float* sum_lp, hipStream_t s) {
+                          int32_t* tokens_out, int32_t* n_tokens_out, float* sum_lp_out,
+                          hipStream_t s) {
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
   const int maxlen = opt->max_length;
@@ -229,6 +241,12 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   float* part_ml = w->d_part_ml.as<float>();
   w->d_done.ensure(sizeof(int32_t) * B);
   w->d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
+  w->d_tok.ensure(sizeof(int32_t) * (int64_t)B * maxlen);
+  w->d_ntok.ensure(sizeof(int32_t) * B);
+  w->d_slp.ensure(sizeof(float) * B);
+  int32_t* tokens = w->d_tok.as<int32_t>();
+  int32_t* n_tokens = w->d_ntok.as<int32_t>();
+  float* sum_lp = w->d_slp.as<float>();
   w->d_supp.ensure(sizeof(int32_t) * (opt->n_suppress > 0 ? opt->n_suppress : 1));
   float* x = w->d_x.as<float>();
   _Float16 *a = w->d_a.as<_Float16>(), *qkv = w->d_qkv.as<_Float16>(), *o = w->d_o.as<_Float16>(),
@@ -265,7 +283,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
   const int sample_begin = opt->prompt_len;  // index of the first sampled token
-  for (int pos = 0; pos + 1 < maxlen; ++pos) {
+  auto step = [&](int pos) {
     embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x, B, s);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
@@ -288,24 +306,68 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
       gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, x, d, B, d, 4 * d, x, d), s);
     }
-    if (pos + 1 < sample_begin) continue;  // still inside the prompt
+    if (pos + 1 < sample_begin) return;  // still inside the prompt
     layernorm_launch(x, w->params.get("decoder.layer_norm.weight", d),
                      w->params.get("decoder.layer_norm.bias", d), a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, w->d_smask.as<uint8_t>(),
                           w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s);
     select_partials_launch(w->d_parts.as<LogitPart>(), nblk, R, w->d_rules.as<RowRules>(), tokens,
                            maxlen, pos, done, sum_lp, n_tokens, B, s);
-    if (opt->check_every > 0 && ((pos + 1 - sample_begin) % opt->check_every) == opt->check_every - 1) {
+  };
+  const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
+  const int chunk = opt->check_every > 0 ? opt->check_every : 16;
+  // every device pointer a captured kernel touches, plus the shape: the graph cache key
+  const std::vector<int64_t> base_key = {
+      B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
+      (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
+      (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
+      (int64_t)w->d_rules.p, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
+      (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
+      R.no_timestamps, R.max_initial_ts};
+  if (w->graphs.size() > 512) {
+    for (auto& kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    w->graphs.clear();
+  }
+  for (int p0 = 0; p0 + 1 < maxlen; p0 += chunk) {
+    const int n = std::min(chunk, maxlen - 1 - p0);
+    if (use_graph) {
+      std::vector<int64_t> key = base_key;
+      key.push_back(p0);
+      key.push_back(n);
+      auto it = w->graphs.find(key);
+      if (it == w->graphs.end()) {
+        hipGraph_t g;
+        JANUS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+          for (int pos = p0; pos < p0 + n; ++pos) step(pos);
+        } catch (...) {
+          hipGraph_t dead;
+          (void)hipStreamEndCapture(s, &dead);
+          if (dead) (void)hipGraphDestroy(dead);
+          throw;
+        }
+        JANUS_HIP(hipStreamEndCapture(s, &g));
+        hipGraphExec_t ge;
+        JANUS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        JANUS_HIP(hipGraphDestroy(g));
+        it = w->graphs.emplace(key, ge).first;
+      }
+      JANUS_HIP(hipGraphLaunch(it->second, s));
+    } else {
+      for (int pos = p0; pos < p0 + n; ++pos) step(pos);
+    }
+    if (opt->check_every > 0 && p0 + n >= sample_begin) {
       JANUS_HIP(hipMemcpyAsync(h_done.data(), done, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
       JANUS_HIP(hipStreamSynchronize(s));
       bool all = true;
       for (int b = 0; b < B; ++b) all = all && h_done[b];
-      if (all) {
-        // remaining positions stay eot-free (-1); callers stop at the first eot
-        break;
-      }
+      if (all) break;  // remaining positions keep -1; callers stop at the first eot
     }
   }
+  JANUS_HIP(hipMemcpyAsync(tokens_out, tokens, sizeof(int32_t) * (int64_t)B * maxlen,
+                           hipMemcpyDeviceToDevice, s));
+  JANUS_HIP(hipMemcpyAsync(n_tokens_out, n_tokens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  JANUS_HIP(hipMemcpyAsync(sum_lp_out, sum_lp, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
 }
 
 }  // namespace janus
@@ -384,7 +446,22 @@ extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc
     std::lock_guard<std::mutex> lk(w->mu);
     hipStream_t s = (hipStream_t)stream;
     prepare(w, s);
+    if (s != nullptr) {
+      decode_greedy(w, reinterpret_cast<const _Float16*>(enc), batch, opt, tokens, n_tokens,
+                    sum_logprob, s);
+      return;
+    }
+    // the null stream cannot be captured: run on a side stream ordered by events
+    if (!w->side) {
+      JANUS_HIP(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
+      JANUS_HIP(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
+      JANUS_HIP(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
+    }
+    JANUS_HIP(hipEventRecord(w->ev_in, s));
+    JANUS_HIP(hipStreamWaitEvent(w->side, w->ev_in, 0));
     decode_greedy(w, reinterpret_cast<const _Float16*>(enc), batch, opt, tokens, n_tokens,
-                  sum_logprob, s);
+                  sum_logprob, w->side);
+    JANUS_HIP(hipEventRecord(w->ev_out, w->side));
+    JANUS_HIP(hipStreamWaitEvent(s, w->ev_out, 0));
   });
 }
