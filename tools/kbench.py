@@ -1,0 +1,79 @@
+"""Kernel microbenchmarks (GPU): the vocoder's conv shapes through the kernel ABI.
+
+python tools/kbench.py [--batch 16] [--reps 5]   -> one line per shape: ms, TFLOP/s, GB/s
+"""
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from janus_amd import _native as nat  # noqa: E402
+
+# (name, Cin, Cout, taps, stride, pad, dil, transposed, pre, post, res, T_in per utt)
+SHAPES = [
+    ("pre512", 512, 512, 13, 1, 6, 1, 0, 0, 0, 0, 2584),
+    ("up0", 512, 256, 0, 8, 4, 1, 1, 1, 0, 0, 2584),
+    ("rb0_k3", 256, 256, 3, 1, 1, 1, 0, 1, 1, 0, 20672),
+    ("rb0_k11d5", 256, 256, 11, 1, 25, 5, 0, 1, 1, 0, 20672),
+    ("up1", 256, 128, 0, 8, 4, 1, 1, 1, 0, 0, 20672),
+    ("rb1_k7d3", 128, 128, 7, 1, 9, 3, 0, 1, 1, 0, 165376),
+    ("rb1_k7c2", 128, 128, 7, 1, 3, 1, 0, 0, 0, 1, 165376),
+    ("rb2_k7d3", 64, 64, 7, 1, 9, 3, 0, 1, 1, 0, 330752),
+    ("rb3_k7d3", 32, 32, 7, 1, 9, 3, 0, 1, 1, 0, 661504),
+    ("rb4_k7d3", 16, 16, 7, 1, 9, 3, 0, 1, 1, 0, 1323008),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    B = a.batch
+    for (name, Cin, Cout, taps, stride, pad, dil, tr, pre, post, use_res, T_in) in SHAPES:
+        if a.only and a.only not in name:
+            continue
+        if tr:
+            T_out = T_in * stride
+            real_taps = 2
+        else:
+            T_out = (T_in + 2 * pad - dil * (taps - 1) - 1) // stride + 1
+            real_taps = taps
+        x = torch.randn(B, T_in, Cin, device=dev).half()
+        wshape = (Cin, Cout, 2 * stride) if tr else (Cout, Cin, taps)
+        w = (torch.randn(*wshape, device=dev) / math.sqrt(Cin * real_taps)).float()
+        bias = torch.randn(Cout, device=dev) * 0.1
+        n = nat.lib().janus_conv1d_packed_size(Cin, Cout, taps, tr, stride)
+        packed = torch.empty(n, dtype=torch.float16, device=dev)
+        nat.call("janus_conv1d_pack", w.data_ptr(), packed.data_ptr(), Cin, Cout, taps, tr, stride, s)
+        out = torch.empty(B, T_out, Cout, device=dev, dtype=torch.float16)
+        res = torch.randn(B, T_out, Cout, device=dev).half() if use_res else None
+
+        def run():
+            nat.call("janus_conv1d_f16", x.data_ptr(), B, T_in, Cin, packed.data_ptr(), bias.data_ptr(),
+                     out.data_ptr(), T_out, Cout, taps, stride, pad, dil, tr, pre, post,
+                     res.data_ptr() if res is not None else None, T_out * Cout, 1.0, 0, s)
+
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.reps
+        flops = 2.0 * Cin * Cout * real_taps * T_out * B
+        byts = 2.0 * B * (T_in * Cin + T_out * Cout * (2 if use_res else 1))
+        print(f"{name:10s} B={B} T_out={T_out:8d} {ms:8.3f} ms {flops / ms / 1e9:8.1f} TF/s "
+              f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
