@@ -59,6 +59,19 @@ int janus_conv1d_f16(const uint16_t* in, int batch, int T_in, int Cin, const uin
                      const uint16_t* res, int64_t res_bs, float scale, int accumulate,
                      void* stream);
 
+/*
+ * Fused fish-speech ResBlock1 unit for narrow stages (C = 16 or 32, odd k <= 11):
+ * out = (accumulate ? out : 0) + scale * (x + c2(silu(c1(silu(x)) + b1)) + b2), with
+ * c1 = Conv1d(C, C, k, dilation, padding dilation*(k-1)/2), c2 = Conv1d(C, C, k,
+ * padding (k-1)/2); x/out fp16 [B][T][C] (must not alias); weights packed by
+ * janus_resunit_pack from PyTorch [C][C][k] fp32 into janus_resunit_packed_size halves.
+ */
+int janus_resunit_packed_size(int C, int k);
+int janus_resunit_pack(const float* w, uint16_t* packed, int C, int k, void* stream);
+int janus_resunit_f16(const uint16_t* x, uint16_t* out, const uint16_t* w1, const float* b1,
+                      const uint16_t* w2, const float* b2, int batch, int T, int C, int k,
+                      int dilation, float scale, int accumulate, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,9 @@ SIGNATURES = {
     "janus_conv1d_pack": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P],
     "janus_conv1d_f16": [_P, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32,
                          _I32, _I32, _I32, _P, _I64, _F32, _I32, _P],
+    "janus_resunit_packed_size": [_I32, _I32],
+    "janus_resunit_pack": [_P, _P, _I32, _I32, _P],
+    "janus_resunit_f16": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F32, _I32, _P],
 }
 RESTYPES = {"janus_conv1d_packed_size": ctypes.c_int64}
 

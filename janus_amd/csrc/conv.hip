@@ -200,30 +200,57 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
     if (kbi + 1 < nkb) wstore((kbi + 1) & 1);
   }
 
-  // epilogue
-  _Float16* outb = a.out + (int64_t)b * a.out_bs;
-  const _Float16* resb = a.res ? a.res + (int64_t)b * a.res_bs : nullptr;
+  // epilogue: bias + post-activation into an fp32 LDS tile (reusing the staging
+  // buffers), then every thread moves 16-byte row chunks: residual and accumulate reads
+  // and the fp16 store are full-width, coalesced accesses.
+  constexpr int ES = BN + 4;  // fp32 row stride
+  float* sE = reinterpret_cast<float*>(smem);
+  __syncthreads();
 #pragma unroll
   for (int n = 0; n < WNT; ++n) {
-    const int co = co0 + wn * WNT * 16 + n * 16 + (lane & 15);
-    if (co >= a.Cout) continue;
-    const float bias = a.bias ? a.bias[co] : 0.0f;
+    const int cl = wn * WNT * 16 + n * 16 + (lane & 15);
+    const int co = co0 + cl;
+    const float bias = (a.bias && co < a.Cout) ? a.bias[co] : 0.0f;
 #pragma unroll
-    for (int m = 0; m < WMT; ++m) {
+    for (int m = 0; m < WMT; ++m)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int r = r0 + wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + rr;
-        if (r >= a.n_rows) continue;
-        const int t = r * a.out_stride + a.out_off + ph;
-        if (t < 0 || t >= a.T_out) continue;
-        float v = act_rt(a.post_act, acc[m][n][rr] + bias);
-        const int64_t o = (int64_t)t * a.Cout + co;
-        if (resb) v += (float)resb[o];
-        v *= a.out_scale;
-        if (a.accumulate) v += (float)outb[o];
-        outb[o] = (_Float16)v;
+        const int rl = wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + rr;
+        sE[rl * ES + cl] = act_rt(a.post_act, acc[m][n][rr] + bias);
       }
+  }
+  __syncthreads();
+  _Float16* outb = a.out + (int64_t)b * a.out_bs;
+  const _Float16* resb = a.res ? a.res + (int64_t)b * a.res_bs : nullptr;
+  constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+  for (int idx = tid; idx < BM * CPR; idx += 256) {
+    const int rl = idx / CPR, cg = (idx % CPR) * 8;
+    const int r = r0 + rl, co = co0 + cg;
+    if (r >= a.n_rows || co >= a.Cout) continue;
+    const int t = r * a.out_stride + a.out_off + ph;
+    if (t < 0 || t >= a.T_out) continue;
+    const int64_t o = (int64_t)t * a.Cout + co;
+    float v[8];
+    const float4 v0 = *reinterpret_cast<const float4*>(sE + rl * ES + cg);
+    const float4 v1 = *reinterpret_cast<const float4*>(sE + rl * ES + cg + 4);
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+    v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    if (resb) {
+      const half8 rv = *reinterpret_cast<const half8*>(resb + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= a.out_scale;
+    if (a.accumulate) {
+      const half8 pv = *reinterpret_cast<const half8*>(outb + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)pv[j];
+    }
+    half8 hv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = (_Float16)v[j];
+    *reinterpret_cast<half8*>(outb + o) = hv;
   }
 }
 
@@ -231,7 +258,9 @@ template <int BM, int BN, int WMT, int WNT, int CK>
 static void conv_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int LI = CK + 8, LW = kConvKB + 8;
   const int rows_max = (BM - 1) * a.in_stride + std::abs((a.taps - 1) * a.dil) + 1;
-  const size_t lds = (size_t)rows_max * LI * 2 + 2 * (size_t)BN * LW * 2;
+  const size_t lds_loop = (size_t)rows_max * LI * 2 + 2 * (size_t)BN * LW * 2;
+  const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = lds_loop > lds_epi ? lds_loop : lds_epi;
   JANUS_CHECK(lds <= 160 * 1024, "conv: LDS tile too large (" + std::to_string(lds) + " B)");
   const int blocks = (int)(cdiv(a.n_rows, BM) * cdiv(a.Cout, BN));
   auto kern = conv_kernel<BM, BN, WMT, WNT, CK>;

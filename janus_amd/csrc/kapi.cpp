@@ -92,3 +92,26 @@ extern "C" int janus_conv1d_f16(const uint16_t* in, int batch, int T_in, int Cin
     conv_launch(a, (hipStream_t)stream);
   });
 }
+
+extern "C" int janus_resunit_packed_size(int C, int k) { return resunit_kp(C, k) * C; }
+
+extern "C" int janus_resunit_pack(const float* w, uint16_t* packed, int C, int k, void* stream) {
+  return guarded([&] {
+    resunit_pack(w, reinterpret_cast<_Float16*>(packed), C, k, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_resunit_f16(const uint16_t* x, uint16_t* out, const uint16_t* w1,
+                                 const float* b1, const uint16_t* w2, const float* b2, int batch,
+                                 int T, int C, int k, int dilation, float scale, int accumulate,
+                                 void* stream) {
+  return guarded([&] {
+    ResUnitArgs a;
+    a.x = reinterpret_cast<const _Float16*>(x); a.out = reinterpret_cast<_Float16*>(out);
+    a.w1 = reinterpret_cast<const _Float16*>(w1); a.b1 = b1;
+    a.w2 = reinterpret_cast<const _Float16*>(w2); a.b2 = b2;
+    a.B = batch; a.T = T; a.C = C; a.k = k; a.d = dilation; a.scale = scale;
+    a.accumulate = accumulate;
+    resunit_launch(a, (hipStream_t)stream);
+  });
+}

@@ -73,6 +73,20 @@ void conv_pack_weights(const float* w, _Float16* packed, int Cin, int Cout, int 
                        int transposed, int u, hipStream_t s);
 void conv_launch(const ConvArgs& a, hipStream_t s);
 
+// Fused ResBlock1 unit (resunit.hip): out = (acc ? out : 0) + scale *
+//   (x + c2(silu(c1(silu(x)) + b1)) + b2), C in {16, 32}, weights packed [C][KP].
+struct ResUnitArgs {
+  const _Float16* x; _Float16* out;
+  const _Float16* w1; const float* b1;
+  const _Float16* w2; const float* b2;
+  int B, T, C, k, d;
+  float scale; int accumulate;
+};
+int resunit_kp(int C, int k);
+bool resunit_supported(int C, int k);
+void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s);
+void resunit_launch(const ResUnitArgs& a, hipStream_t s);
+
 // ------------------------------------------------------------------ mel
 void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* basis,
                 const float* filters, float* logmel, uint32_t* maxkey, int n_frames_out,

@@ -10,6 +10,7 @@
 // activations with SiLU fused into operand staging and bias / SiLU / residual /
 // 1/3-mean fused into the epilogue, so each ResBlock1 conv pair costs two launches and
 // no elementwise passes. Optional per-conv HIP-event timing feeds bench.py's roofline.
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 #include "devmem.h"
@@ -30,6 +31,11 @@ struct VConv {
   const float* bias = nullptr;
   int cin = 0, cout = 0, taps = 0, stride = 1, pad = 0, dil = 1, transposed = 0;
 };
+struct VUnit {  // fused (convs1[m], convs2[m]) pair for narrow stages
+  DevMem w1, w2;
+  const float *b1 = nullptr, *b2 = nullptr;
+  int c = 0, k = 0, d = 1;
+};
 struct TimedLaunch {
   hipEvent_t a, b;
   double flops;
@@ -44,6 +50,8 @@ struct janus_vocoder {
   janus::VConv pre;
   std::vector<janus::VConv> ups;
   std::vector<janus::VConv> rb;  // [stage][kernel][dilation][conv1|conv2]
+  std::vector<janus::VUnit> units;  // same indexing / 2, fused path (C <= 32)
+  bool fuse = true;
   const float* post_w = nullptr;
   float post_b = 0.f;
   janus::DevMem buf[5];
@@ -82,6 +90,8 @@ static void prepare(janus_vocoder* v, hipStream_t s) {
   v->ups.resize(c.n_ups);
   v->rb.clear();
   v->rb.resize((size_t)c.n_ups * c.n_kernels * c.n_dilations * 2);
+  v->units.clear();
+  v->units.resize((size_t)c.n_ups * c.n_kernels * c.n_dilations);
   int ch = c.channels;
   for (int i = 0; i < c.n_ups; ++i) {
     const int u = c.up_rates[i];
@@ -96,6 +106,19 @@ static void prepare(janus_vocoder* v, hipStream_t s) {
                   k, 1, d * (k - 1) / 2, d, 0, s);
         make_conv(v, v->rb[rb_index(c, i, kj, m, 1)], p + ".convs2." + std::to_string(m), ch, ch,
                   k, 1, (k - 1) / 2, 1, 0, s);
+        if (resunit_supported(ch, k)) {
+          VUnit& U = v->units[rb_index(c, i, kj, m, 0) / 2];
+          U.c = ch; U.k = k; U.d = d;
+          const int64_t n = (int64_t)resunit_kp(ch, k) * ch;
+          U.w1.ensure(sizeof(_Float16) * n);
+          U.w2.ensure(sizeof(_Float16) * n);
+          resunit_pack(v->params.get(p + ".convs1." + std::to_string(m) + ".weight", (int64_t)ch * ch * k),
+                       U.w1.as<_Float16>(), ch, k, s);
+          resunit_pack(v->params.get(p + ".convs2." + std::to_string(m) + ".weight", (int64_t)ch * ch * k),
+                       U.w2.as<_Float16>(), ch, k, s);
+          U.b1 = v->params.get(p + ".convs1." + std::to_string(m) + ".bias", ch);
+          U.b2 = v->params.get(p + ".convs2." + std::to_string(m) + ".bias", ch);
+        }
       }
     }
   }
@@ -140,6 +163,26 @@ static void run_conv(janus_vocoder* v, const VConv& cv, const _Float16* in, int 
   }
 }
 
+static void run_unit(janus_vocoder* v, const VUnit& U, const _Float16* x, _Float16* out, int B,
+                     int T, float scale, int acc, hipStream_t s) {
+  ResUnitArgs a;
+  a.x = x; a.out = out; a.w1 = U.w1.as<_Float16>(); a.b1 = U.b1; a.w2 = U.w2.as<_Float16>();
+  a.b2 = U.b2; a.B = B; a.T = T; a.C = U.c; a.k = U.k; a.d = U.d; a.scale = scale;
+  a.accumulate = acc;
+  if (v->timing) {
+    TimedLaunch t;
+    t.a = take_event(v);
+    t.b = take_event(v);
+    t.flops = 2.0 * 2.0 * U.c * U.c * U.k * (double)T * B;
+    JANUS_HIP(hipEventRecord(t.a, s));
+    resunit_launch(a, s);
+    JANUS_HIP(hipEventRecord(t.b, s));
+    v->pending.push_back(t);
+  } else {
+    resunit_launch(a, s);
+  }
+}
+
 static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* wav, int16_t* pcm,
                     hipStream_t s) {
   const auto& c = v->cfg;
@@ -168,6 +211,17 @@ static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* 
     for (int kj = 0; kj < c.n_kernels; ++kj) {
       const _Float16* x = U;
       for (int m = 0; m < c.n_dilations; ++m) {
+        const VUnit& U = v->units[rb_index(c, i, kj, m, 0) / 2];
+        if (v->fuse && U.c > 0) {
+          if (m + 1 < c.n_dilations) {
+            _Float16* xn = X[m & 1];
+            run_unit(v, U, x, xn, B, T, 1.0f, 0, s);
+            x = xn;
+          } else {
+            run_unit(v, U, x, H, B, T, inv_k, kj > 0 ? 1 : 0, s);
+          }
+          continue;
+        }
         const VConv& c1 = v->rb[rb_index(c, i, kj, m, 0)];
         const VConv& c2 = v->rb[rb_index(c, i, kj, m, 1)];
         run_conv(v, c1, x, B, T, S, T, ACT_SILU, ACT_SILU, nullptr, 1.0f, 0, s);
@@ -210,6 +264,7 @@ extern "C" int janus_vocoder_create(const janus_vocoder_config* cfg, janus_vocod
                 "vocoder: bad config");
     auto* v = new janus_vocoder();
     v->cfg = *cfg;
+    v->fuse = std::getenv("JANUS_NO_FUSE") == nullptr;
     *out = v;
   });
 }

@@ -139,3 +139,35 @@ def test_conv1d(gpu, case):
     assert out.shape == ref.shape
     err = rel_err(out, ref)
     assert err < 2e-3, err
+
+
+@pytest.mark.parametrize("C,k,d,acc", [(16, 3, 1, 0), (16, 11, 5, 1), (32, 7, 3, 0), (32, 11, 5, 1),
+                                       (16, 7, 1, 1), (32, 3, 3, 0)])
+def test_resunit(gpu, C, k, d, acc):
+    B, T = 2, 1500
+    g = torch.Generator().manual_seed(C * 100 + k * 10 + d)
+    x = torch.randn(B, T, C, generator=g).half()
+    w1 = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)
+    w2 = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)
+    b1 = torch.randn(C, generator=g) * 0.1
+    b2 = torch.randn(C, generator=g) * 0.1
+    prev = torch.randn(B, T, C, generator=g).half()
+    scale = 1 / 3 if acc else 1.0
+    xd = x.double().transpose(1, 2)
+    h = F.conv1d(F.silu(xd).half().double(), w1.half().double(), b1.double(), padding=d * (k - 1) // 2,
+                 dilation=d)
+    h = F.silu(h).half().double()
+    y = F.conv1d(h, w2.half().double(), b2.double(), padding=(k - 1) // 2) + xd
+    ref = y.transpose(1, 2) * scale + (prev.double() if acc else 0)
+    n = nat.lib().janus_resunit_packed_size(C, k)
+    p1 = torch.empty(n, dtype=torch.float16, device=gpu)
+    p2 = torch.empty(n, dtype=torch.float16, device=gpu)
+    dw1, dw2 = w1.to(gpu), w2.to(gpu)
+    nat.call("janus_resunit_pack", dw1.data_ptr(), p1.data_ptr(), C, k, stream())
+    nat.call("janus_resunit_pack", dw2.data_ptr(), p2.data_ptr(), C, k, stream())
+    dx, db1, db2 = x.to(gpu), b1.to(gpu), b2.to(gpu)
+    out = prev.to(gpu).clone()
+    nat.call("janus_resunit_f16", dx.data_ptr(), out.data_ptr(), p1.data_ptr(), db1.data_ptr(),
+             p2.data_ptr(), db2.data_ptr(), B, T, C, k, d, scale, acc, stream())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 2e-3

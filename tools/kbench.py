@@ -75,5 +75,36 @@ def main():
               f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
 
 
+def resunits(B, reps):
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    for (C, k, d, T) in [(32, 7, 3, 661504), (32, 11, 5, 661504), (16, 7, 3, 1323008), (16, 3, 1, 1323008)]:
+        x = torch.randn(B, T, C, device=dev).half()
+        out = torch.empty_like(x)
+        n = nat.lib().janus_resunit_packed_size(C, k)
+        w = (torch.randn(C, C, k, device=dev) / math.sqrt(C * k)).float()
+        p = torch.empty(n, dtype=torch.float16, device=dev)
+        nat.call("janus_resunit_pack", w.data_ptr(), p.data_ptr(), C, k, s)
+        bias = torch.zeros(C, device=dev)
+
+        def run():
+            nat.call("janus_resunit_f16", x.data_ptr(), out.data_ptr(), p.data_ptr(), bias.data_ptr(),
+                     p.data_ptr(), bias.data_ptr(), B, T, C, k, d, 1.0, 0, s)
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        flops = 2 * 2.0 * C * C * k * T * B
+        byts = 2.0 * B * T * C * 3
+        print(f"unit C{C} k{k} d{d} B={B} T={T:8d} {ms:8.3f} ms {flops / ms / 1e9:8.1f} TF/s "
+              f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
+
+
 if __name__ == "__main__":
     main()
+    resunits(16, 5)
