@@ -117,13 +117,16 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from janus_amd.dist import gather_packets, shard
     from janus_amd.pipeline import JanusPipeline
     from janus_amd.workload import synth_speech
 
     dev = torch.device("cuda", local)
-    B = args.batch
-    # rank r owns utterances [r*B, (r+1)*B) of the job (seed = 1000*config + index, config 4)
-    utts = [synth_speech(4000 + rank * B + i, args.seconds) for i in range(B)]
+    # weak scaling: B utterances per GPU; rank r owns shard(r) of the job's world*B
+    # utterances (seed = 1000*config + global index, config 4)
+    u0, u1 = shard(rank, world, world * args.batch)
+    B = u1 - u0
+    utts = [synth_speech(4000 + i, args.seconds) for i in range(u0, u1)]
     lengths = [len(u) for u in utts]
     offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
@@ -157,11 +160,11 @@ def main():
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
     total_t = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+    n_packets = sum(p is not None for p in enc.packets)
     if world > 1:
         dist.all_reduce(total_t, op=dist.ReduceOp.MAX)
-        nbytes = torch.tensor([sum(len(p or b"") for p in enc.packets)], dtype=torch.int64, device=dev)
-        gathered = [torch.zeros_like(nbytes) for _ in range(world)]
-        dist.all_gather(gathered, nbytes)
+        # result gather (RCCL over xGMI): the job's packets on every rank, untimed
+        n_packets = sum(p is not None for p in gather_packets(enc.packets, dev))
     wall = float(total_t.item())
     ms_per_step = wall / args.steps * 1000.0
     audio_s = world * B * args.seconds
@@ -195,6 +198,7 @@ def main():
             "xrt_per_gpu": round(value / world, 2),
             "p50_latency_ms": round(float(np.median(times)) * 1000.0, 2),
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
+            "packets_gathered": n_packets,
             "roofline": {
                 "kernel": "conv1d implicit-GEMM (vocoder, v_mfma_f32_16x16x32_f16)",
                 "bound": "mfma",
