@@ -9,7 +9,7 @@ resident in HBM. One step = the whole batch through
           (30 s = 2584 latent frames -> 1 323 008 samples @ 44.1 kHz, f32 + int16)
 Weights are seeded synthetic tensors of the real shapes (no checkpoints offline).
 Multi-GPU: one process per GPU, utterances sharded with no data-path collective; packet
-bytes and per-utterance stats are gathered to rank 0 once per step (RCCL).
+bytes are all-gathered once after the timed steps (RCCL over xGMI).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 ``roofline`` object for the dominant kernel (the vocoder's implicit-GEMM MFMA conv,
@@ -147,19 +147,24 @@ def main():
     pipe.vocoder.set_timing(True)
     times = []
     tok_counts = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_begin = time.perf_counter()
     for _ in range(args.steps):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         enc = step()
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
         tok_counts.append(float(enc.n_tokens.float().mean().item()))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
-    total_t = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+    total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
     n_packets = sum(p is not None for p in enc.packets)
     if world > 1:
         dist.all_reduce(total_t, op=dist.ReduceOp.MAX)
