@@ -260,16 +260,33 @@ __global__ __launch_bounds__(256) void decode_split_kernel(
   }
   const _Float16* kb = k + (int64_t)b * kv_bs;
   const _Float16* vb = v + (int64_t)b * kv_bs;
-  for (int t = t0 + w; t < t1; t += 4) {
-    uint4 u = active ? *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs + lane * 8) : make_uint4(0, 0, 0, 0);
-    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
+  // issue every K and V row load of this wave before any use (<= 16 keys per wave):
+  // 32 x 16 B per lane in flight hides the HBM latency of the once-read cache
+  constexpr int KPW = kSplitKeys / 4;
+  uint4 kr[KPW], vr[KPW];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int t = t0 + w + 4 * i;
+    kr[i] = (active && t < t1) ? *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs + lane * 8)
+                               : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int t = t0 + w + 4 * i;
+    vr[i] = (active && t < t1) ? *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs + lane * 8)
+                               : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int t = t0 + w + 4 * i;
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&kr[i]);
     float dot = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dot += (float)h8[j] * qv[j];
     dot += __shfl_xor(dot, 1);
     dot += __shfl_xor(dot, 2);
     dot += __shfl_xor(dot, 4);
-    if ((lane & 7) == 0 && active) sc[t - t0][head] = dot;
+    if ((lane & 7) == 0 && active && t < t1) sc[t - t0][head] = dot;
   }
   __syncthreads();
   // per-head max / exp / sum over this split: wave w handles heads w, w+4
@@ -291,10 +308,11 @@ __global__ __launch_bounds__(256) void decode_split_kernel(
   float a[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) a[j] = 0.f;
-  for (int t = t0 + w; t < t1; t += 4) {
-    uint4 u = active ? *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs + lane * 8) : make_uint4(0, 0, 0, 0);
-    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
-    const float p = active ? sc[t - t0][head] : 0.f;
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int t = t0 + w + 4 * i;
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&vr[i]);
+    const float p = (active && t < t1) ? sc[t - t0][head] : 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += p * (float)h8[j];
   }
@@ -354,7 +372,7 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
   if (B <= 0 || Tkv <= 0) return;
   const int nsplit = decode_split_count(Tkv);
   const int chunk = (Tkv + nsplit - 1) / nsplit;
-  JANUS_CHECK(chunk <= 2 * kSplitKeys && nsplit <= 64, "split decode attention: too many keys");
+  JANUS_CHECK(chunk <= kSplitKeys && nsplit <= 64, "split decode attention: too many keys");
   decode_split_kernel<<<dim3(nsplit, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, H, chunk,
                                                       scale * 1.4426950408889634f, part_o, part_ml);
   JANUS_LAUNCH_CHECK();

@@ -204,6 +204,117 @@ static void launch_skinny(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
+// ------------------------------------------------------- skinny M + fused LN
+// C = epi( LN(x)[M,K] · W[N,K]^T + bias ), M <= 64, x fp32 (the residual stream): the
+// block recomputes the 64 rows' LayerNorm statistics (two-pass, eps as given) and
+// normalises each A fragment on the fly, so decoder pre-LN blocks need no separate
+// LayerNorm launch. EPI_QKV writes q to C and k/v straight into the KV cache rows.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(SkinnyLnArgs p) {
+  __shared__ float red[4][64][17];
+  __shared__ float s_mean[64], s_rstd[64];
+  const int M = p.M, N = p.N, K = p.K;
+  const int col0 = blockIdx.x * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // row statistics: wave w -> rows 16w .. 16w+15
+  for (int i = 0; i < 16; ++i) {
+    const int r = w * 16 + i;
+    if (r >= M) break;
+    const float* xr = p.x + (int64_t)r * p.ldx;
+    float sm = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + k);
+      sm += v.x + v.y + v.z + v.w;
+    }
+    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
+    const float mean = sm / K;
+    float sq = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + k);
+      const float a0 = v.x - mean, a1 = v.y - mean, a2 = v.z - mean, a3 = v.w - mean;
+      sq += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+    }
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+    if (lane == 0) { s_mean[r] = mean; s_rstd[r] = rsqrtf(sq / K + p.eps); }
+  }
+  __syncthreads();
+  const int kq = ((K + 3) / 4 + 31) / 32 * 32;
+  const int kbeg = w * kq, kend = min(K, kbeg + kq);
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+  const int bcol = col0 + (lane & 15);
+  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    const int kk = k0 + 8 * (lane >> 4);
+    const bool kok = kk < kend;
+    const half8 b = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+    float g[8], be[8];
+    if (kok) {
+      const float4 g0 = *reinterpret_cast<const float4*>(p.gamma + kk);
+      const float4 g1 = *reinterpret_cast<const float4*>(p.gamma + kk + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(p.beta + kk);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.beta + kk + 4);
+      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
+      be[0] = b0.x; be[1] = b0.y; be[2] = b0.z; be[3] = b0.w; be[4] = b1.x; be[5] = b1.y; be[6] = b1.z; be[7] = b1.w;
+    }
+    half8 a[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int r = m * 16 + (lane & 15);
+      a[m] = zero_half8();
+      if (kok && r < M) {
+        const float* xr = p.x + (int64_t)r * p.ldx + kk;
+        const float4 x0 = *reinterpret_cast<const float4*>(xr);
+        const float4 x1 = *reinterpret_cast<const float4*>(xr + 4);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float mean = s_mean[r], rstd = s_rstd[r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[m][j] = (_Float16)((xv[j] - mean) * rstd * g[j] + be[j]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
+  __syncthreads();
+  for (int i = tid; i < 64 * 16; i += 256) {
+    const int row = i >> 4, c = i & 15, col = col0 + c;
+    if (row >= M || col >= N) continue;
+    float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
+    v += p.bias ? p.bias[col] : 0.0f;
+    if constexpr (EPI == EPI_GELU_F16) {
+      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
+    } else if constexpr (EPI == EPI_QKV) {
+      const int d = p.qkv_d;
+      if (col < d) {
+        static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+      } else {
+        _Float16* cache = col < 2 * d ? p.kc : p.vc;
+        cache[((int64_t)row * p.n_ctx + p.pos) * d + (col % d)] = (_Float16)v;
+      }
+    } else {
+      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+    }
+  }
+}
+
+void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& p, hipStream_t s) {
+  JANUS_CHECK(p.M <= 64 && p.K % 8 == 0 && p.ldx % 4 == 0, "skinny LN gemm: M <= 64, K % 8 == 0");
+  if (p.M <= 0 || p.N <= 0) return;
+  const int blocks = (p.N + 15) / 16;
+  switch (epi) {
+    case EPI_F16: gemm_skinny_ln_kernel<EPI_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_skinny_ln_kernel<EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_QKV: gemm_skinny_ln_kernel<EPI_QKV><<<blocks, 256, 0, s>>>(p); break;
+    default: throw Error("skinny LN gemm: bad epilogue");
+  }
+  JANUS_LAUNCH_CHECK();
+}
+
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
   JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");

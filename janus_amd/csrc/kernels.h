@@ -5,7 +5,7 @@
 namespace janus {
 
 // ------------------------------------------------------------------ GEMM
-enum GemmEpi { EPI_F16 = 0, EPI_GELU_F16 = 1, EPI_RESID_F32 = 2, EPI_F32 = 3 };
+enum GemmEpi { EPI_F16 = 0, EPI_GELU_F16 = 1, EPI_RESID_F32 = 2, EPI_F32 = 3, EPI_QKV = 4 };
 
 struct GemmArgs {
   const _Float16* A; int64_t lda;  // [M][K]
@@ -16,6 +16,19 @@ struct GemmArgs {
   int M, N, K;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
+
+// M <= 64 GEMM with the LayerNorm of its fp32 A operand fused (decoder pre-LN blocks).
+// EPI_QKV: columns [0, d) -> C, [d, 2d) -> kc[row][pos], [2d, 3d) -> vc[row][pos].
+struct SkinnyLnArgs {
+  const float* x; int64_t ldx;
+  const float* gamma; const float* beta; float eps;
+  const _Float16* W; int64_t ldw;
+  const float* bias;
+  void* C; int64_t ldc;
+  int M, N, K;
+  _Float16* kc; _Float16* vc; int pos, n_ctx, qkv_d;
+};
+void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& p, hipStream_t s);
 
 // ------------------------------------------------------------- LayerNorm
 // out[r][:] = fp16( (x[r]-mean)/sqrt(var+eps) * g + b ), x fp32 [rows][d]

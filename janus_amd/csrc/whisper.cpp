@@ -283,6 +283,16 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
   const int sample_begin = opt->prompt_len;  // index of the first sampled token
+  const bool fused_ln = B <= 64 && std::getenv("JANUS_NO_FUSED_LN") == nullptr;
+  auto lnargs = [&](const float* xin, const float* g, const float* bta, const _Float16* W,
+                    const float* bias, void* C, int64_t ldc, int N, _Float16* kcp, _Float16* vcp,
+                    int pos) {
+    SkinnyLnArgs p;
+    p.x = xin; p.ldx = d; p.gamma = g; p.beta = bta; p.eps = 1e-5f; p.W = W; p.ldw = d;
+    p.bias = bias; p.C = C; p.ldc = ldc; p.M = B; p.N = N; p.K = d;
+    p.kc = kcp; p.vc = vcp; p.pos = pos; p.n_ctx = NC; p.qkv_d = d;
+    return p;
+  };
   auto step = [&](int pos) {
     embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x, B, s);
     for (int l = 0; l < nl; ++l) {
@@ -291,19 +301,34 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       _Float16* vc = w->d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
       _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
       _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
-      layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
-      gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
-      kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
+      if (fused_ln) {
+        gemm_skinny_ln_launch(EPI_QKV, lnargs(x, L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
+                                              qkv, 3 * d, 3 * d, kc, vc, pos), s);
+      } else {
+        layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
+        gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
+        kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
+      }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s);
       gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, x, d, B, d, d, x, d), s);
-      layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-      gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+      if (fused_ln) {
+        gemm_skinny_ln_launch(EPI_F16, lnargs(x, L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
+                                              nullptr, nullptr, pos), s);
+      } else {
+        layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+        gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+      }
       decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                     part_ml, s);
       gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo_c.as<_Float16>(), d, L.bo_c, x, d, B, d, d, x, d), s);
-      layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
-      gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
+      if (fused_ln) {
+        gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(x, L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
+                                                   4 * d, nullptr, nullptr, pos), s);
+      } else {
+        layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+        gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
+      }
       gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, x, d, B, d, 4 * d, x, d), s);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
