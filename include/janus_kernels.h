@@ -52,6 +52,8 @@ int janus_conv1d_pack(const float* w, uint16_t* packed, int Cin, int Cout, int t
  * transposed=1: ConvTranspose1d(Cin, Cout, 2*stride, stride, padding) (taps ignored).
  * y = post_act(conv(pre_act(x)) + bias); y += res (fp16 [B][T_out][Cout], may be NULL,
  * res_bs = batch stride in elements, 0 to broadcast); out = (accumulate ? out : 0) + scale*y.
+ * (pre_act, post_act) is one of (NONE, NONE), (SILU, NONE), (SILU, SILU), (NONE, GELU) —
+ * the pairs of the Whisper stem and the generator, compiled in; others return an error.
  */
 int janus_conv1d_f16(const uint16_t* in, int batch, int T_in, int Cin, const uint16_t* packed,
                      const float* bias, uint16_t* out, int T_out, int Cout, int taps, int stride,

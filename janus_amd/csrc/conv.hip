@@ -80,20 +80,14 @@ __device__ __forceinline__ float act_apply(float x) {
   else return x;
 }
 
-__device__ __forceinline__ float act_rt(int act, float x) {
-  switch (act) {
-    case ACT_SILU: return silu(x);
-    case ACT_GELU: return gelu_erf(x);
-    case ACT_TANH: return tanhf(x);
-    default: return x;
-  }
-}
 
-template <int BM, int BN, int WMT, int WNT, int CK>
+// PRE / POST: compile-time activations (ACT_*), so staging and epilogue carry no
+// per-element dispatch.
+template <int BM, int BN, int WMT, int WNT, int CK, int PRE, int POST>
 __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
   constexpr int KB = kConvKB, TPG = KB / CK;
-  constexpr int LI = CK + 8;   // input row stride in halves (odd multiple of 16 B)
-  constexpr int LW = KB + 8;   // weight row stride
+  constexpr int LI = frag_pitch(CK);   // input row stride in halves (conflict-free b128)
+  constexpr int LW = frag_pitch(KB);   // weight row stride
   constexpr int WN = BN / (16 * WNT);
   static_assert((BM / (16 * WMT)) * WN == 4, "4 waves");
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
@@ -139,6 +133,41 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
       }
     }
   };
+  // Input staging: every thread issues all of its loads for a channel chunk before any
+  // LDS store (NLD 16-byte loads in flight), so one HBM latency is paid per chunk instead
+  // of one per row group. With several chunks the next chunk's rows are loaded into
+  // registers while the current chunk computes.
+  constexpr int PER_ROW = CK / 8;
+  constexpr int NLD = ((BM + 64) * PER_ROW + 255) / 256;
+  const bool batched = nrows * PER_ROW <= NLD * 256;
+  uint4 pf[NLD];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / PER_ROW, cc = idx % PER_ROW;
+      const int gr = row_base + row;
+      pf[i] = (row < nrows && gr >= 0 && gr < a.T_in)
+                  ? *reinterpret_cast<const uint4*>(inb + (int64_t)gr * a.Cin + c * CK + cc * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / PER_ROW, cc = idx % PER_ROW;
+      if (row < nrows) {
+        uint4 v = pf[i];
+        if constexpr (PRE != ACT_NONE) {
+          _Float16* hv = reinterpret_cast<_Float16*>(&v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = (_Float16)act_apply<PRE>((float)hv[j]);
+        }
+        *reinterpret_cast<uint4*>(sIn + row * LI + cc * 8) = v;
+      }
+    }
+  };
   auto stage_input = [&](int c) {
     const int per_row = CK / 8;
     for (int idx = tid; idx < nrows * per_row; idx += 256) {
@@ -147,10 +176,10 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (gr >= 0 && gr < a.T_in) {
         v = *reinterpret_cast<const uint4*>(inb + (int64_t)gr * a.Cin + c * CK + cc * 8);
-        if (a.pre_act != ACT_NONE) {
+        if constexpr (PRE != ACT_NONE) {
           _Float16* hv = reinterpret_cast<_Float16*>(&v);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) hv[j] = (_Float16)act_rt(a.pre_act, (float)hv[j]);
+          for (int j = 0; j < 8; ++j) hv[j] = (_Float16)act_apply<PRE>((float)hv[j]);
         }
       }
       *reinterpret_cast<uint4*>(sIn + row * LI + cc * 8) = v;
@@ -163,35 +192,39 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
 #pragma unroll
     for (int n = 0; n < WNT; ++n) acc[m][n] = zero_f32x4();
 
+  // per-thread fragment addressing (lane -> row lane&15, k chunk 8*(lane>>4))
+  const int kq = 8 * (lane >> 4);
+  const int a_mstep = a.in_stride * LI;                              // one output row
+  const int a_off = (wm * WMT * 16 + (lane & 15)) * a_mstep;
+  const int b_off = (wn * WNT * 16 + (lane & 15)) * LW;
   const int nkb = chunks * groups;
+  if (batched) load_chunk(0);
   wload(0, 0);
   wstore(0);
   for (int kbi = 0; kbi < nkb; ++kbi) {
     const int c = kbi / groups, g = kbi % groups;
     if (g == 0) {
       __syncthreads();  // previous chunk's input tile fully consumed
-      stage_input(c);
+      if (batched) store_chunk();
+      else stage_input(c);
     }
     __syncthreads();    // input tile + weights[kbi&1] visible
+    if (batched && g == 0 && c + 1 < chunks) load_chunk(c + 1);  // lands during this chunk
     if (kbi + 1 < nkb) wload((kbi + 1) / groups, (kbi + 1) % groups);
-    const _Float16* w_cur = sW + (kbi & 1) * BN * LW;
+    const _Float16* w_cur = sW + (kbi & 1) * BN * LW + b_off;
 #pragma unroll
     for (int ks = 0; ks < KB / 32; ++ks) {
-      const int kk = ks * 32 + 8 * (lane >> 4);
+      const int kk = ks * 32 + kq;
       const int tap = g * TPG + kk / CK;
-      const int ci = kk % CK;
       const bool tap_ok = tap < a.taps;
-      const int lrow_off = tap * a.dil - lo_tap;
+      const _Float16* ap = sIn + a_off + (tap * a.dil - lo_tap) * LI + kk % CK;
       half8 av[WMT], bv[WNT];
 #pragma unroll
-      for (int m = 0; m < WMT; ++m) {
-        const int r = wm * WMT * 16 + m * 16 + (lane & 15);
-        av[m] = tap_ok ? *reinterpret_cast<const half8*>(sIn + (r * a.in_stride + lrow_off) * LI + ci)
-                       : zero_half8();
-      }
+      for (int m = 0; m < WMT; ++m)
+        av[m] = tap_ok ? *reinterpret_cast<const half8*>(ap + m * 16 * a_mstep) : zero_half8();
 #pragma unroll
       for (int n = 0; n < WNT; ++n)
-        bv[n] = *reinterpret_cast<const half8*>(w_cur + (wn * WNT * 16 + n * 16 + (lane & 15)) * LW + kk);
+        bv[n] = *reinterpret_cast<const half8*>(w_cur + n * 16 * LW + kk);
 #pragma unroll
       for (int m = 0; m < WMT; ++m)
 #pragma unroll
@@ -216,54 +249,60 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int rl = wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + rr;
-        sE[rl * ES + cl] = act_rt(a.post_act, acc[m][n][rr] + bias);
+        sE[rl * ES + cl] = act_apply<POST>(acc[m][n][rr] + bias);
       }
   }
   __syncthreads();
   _Float16* outb = a.out + (int64_t)b * a.out_bs;
   const _Float16* resb = a.res ? a.res + (int64_t)b * a.res_bs : nullptr;
   constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
-  for (int idx = tid; idx < BM * CPR; idx += 256) {
+  constexpr int NE = BM * CPR / 256;
+  static_assert(BM * CPR % 256 == 0, "epilogue chunks");
+  // all residual / accumulate loads of the thread first (one latency), then the math
+  uint4 rq[NE], pq[NE];
+  int64_t oo[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int idx = tid + i * 256;
     const int rl = idx / CPR, cg = (idx % CPR) * 8;
     const int r = r0 + rl, co = co0 + cg;
-    if (r >= a.n_rows || co >= a.Cout) continue;
     const int t = r * a.out_stride + a.out_off + ph;
-    if (t < 0 || t >= a.T_out) continue;
-    const int64_t o = (int64_t)t * a.Cout + co;
-    float v[8];
+    const bool ok = r < a.n_rows && co < a.Cout && t >= 0 && t < a.T_out;
+    oo[i] = ok ? (int64_t)t * a.Cout + co : -1;
+    rq[i] = (ok && resb) ? *reinterpret_cast<const uint4*>(resb + oo[i]) : make_uint4(0, 0, 0, 0);
+    pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(outb + oo[i])
+                                 : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    if (oo[i] < 0) continue;
+    const int idx = tid + i * 256;
+    const int rl = idx / CPR, cg = (idx % CPR) * 8;
     const float4 v0 = *reinterpret_cast<const float4*>(sE + rl * ES + cg);
     const float4 v1 = *reinterpret_cast<const float4*>(sE + rl * ES + cg + 4);
-    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
-    v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
-    if (resb) {
-      const half8 rv = *reinterpret_cast<const half8*>(resb + o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= a.out_scale;
-    if (a.accumulate) {
-      const half8 pv = *reinterpret_cast<const half8*>(outb + o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += (float)pv[j];
-    }
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const half8 rv = *reinterpret_cast<const half8*>(&rq[i]);
+    const half8 pv = *reinterpret_cast<const half8*>(&pq[i]);
     half8 hv;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) hv[j] = (_Float16)v[j];
-    *reinterpret_cast<half8*>(outb + o) = hv;
+    for (int j = 0; j < 8; ++j) {
+      // y = scale * (conv + res) (+ out): res/pv are zero when absent
+      hv[j] = (_Float16)((v[j] + (float)rv[j]) * a.out_scale + (float)pv[j]);
+    }
+    *reinterpret_cast<half8*>(outb + oo[i]) = hv;
   }
 }
 
-template <int BM, int BN, int WMT, int WNT, int CK>
+template <int BM, int BN, int WMT, int WNT, int CK, int PRE, int POST>
 static void conv_cfg(const ConvArgs& a, hipStream_t s) {
-  constexpr int LI = CK + 8, LW = kConvKB + 8;
+  constexpr int LI = frag_pitch(CK), LW = frag_pitch(kConvKB);
   const int rows_max = (BM - 1) * a.in_stride + std::abs((a.taps - 1) * a.dil) + 1;
   const size_t lds_loop = (size_t)rows_max * LI * 2 + 2 * (size_t)BN * LW * 2;
   const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   const size_t lds = lds_loop > lds_epi ? lds_loop : lds_epi;
   JANUS_CHECK(lds <= 160 * 1024, "conv: LDS tile too large (" + std::to_string(lds) + " B)");
   const int blocks = (int)(cdiv(a.n_rows, BM) * cdiv(a.Cout, BN));
-  auto kern = conv_kernel<BM, BN, WMT, WNT, CK>;
+  auto kern = conv_kernel<BM, BN, WMT, WNT, CK, PRE, POST>;
   static bool attr_set = false;
   if (!attr_set) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -274,12 +313,23 @@ static void conv_cfg(const ConvArgs& a, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
+template <int BM, int BN, int WMT, int WNT, int CK>
+static void conv_act(const ConvArgs& a, hipStream_t s) {
+  // the (pre, post) pairs the Whisper stem and the Firefly-GAN generator use
+  if (a.pre_act == ACT_NONE && a.post_act == ACT_NONE) conv_cfg<BM, BN, WMT, WNT, CK, ACT_NONE, ACT_NONE>(a, s);
+  else if (a.pre_act == ACT_SILU && a.post_act == ACT_NONE) conv_cfg<BM, BN, WMT, WNT, CK, ACT_SILU, ACT_NONE>(a, s);
+  else if (a.pre_act == ACT_SILU && a.post_act == ACT_SILU) conv_cfg<BM, BN, WMT, WNT, CK, ACT_SILU, ACT_SILU>(a, s);
+  else if (a.pre_act == ACT_NONE && a.post_act == ACT_GELU) conv_cfg<BM, BN, WMT, WNT, CK, ACT_NONE, ACT_GELU>(a, s);
+  else throw Error("conv: unsupported (pre_act, post_act) = (" + std::to_string(a.pre_act) + ", " +
+                   std::to_string(a.post_act) + ")");
+}
+
 template <int BM, int BN, int WMT, int WNT>
 static void conv_ck(const ConvArgs& a, hipStream_t s) {
   const ConvPack g = conv_pack_geometry(a.Cin, a.Cout, a.taps);
-  if (g.ck == 64) conv_cfg<BM, BN, WMT, WNT, 64>(a, s);
-  else if (g.ck == 32) conv_cfg<BM, BN, WMT, WNT, 32>(a, s);
-  else conv_cfg<BM, BN, WMT, WNT, 16>(a, s);
+  if (g.ck == 64) conv_act<BM, BN, WMT, WNT, 64>(a, s);
+  else if (g.ck == 32) conv_act<BM, BN, WMT, WNT, 32>(a, s);
+  else conv_act<BM, BN, WMT, WNT, 16>(a, s);
 }
 
 void conv_launch(const ConvArgs& a, hipStream_t s) {

@@ -38,18 +38,48 @@ void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t 
 }
 
 // x[b][:] = tok_emb[tokens[b][pos]] + pos_emb[pos]   (fp32 residual stream)
-__global__ void embed_kernel(const _Float16* __restrict__ tok_emb, const float* __restrict__ pos_emb,
-                             const int32_t* __restrict__ tokens, int ld_tokens, int pos, int d,
-                             float* __restrict__ x) {
+// 16-column LayerNorm piece (sum, M2 about the piece mean) of 16 values spread two per
+// lane over 8 aligned lanes; every lane of the group returns it.
+__device__ __forceinline__ float2 ln_piece8x2(float v0, float v1) {
+  float s = v0 + v1;
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  s += __shfl_xor(s, 4);
+  const float m = s * (1.0f / 16.0f);
+  float q = (v0 - m) * (v0 - m) + (v1 - m) * (v1 - m);
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  q += __shfl_xor(q, 4);
+  return make_float2(s, q);
+}
+
+__global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__ tok_emb,
+                                                    const float* __restrict__ pos_emb,
+                                                    const int32_t* __restrict__ tokens,
+                                                    int ld_tokens, int pos, int d,
+                                                    float* __restrict__ x,
+                                                    float2* __restrict__ part) {
   const int b = blockIdx.x;
   const int tok = tokens[(int64_t)b * ld_tokens + pos];
-  for (int i = threadIdx.x; i < d; i += blockDim.x)
-    x[(int64_t)b * d + i] = (float)tok_emb[(int64_t)tok * d + i] + pos_emb[(int64_t)pos * d + i];
+  for (int base = 0; base < d; base += 512) {
+    const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece
+    float v0 = 0.f, v1 = 0.f;
+    if (col < d) {
+      v0 = (float)tok_emb[(int64_t)tok * d + col] + pos_emb[(int64_t)pos * d + col];
+      v1 = (float)tok_emb[(int64_t)tok * d + col + 1] + pos_emb[(int64_t)pos * d + col + 1];
+      *reinterpret_cast<float2*>(x + (int64_t)b * d + col) = make_float2(v0, v1);
+    }
+    if (part) {
+      const float2 pc = ln_piece8x2(v0, v1);
+      if (col < d && (threadIdx.x & 7) == 0) part[(int64_t)b * (d / 16) + col / 16] = pc;
+    }
+  }
 }
 
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
-                  int ld_tokens, int pos, int d, float* x, int B, hipStream_t s) {
-  embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tokens, ld_tokens, pos, d, x);
+                  int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s) {
+  JANUS_CHECK(d % 16 == 0, "embed: d % 16 != 0");
+  embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tokens, ld_tokens, pos, d, x, part);
   JANUS_LAUNCH_CHECK();
 }
 

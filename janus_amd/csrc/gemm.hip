@@ -144,6 +144,10 @@ static void launch_cfg(int epi, const GemmArgs& p, hipStream_t s) {
 // the 4 waves split K and reduce through LDS, so an N = 512 projection still spreads
 // over 32 blocks and every weight byte is read once per step (weight-streaming bound).
 template <int EPI>
+__device__ __forceinline__ void skinny_epilogue(const GemmArgs& p, float (*red)[64][17], int col0,
+                                                int M, int N);
+
+template <int EPI>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
   __shared__ float red[4][64][17];
   const int M = p.M, N = p.N, K = p.K;
@@ -175,17 +179,49 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
   __syncthreads();
+  skinny_epilogue<EPI>(p, red, col0, M, N);
+}
+
+// Shared epilogue of the skinny kernels: thread i -> (row i>>4, col col0 + (i&15)), so
+// the 16 lanes of an aligned group hold one row's 16 columns (LayerNorm pieces).
+template <int EPI>
+__device__ __forceinline__ void skinny_epilogue(const GemmArgs& p, float (*red)[64][17], int col0,
+                                                int M, int N) {
+  const int tid = threadIdx.x;
   for (int i = tid; i < 64 * 16; i += 256) {
     const int row = i >> 4, c = i & 15, col = col0 + c;
-    if (row >= M || col >= N) continue;
+    const bool ok = row < M && col < N;
     float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
-    v += p.bias ? p.bias[col] : 0.0f;
+    v += (p.bias && ok) ? p.bias[col] : 0.0f;
+    if constexpr (EPI == EPI_RESID_F32) {
+      const float y = ok ? p.R[(int64_t)row * p.ldr + col] + v : 0.0f;
+      if (ok) static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = y;
+      if (p.ln_part) {  // uniform branch: all 16 lanes of the row group take part
+        float sm = y;
+        sm += __shfl_xor(sm, 1); sm += __shfl_xor(sm, 2);
+        sm += __shfl_xor(sm, 4); sm += __shfl_xor(sm, 8);
+        const float mu = sm * (1.0f / 16.0f);
+        float q = (y - mu) * (y - mu);
+        q += __shfl_xor(q, 1); q += __shfl_xor(q, 2);
+        q += __shfl_xor(q, 4); q += __shfl_xor(q, 8);
+        if (c == 0 && row < M) p.ln_part[(int64_t)row * (N / 16) + col0 / 16] = make_float2(sm, q);
+      }
+      continue;
+    }
+    if (!ok) continue;
     if constexpr (EPI == EPI_F16) {
       static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
     } else if constexpr (EPI == EPI_GELU_F16) {
       static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
-    } else if constexpr (EPI == EPI_RESID_F32) {
-      static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = p.R[(int64_t)row * p.ldr + col] + v;
+    } else if constexpr (EPI == EPI_QKV) {
+      // q -> C; k, v -> cache rows (row * n_ctx + pos); R/ldr carry the cache pointers
+      const int dq = p.qkv_d;
+      if (col < dq) {
+        static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+      } else {
+        _Float16* cache = col < 2 * dq ? p.kc : p.vc;
+        cache[((int64_t)row * p.n_ctx + p.pos) * dq + (col % dq)] = (_Float16)v;
+      }
     } else {
       static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
     }
@@ -199,16 +235,18 @@ static void launch_skinny(int epi, const GemmArgs& p, hipStream_t s) {
     case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
     case EPI_RESID_F32: gemm_skinny_kernel<EPI_RESID_F32><<<blocks, 256, 0, s>>>(p); break;
     case EPI_F32: gemm_skinny_kernel<EPI_F32><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_QKV: gemm_skinny_kernel<EPI_QKV><<<blocks, 256, 0, s>>>(p); break;
     default: throw Error("bad gemm epilogue");
   }
   JANUS_LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------- skinny M + fused LN
-// C = epi( LN(x)[M,K] · W[N,K]^T + bias ), M <= 64, x fp32 (the residual stream): the
-// block recomputes the 64 rows' LayerNorm statistics (two-pass, eps as given) and
-// normalises each A fragment on the fly, so decoder pre-LN blocks need no separate
-// LayerNorm launch. EPI_QKV writes q to C and k/v straight into the KV cache rows.
+// C = epi( LN(x)[M,K] · W[N,K]^T + bias ), M <= 64, x fp32 (the residual stream). The
+// row statistics come from the K/16 LayerNorm pieces its producer wrote (SkinnyLnArgs):
+// thread (row tid/4, quarter tid%4) combines a quarter of the pieces, four lanes finish
+// the row (Chan: M2 = sum M2_i + 16 * sum (mu_i - mean)^2). A fragments are normalised
+// on load. Replaces the LayerNorm launch in front of every decoder projection.
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(SkinnyLnArgs p) {
   __shared__ float red[4][64][17];
@@ -216,39 +254,55 @@ __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(SkinnyLnArgs p) {
   const int M = p.M, N = p.N, K = p.K;
   const int col0 = blockIdx.x * 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // row statistics: wave w -> rows 16w .. 16w+15
-  for (int i = 0; i < 16; ++i) {
-    const int r = w * 16 + i;
-    if (r >= M) break;
-    const float* xr = p.x + (int64_t)r * p.ldx;
-    float sm = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + k);
-      sm += v.x + v.y + v.z + v.w;
-    }
-    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
-    const float mean = sm / K;
-    float sq = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + k);
-      const float a0 = v.x - mean, a1 = v.y - mean, a2 = v.z - mean, a3 = v.w - mean;
-      sq += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-    }
-    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
-    if (lane == 0) { s_mean[r] = mean; s_rstd[r] = rsqrtf(sq / K + p.eps); }
-  }
-  __syncthreads();
   const int kq = ((K + 3) / 4 + 31) / 32 * 32;
   const int kbeg = w * kq, kend = min(K, kbeg + kq);
+  const int bcol = col0 + (lane & 15);
+  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
+  // the first weight fragment does not depend on the statistics: start it now
+  half8 b_next = (kbeg + 8 * (lane >> 4) < kend && bcol < N)
+                     ? *reinterpret_cast<const half8*>(wrow + kbeg + 8 * (lane >> 4)) : zero_half8();
+  {
+    const int r = tid >> 2, qd = tid & 3, np = K / 16;
+    float2 pc[8];
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int g = qd + 4 * j;
+      pc[j] = (r < M && g < np) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+      sm += pc[j].x;
+    }
+    for (int g = qd + 32; g < np; g += 4) sm += (r < M) ? p.part[(int64_t)r * np + g].x : 0.f;
+    sm += __shfl_xor(sm, 1);
+    sm += __shfl_xor(sm, 2);
+    const float mean = sm / K;
+    float m2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int g = qd + 4 * j;
+      if (g < np) {
+        const float dm = pc[j].x * (1.0f / 16.0f) - mean;
+        m2 += pc[j].y + 16.0f * dm * dm;
+      }
+    }
+    for (int g = qd + 32; g < np; g += 4) {
+      const float2 q = (r < M) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+      const float dm = q.x * (1.0f / 16.0f) - mean;
+      m2 += q.y + 16.0f * dm * dm;
+    }
+    m2 += __shfl_xor(m2, 1);
+    m2 += __shfl_xor(m2, 2);
+    if (qd == 0) { s_mean[r] = mean; s_rstd[r] = rsqrtf(m2 / K + p.eps); }
+  }
+  __syncthreads();
   f32x4 acc[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
-  const int bcol = col0 + (lane & 15);
-  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
   for (int k0 = kbeg; k0 < kend; k0 += 32) {
     const int kk = k0 + 8 * (lane >> 4);
     const bool kok = kk < kend;
-    const half8 b = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+    const half8 b = b_next;
+    const int kn = kk + 32;
+    b_next = (kn < kend && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kn) : zero_half8();
     float g[8], be[8];
     if (kok) {
       const float4 g0 = *reinterpret_cast<const float4*>(p.gamma + kk);
@@ -281,29 +335,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(SkinnyLnArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
   __syncthreads();
-  for (int i = tid; i < 64 * 16; i += 256) {
-    const int row = i >> 4, c = i & 15, col = col0 + c;
-    if (row >= M || col >= N) continue;
-    float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
-    v += p.bias ? p.bias[col] : 0.0f;
-    if constexpr (EPI == EPI_GELU_F16) {
-      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
-    } else if constexpr (EPI == EPI_QKV) {
-      const int d = p.qkv_d;
-      if (col < d) {
-        static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
-      } else {
-        _Float16* cache = col < 2 * d ? p.kc : p.vc;
-        cache[((int64_t)row * p.n_ctx + p.pos) * d + (col % d)] = (_Float16)v;
-      }
-    } else {
-      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
-    }
-  }
+  GemmArgs q{};
+  q.bias = p.bias; q.C = p.C; q.ldc = p.ldc;
+  q.kc = p.kc; q.vc = p.vc; q.pos = p.pos; q.n_ctx = p.n_ctx; q.qkv_d = p.qkv_d;
+  skinny_epilogue<EPI>(q, red, col0, M, N);
 }
 
 void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& p, hipStream_t s) {
-  JANUS_CHECK(p.M <= 64 && p.K % 8 == 0 && p.ldx % 4 == 0, "skinny LN gemm: M <= 64, K % 8 == 0");
+  JANUS_CHECK(p.M <= 64 && p.K % 16 == 0 && p.K <= 2048 && p.ldx % 4 == 0 && p.part,
+              "skinny LN gemm: M <= 64, K % 16 == 0, K <= 2048, LayerNorm pieces required");
   if (p.M <= 0 || p.N <= 0) return;
   const int blocks = (p.N + 15) / 16;
   switch (epi) {
@@ -319,6 +359,10 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
   JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");
   if (p.M <= 0 || p.N <= 0) return;
+  JANUS_CHECK(p.M <= 64 || (epi != EPI_QKV && !p.ln_part),
+              "gemm: the KV-cache and LayerNorm-piece epilogues need M <= 64");
+  JANUS_CHECK(!p.ln_part || (epi == EPI_RESID_F32 && p.N % 16 == 0),
+              "gemm: LayerNorm pieces come from a RESID epilogue with N % 16 == 0");
   if (p.M <= 64) launch_skinny(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }

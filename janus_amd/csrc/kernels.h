@@ -14,13 +14,24 @@ struct GemmArgs {
   void* C; int64_t ldc;            // fp16 or fp32 by epilogue
   const float* R; int64_t ldr;     // fp32 residual (EPI_RESID_F32), may alias C
   int M, N, K;
+  // EPI_QKV (M <= 64 only): columns [0,d) -> C, [d,2d) -> kc, [2d,3d) -> vc at row pos
+  _Float16* kc = nullptr; _Float16* vc = nullptr; int pos = 0, n_ctx = 0, qkv_d = 0;
+  // EPI_RESID_F32 (M <= 64 only): also write the LayerNorm pieces of the new rows,
+  // ln_part[row][col / 16] (see SkinnyLnArgs)
+  float2* ln_part = nullptr;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
 
 // M <= 64 GEMM with the LayerNorm of its fp32 A operand fused (decoder pre-LN blocks).
 // EPI_QKV: columns [0, d) -> C, [d, 2d) -> kc[row][pos], [2d, 3d) -> vc[row][pos].
+// LayerNorm fused into the consumer through row-statistic PIECES: the kernel that
+// produces a residual-stream row writes, per 16-column group g, part[row][g] =
+// (sum, M2 about the group mean); the consumer combines the K/16 pieces of a row
+// (Chan's parallel variance) and normalises its A fragments on load. No separate
+// LayerNorm launch, no atomics, deterministic.
 struct SkinnyLnArgs {
   const float* x; int64_t ldx;
+  const float2* part;               // [M][K/16] pieces of x's rows
   const float* gamma; const float* beta; float eps;
   const _Float16* W; int64_t ldw;
   const float* bias;

@@ -21,7 +21,11 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the
+// ~10-instruction IEEE division: SiLU runs on every staged vocoder activation.
+__device__ __forceinline__ float silu(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
 
 __device__ __forceinline__ half8 zero_half8() {
   half8 z;
@@ -31,6 +35,17 @@ __device__ __forceinline__ half8 zero_half8() {
 }
 
 __device__ __forceinline__ f32x4 zero_f32x4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// LDS row pitch (in halves) for tiles read as MFMA fragments with ds_read_b128: a pitch
+// of 16*P bytes with P % 4 == 2 puts the 16 lanes of every gfx950 b128 lane group
+// ({0-3,12-15,20-27}, ...: rows r, r+12.. of one 16-B column chunk and rows r+4.. of the
+// next) on 16 distinct 4-bank slots — conflict-free. (P % 4 == 1, e.g. the classic
+// "+8 halves" pad of a 64-half row, is 2-way.)
+__host__ __device__ constexpr int frag_pitch(int min_halves) {
+  int p = (min_halves + 7) / 8;
+  while (p % 4 != 2) ++p;
+  return p * 8;
+}
 
 // XCD-aware remap of a 1-D block index (bijective; MI355X deals blocks round-robin
 // over 8 XCDs, so consecutive logical tiles are placed on one XCD's L2).

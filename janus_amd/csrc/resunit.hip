@@ -10,6 +10,7 @@
 // matrices stay in LDS for the block. HBM traffic per unit: read x once (+ the residual
 // re-read, L2-hot), write out once — half of two separate conv launches.
 #include <algorithm>
+#include <cstdlib>
 #include "mfma.h"
 #include "kernels.h"
 
@@ -34,13 +35,16 @@ void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
 
 template <int C, int BM>
 struct ResUnitGeo {
-  static constexpr int LI = C + 8;                          // halves per activation row
+  // halves per activation row: conflict-free fragment pitch for C = 32; C = 16 keeps the
+  // 48-B pitch (its sS/sX store pattern measured 10% faster than the 32-B one)
+  static constexpr int LI = C == 16 ? 24 : frag_pitch(C);
   static constexpr int CPR = C / 8;                         // 16-byte chunks per row
   static constexpr int R0MAX = BM + 10 + 50;                // k <= 11, d <= 5
   static constexpr int NPF = (R0MAX * CPR + 255) / 256;     // prefetch uint4 per thread
   static constexpr int MT1 = ((BM + 10 + 15) / 16 + 3) / 4; // c1 M-tiles per wave
   static constexpr int MT2 = BM / 64;                       // c2 M-tiles per wave
   static constexpr int ES = C + 4;                          // fp32 epilogue row stride
+  static constexpr int NE = BM * CPR / 256;                 // epilogue uint4 per thread
 };
 
 // Persistent: each block loads both weight matrices into LDS once, then walks tiles
@@ -55,11 +59,12 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
   const int k = a.k, d = a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2, R0 = R1 + 2 * p1;
-  const int LW = KP + 8;
+  const int LW = frag_pitch(KP);
   _Float16* sX = smem;                        // [R0][LI]   silu(x)
   _Float16* sS = sX + R0 * LI;                // [R1p][LI]  silu(c1(.) + b1)
   float* sE = reinterpret_cast<float*>(smem); // [BM][ES] epilogue tile (aliases sX/sS)
-  _Float16* sW1 = smem + act_halves;          // [C][LW]
+  _Float16* sR = smem + act_halves;           // [BM][LI]   raw x (the unit's residual)
+  _Float16* sW1 = sR + BM * LI;               // [C][LW]
   _Float16* sW2 = sW1 + C * LW;               // [C][LW]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 
@@ -90,7 +95,6 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int b = tile / tiles_per_utt, t0 = (tile % tiles_per_utt) * BM;
-    const _Float16* xb = a.x + (int64_t)b * T * C;
     __syncthreads();  // previous tile's epilogue reads of sE are done (and W staged)
 #pragma unroll
     for (int i = 0; i < G::NPF; ++i) {
@@ -98,6 +102,8 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+        const int rr = r - p2 - p1;
+        if (rr >= 0 && rr < BM) *reinterpret_cast<half8*>(sR + rr * LI + cc * 8) = v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
@@ -105,6 +111,17 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
     }
     __syncthreads();
     prefetch(tile + gridDim.x);  // in flight during this tile's compute
+    _Float16* ob = a.out + (int64_t)b * T * C;
+    uint4 acc_in[G::NE];         // accumulate target, also in flight during compute
+    if (a.accumulate) {
+#pragma unroll
+      for (int i = 0; i < G::NE; ++i) {
+        const int idx = tid + i * 256;
+        const int r = idx / CPR, cg = (idx % CPR) * 8;
+        acc_in[i] = t0 + r < T ? *reinterpret_cast<const uint4*>(ob + (int64_t)(t0 + r) * C + cg)
+                               : make_uint4(0, 0, 0, 0);
+      }
+    }
 
     // ---- c1 over R1 rows (c1 row r <-> time t0 - p2 + r): A = sX[r + tap*d]
     {
@@ -188,18 +205,18 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
         }
       }
     __syncthreads();
-    _Float16* ob = a.out + (int64_t)b * T * C;
-    for (int idx = tid; idx < BM * CPR; idx += 256) {
+#pragma unroll
+    for (int i = 0; i < G::NE; ++i) {
+      const int idx = tid + i * 256;
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const int t = t0 + r;
       if (t >= T) continue;
       const int64_t o = (int64_t)t * C + cg;
-      const half8 xv = *reinterpret_cast<const half8*>(xb + o);
+      const half8 xv = *reinterpret_cast<const half8*>(sR + r * LI + cg);
       const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
       const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
       const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      half8 pv;
-      if (a.accumulate) pv = *reinterpret_cast<const half8*>(ob + o);
+      const half8 pv = *reinterpret_cast<const half8*>(&acc_in[i]);
       half8 hv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -221,7 +238,7 @@ static void resunit_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_CHECK(R0 <= G::R0MAX, "resunit: (k-1)*(d+1) exceeds the prefetch budget");
   const int act = std::max((R0 + R1p) * G::LI, BM * G::ES * 2);  // halves
   const int act_halves = (act + 7) / 8 * 8;
-  const size_t lds = ((size_t)act_halves + 2 * (size_t)C * (KP + 8)) * 2;
+  const size_t lds = ((size_t)act_halves + (size_t)BM * G::LI + 2 * (size_t)C * frag_pitch(KP)) * 2;
   JANUS_CHECK(lds <= 160 * 1024, "resunit: LDS tile too large");
   auto kern = resunit_kernel<C, BM>;
   static bool attr = false;
@@ -232,7 +249,7 @@ static void resunit_cfg(const ResUnitArgs& a, hipStream_t s) {
   }
   const int tiles_per_utt = (a.T + BM - 1) / BM;
   const int n_tiles = tiles_per_utt * a.B;
-  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / lds)));
   const int grid = std::min(n_tiles, 256 * per_cu);
   kern<<<grid, 256, lds, s>>>(a, KP, tiles_per_utt, n_tiles, act_halves);
   JANUS_LAUNCH_CHECK();
@@ -244,8 +261,18 @@ void resunit_launch(const ResUnitArgs& a, hipStream_t s) {
   JANUS_CHECK(resunit_supported(a.C, a.k), "resunit: C must be 16 or 32, k odd <= 11");
   JANUS_CHECK(a.x != a.out, "resunit: out must not alias x");
   if (a.B <= 0 || a.T <= 0) return;
-  if (a.C == 16) resunit_cfg<16, 512>(a, s);
-  else resunit_cfg<32, 128>(a, s);
+  // tile rows per block (JANUS_RU_BM overrides, for tuning sweeps)
+  static const int bm = [] { const char* e = std::getenv("JANUS_RU_BM"); return e ? std::atoi(e) : 0; }();
+  // measured (B=16, 30 s, accumulate): C16 BM 256 beats 512 by 1.8x (3 blocks/CU vs 2);
+  // C32 k<=7 is best at BM 128, k 11 at BM 64 (1.84 vs 2.23 ms)
+  if (a.C == 16) {
+    if (bm == 512) resunit_cfg<16, 512>(a, s);
+    else resunit_cfg<16, 256>(a, s);
+  } else {
+    if (bm == 256) resunit_cfg<32, 256>(a, s);
+    else if (bm == 64 || (bm == 0 && a.k > 7)) resunit_cfg<32, 64>(a, s);
+    else resunit_cfg<32, 128>(a, s);
+  }
 }
 
 }  // namespace janus

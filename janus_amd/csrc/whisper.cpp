@@ -42,7 +42,7 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp;
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t side = nullptr;  // graph capture needs a non-null stream
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -283,18 +283,27 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
   const int sample_begin = opt->prompt_len;  // index of the first sampled token
+  // B <= 64: LayerNorm rides on the projections (row-statistic pieces written by the
+  // producer of each residual row, normalised on load by the consumer GEMM)
   const bool fused_ln = B <= 64 && std::getenv("JANUS_NO_FUSED_LN") == nullptr;
-  auto lnargs = [&](const float* xin, const float* g, const float* bta, const _Float16* W,
-                    const float* bias, void* C, int64_t ldc, int N, _Float16* kcp, _Float16* vcp,
-                    int pos) {
+  w->d_lnp.ensure(sizeof(float2) * B * (d / 16));
+  float2* lnp = w->d_lnp.as<float2>();
+  auto lnargs = [&](const float* g, const float* bta, const _Float16* W, const float* bias,
+                    void* C, int64_t ldc, int N, _Float16* kcp, _Float16* vcp, int pos) {
     SkinnyLnArgs p;
-    p.x = xin; p.ldx = d; p.gamma = g; p.beta = bta; p.eps = 1e-5f; p.W = W; p.ldw = d;
+    p.x = x; p.ldx = d; p.part = lnp; p.gamma = g; p.beta = bta; p.eps = 1e-5f; p.W = W; p.ldw = d;
     p.bias = bias; p.C = C; p.ldc = ldc; p.M = B; p.N = N; p.K = d;
     p.kc = kcp; p.vc = vcp; p.pos = pos; p.n_ctx = NC; p.qkv_d = d;
     return p;
   };
+  auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias) {
+    GemmArgs g = gargs(A, K, W.as<_Float16>(), K, bias, x, d, B, d, K, x, d);
+    if (fused_ln) g.ln_part = lnp;
+    gemm_launch(EPI_RESID_F32, g, s);
+  };
   auto step = [&](int pos) {
-    embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x, B, s);
+    embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
+                 fused_ln ? lnp : nullptr, B, s);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = w->d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
@@ -302,18 +311,24 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
       _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
       if (fused_ln) {
-        gemm_skinny_ln_launch(EPI_QKV, lnargs(x, L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
+        gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
         layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
-        gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
-        kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
+        if (B <= 64) {
+          GemmArgs g = gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d);
+          g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
+          gemm_launch(EPI_QKV, g, s);
+        } else {
+          gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
+          kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
+        }
       }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s);
-      gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, x, d, B, d, d, x, d), s);
+      resid(o, d, L.wo, L.bo);
       if (fused_ln) {
-        gemm_skinny_ln_launch(EPI_F16, lnargs(x, L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
+        gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
                                               nullptr, nullptr, pos), s);
       } else {
         layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
@@ -321,15 +336,15 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       }
       decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                     part_ml, s);
-      gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo_c.as<_Float16>(), d, L.bo_c, x, d, B, d, d, x, d), s);
+      resid(o, d, L.wo_c, L.bo_c);
       if (fused_ln) {
-        gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(x, L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
+        gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
         layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
         gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
       }
-      gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, x, d, B, d, 4 * d, x, d), s);
+      resid(f, 4 * d, L.w2, L.b2);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
     layernorm_launch(x, w->params.get("decoder.layer_norm.weight", d),
@@ -346,7 +361,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
       (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
-      (int64_t)w->d_rules.p, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
+      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
   if (w->graphs.size() > 512) {

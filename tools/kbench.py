@@ -32,10 +32,16 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--units-only", action="store_true")
     a = ap.parse_args()
+    if a.units_only:
+        resunits(a.batch, a.reps)
+        return
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
     B = a.batch
+    if not a.only:
+        resunits(B, a.reps)
     for (name, Cin, Cout, taps, stride, pad, dil, tr, pre, post, use_res, T_in) in SHAPES:
         if a.only and a.only not in name:
             continue
@@ -89,7 +95,7 @@ def resunits(B, reps):
 
         def run():
             nat.call("janus_resunit_f16", x.data_ptr(), out.data_ptr(), p.data_ptr(), bias.data_ptr(),
-                     p.data_ptr(), bias.data_ptr(), B, T, C, k, d, 1.0, 0, s)
+                     p.data_ptr(), bias.data_ptr(), B, T, C, k, d, 1.0 / 3.0, 1, s)
         run()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -100,11 +106,10 @@ def resunits(B, reps):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         flops = 2 * 2.0 * C * C * k * T * B
-        byts = 2.0 * B * T * C * 3
+        byts = 2.0 * B * T * C * 3  # read x, read+write the ParallelBlock accumulator
         print(f"unit C{C} k{k} d{d} B={B} T={T:8d} {ms:8.3f} ms {flops / ms / 1e9:8.1f} TF/s "
               f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
     main()
-    resunits(16, 5)
