@@ -104,7 +104,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
 
   const int lo_tap = min(0, (a.taps - 1) * a.dil);
   const int row_base = r0 * a.in_stride + a.in_off + lo_tap;   // global input row of LDS row 0
-  const int nrows = (BM - 1) * a.in_stride + abs((a.taps - 1) * a.dil) + 1;
+  // rows staged: every tap of every k-group, including the zero-weight padding taps of
+  // the last group (TPG > 1), so fragment reads need no per-tap guard (host checks that
+  // transposed convs, dil < 0, have no padding taps)
+  const int nrows = (BM - 1) * a.in_stride +
+                    abs(((a.taps + TPG - 1) / TPG * TPG - 1) * a.dil) + 1;
   const int chunks = a.Cin / CK, groups = (a.taps + TPG - 1) / TPG;
   const _Float16* inb = a.in + (int64_t)b * a.in_bs;
   const _Float16* wph = a.w + (int64_t)ph * chunks * groups * a.Cout * KB;
@@ -216,12 +220,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
     for (int ks = 0; ks < KB / 32; ++ks) {
       const int kk = ks * 32 + kq;
       const int tap = g * TPG + kk / CK;
-      const bool tap_ok = tap < a.taps;
       const _Float16* ap = sIn + a_off + (tap * a.dil - lo_tap) * LI + kk % CK;
       half8 av[WMT], bv[WNT];
 #pragma unroll
       for (int m = 0; m < WMT; ++m)
-        av[m] = tap_ok ? *reinterpret_cast<const half8*>(ap + m * 16 * a_mstep) : zero_half8();
+        av[m] = *reinterpret_cast<const half8*>(ap + m * 16 * a_mstep);
 #pragma unroll
       for (int n = 0; n < WNT; ++n)
         bv[n] = *reinterpret_cast<const half8*>(w_cur + n * 16 * LW + kk);
@@ -296,7 +299,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
 template <int BM, int BN, int WMT, int WNT, int CK, int PRE, int POST>
 static void conv_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int LI = frag_pitch(CK), LW = frag_pitch(kConvKB);
-  const int rows_max = (BM - 1) * a.in_stride + std::abs((a.taps - 1) * a.dil) + 1;
+  constexpr int TPG = kConvKB / CK;
+  const int taps_padded = (a.taps + TPG - 1) / TPG * TPG;
+  JANUS_CHECK(a.dil > 0 || taps_padded == a.taps,
+              "conv: transposed conv with padding taps (Cin % 32 != 0) unsupported");
+  const int rows_max = (BM - 1) * a.in_stride + std::abs((taps_padded - 1) * a.dil) + 1;
   const size_t lds_loop = (size_t)rows_max * LI * 2 + 2 * (size_t)BN * LW * 2;
   const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   const size_t lds = lds_loop > lds_epi ? lds_loop : lds_epi;

@@ -7,8 +7,8 @@
 //
 // Tiling: BMxBNx64 block tile, 4 waves (each WMT x WNT 16x16 tiles), register-staged
 // double-buffered LDS (one barrier per 64-deep K step; next tile's global loads issued
-// before the current tile's MFMAs), rows padded by 16 B so the 16-lane ds_read_b128
-// groups are conflict-free, XCD-aware tile order (blocks sharing an A panel on one L2).
+// before the current tile's MFMAs), rows padded to a 160-B pitch so the ds_read_b128
+// lane groups are conflict-free (frag_pitch), XCD-aware tile order (blocks sharing an A panel on one L2).
 #include "mfma.h"
 #include "kernels.h"
 
@@ -16,7 +16,7 @@ namespace janus {
 
 template <int BM, int BN, int WMT, int WNT, int EPI>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
-  constexpr int BK = 64, LS = BK + 8;  // LDS row stride in halves (144 B = 16 B * 9)
+  constexpr int BK = 64, LS = frag_pitch(BK);  // LDS row stride (conflict-free b128 reads)
   constexpr int WN = BN / (16 * WNT);
   static_assert((BM / (16 * WMT)) * WN == 4, "4 waves per block");
   constexpr int KC = BK / 8;                  // 16-byte chunks per tile row
@@ -140,219 +140,242 @@ static void launch_cfg(int epi, const GemmArgs& p, hipStream_t s) {
 
 
 // ---------------------------------------------------------------- skinny M
-// M <= 64 (decoder steps: one row per utterance). Block = all 64 rows x 16 columns;
-// the 4 waves split K and reduce through LDS, so an N = 512 projection still spreads
-// over 32 blocks and every weight byte is read once per step (weight-streaming bound).
-template <int EPI>
-__device__ __forceinline__ void skinny_epilogue(const GemmArgs& p, float (*red)[64][17], int col0,
-                                                int M, int N);
+// M <= 64 (decoder steps: one row per utterance). These GEMMs are latency-bound (0.5-2 MB
+// of weights, 64 rows), so the design minimises dependent memory round trips: a block is
+// all 64 rows x 16 columns with 16 waves splitting K (an N = 512 projection still spreads
+// over 32 blocks and every weight byte is read once per step); each wave issues the loads
+// of up to G k-steps before its first MFMA (one k-step per wave at K = 512), the epilogue's
+// residual / bias loads are issued at kernel entry, and the 16 partial products are
+// reduced through LDS. LNA: A is the fp32 residual stream, LayerNorm-ed on load from the
+// row-statistic pieces its producer wrote (SkinnyLnArgs).
+struct SkinnyArgs {
+  const _Float16* A; int64_t lda;
+  const float* x; int64_t ldx; const float2* part; const float* gamma; const float* beta;
+  float eps;
+  const _Float16* W; int64_t ldw;
+  const float* bias;
+  void* C; int64_t ldc;
+  const float* R; int64_t ldr;
+  int M, N, K;
+  _Float16* kc; _Float16* vc; int pos, n_ctx, qkv_d;
+  float2* ln_part;
+};
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
-  __shared__ float red[4][64][17];
+constexpr int kSkWaves = 16;
+
+template <int EPI, bool LNA>
+__global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
+  constexpr int G = LNA ? 1 : 2;  // k-steps in flight per wave (128-VGPR budget at 1024 threads)
+  __shared__ float red[8][64][17];
+  __shared__ float s_mean[64], s_rstd[64];
   const int M = p.M, N = p.N, K = p.K;
   const int col0 = blockIdx.x * 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kq = ((K + 3) / 4 + 31) / 32 * 32;  // per-wave K slice, multiple of 32
+  const int kq = ((K + kSkWaves - 1) / kSkWaves + 31) / 32 * 32;
   const int kbeg = w * kq, kend = min(K, kbeg + kq);
+  const int bcol = col0 + (lane & 15);
+  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+
+  // epilogue operands independent of the product, in flight from the start
+  const int erow = tid >> 4, ec = tid & 15, ecol = col0 + ec;
+  const bool eok = erow < M && ecol < N;
+  float e_add = (p.bias && eok) ? p.bias[ecol] : 0.0f;
+  if constexpr (EPI == EPI_RESID_F32) e_add += eok ? p.R[(int64_t)erow * p.ldr + ecol] : 0.0f;
+
+  half8 bw[G];
+  half8 ah[LNA ? 1 : G][4];
+  float4 ax[LNA ? G : 1][4][2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int kk = k0 + 32 * g + kc8;
+      const bool ok = kk < kend;
+      bw[g] = (ok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int r = m * 16 + lr;
+        if constexpr (LNA) {
+          const float* xr = p.x + (int64_t)r * p.ldx + kk;
+          const bool rok = ok && r < M;
+          ax[g][m][0] = rok ? *reinterpret_cast<const float4*>(xr) : make_float4(0.f, 0.f, 0.f, 0.f);
+          ax[g][m][1] = rok ? *reinterpret_cast<const float4*>(xr + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          ah[g][m] = (ok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kk)
+                                   : zero_half8();
+        }
+      }
+    }
+  };
+  load(kbeg);
+
+  if constexpr (LNA) {
+    // row statistics from the producer's pieces: waves 0-3, thread = (row, quarter)
+    if (tid < 256) {
+      const int r = tid >> 2, qd = tid & 3, np = K / 16;
+      constexpr int NPQ = 12;  // pieces per thread held in registers (K <= 768)
+      float2 pc[NPQ];
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < NPQ; ++j) {
+        const int g = qd + 4 * j;
+        pc[j] = (r < M && g < np) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < NPQ; ++j) sm += pc[j].x;
+      for (int g = qd + 4 * NPQ; g < np; g += 4) sm += (r < M) ? p.part[(int64_t)r * np + g].x : 0.f;
+      sm += __shfl_xor(sm, 1);
+      sm += __shfl_xor(sm, 2);
+      const float mean = sm / K;
+      float m2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NPQ; ++j) {
+        if (qd + 4 * j < np) {
+          const float dm = pc[j].x * (1.0f / 16.0f) - mean;
+          m2 += pc[j].y + 16.0f * dm * dm;
+        }
+      }
+      for (int g = qd + 4 * NPQ; g < np; g += 4) {
+        const float2 q = (r < M) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+        const float dm = q.x * (1.0f / 16.0f) - mean;
+        m2 += q.y + 16.0f * dm * dm;
+      }
+      m2 += __shfl_xor(m2, 1);
+      m2 += __shfl_xor(m2, 2);
+      if (qd == 0) { s_mean[r] = mean; s_rstd[r] = rsqrtf(m2 / K + p.eps); }
+    }
+    __syncthreads();
+  }
+
   f32x4 acc[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
-  const int bcol = col0 + (lane & 15);
-  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
-
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const int kk = k0 + 8 * (lane >> 4);
-    const bool kok = kk < kend;
-    const half8 b = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
-    half8 a[4];
+  for (int k0 = kbeg; k0 < kend; k0 += 32 * G) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int r = m * 16 + (lane & 15);
-      a[m] = (kok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kk) : zero_half8();
-    }
+    for (int g = 0; g < G; ++g) {
+      const int kk = k0 + 32 * g + kc8;
+      if (k0 + 32 * g >= kend) break;  // wave-uniform
+      half8 af[4];
+      if constexpr (LNA) {
+        const bool ok = kk < kend;
+        float ga[8], be[8];
+        {
+          const float4 g0 = ok ? *reinterpret_cast<const float4*>(p.gamma + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 g1 = ok ? *reinterpret_cast<const float4*>(p.gamma + kk + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 b0 = ok ? *reinterpret_cast<const float4*>(p.beta + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 b1 = ok ? *reinterpret_cast<const float4*>(p.beta + kk + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          ga[0] = g0.x; ga[1] = g0.y; ga[2] = g0.z; ga[3] = g0.w; ga[4] = g1.x; ga[5] = g1.y; ga[6] = g1.z; ga[7] = g1.w;
+          be[0] = b0.x; be[1] = b0.y; be[2] = b0.z; be[3] = b0.w; be[4] = b1.x; be[5] = b1.y; be[6] = b1.z; be[7] = b1.w;
+        }
 #pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
-  }
+        for (int m = 0; m < 4; ++m) {
+          const int r = m * 16 + lr;
+          const float mean = s_mean[r], rstd = s_rstd[r];
+          const float xv[8] = {ax[g][m][0].x, ax[g][m][0].y, ax[g][m][0].z, ax[g][m][0].w,
+                               ax[g][m][1].x, ax[g][m][1].y, ax[g][m][1].z, ax[g][m][1].w};
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
-  __syncthreads();
-  skinny_epilogue<EPI>(p, red, col0, M, N);
-}
-
-// Shared epilogue of the skinny kernels: thread i -> (row i>>4, col col0 + (i&15)), so
-// the 16 lanes of an aligned group hold one row's 16 columns (LayerNorm pieces).
-template <int EPI>
-__device__ __forceinline__ void skinny_epilogue(const GemmArgs& p, float (*red)[64][17], int col0,
-                                                int M, int N) {
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 64 * 16; i += 256) {
-    const int row = i >> 4, c = i & 15, col = col0 + c;
-    const bool ok = row < M && col < N;
-    float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
-    v += (p.bias && ok) ? p.bias[col] : 0.0f;
-    if constexpr (EPI == EPI_RESID_F32) {
-      const float y = ok ? p.R[(int64_t)row * p.ldr + col] + v : 0.0f;
-      if (ok) static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = y;
-      if (p.ln_part) {  // uniform branch: all 16 lanes of the row group take part
-        float sm = y;
-        sm += __shfl_xor(sm, 1); sm += __shfl_xor(sm, 2);
-        sm += __shfl_xor(sm, 4); sm += __shfl_xor(sm, 8);
-        const float mu = sm * (1.0f / 16.0f);
-        float q = (y - mu) * (y - mu);
-        q += __shfl_xor(q, 1); q += __shfl_xor(q, 2);
-        q += __shfl_xor(q, 4); q += __shfl_xor(q, 8);
-        if (c == 0 && row < M) p.ln_part[(int64_t)row * (N / 16) + col0 / 16] = make_float2(sm, q);
-      }
-      continue;
-    }
-    if (!ok) continue;
-    if constexpr (EPI == EPI_F16) {
-      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
-    } else if constexpr (EPI == EPI_GELU_F16) {
-      static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
-    } else if constexpr (EPI == EPI_QKV) {
-      // q -> C; k, v -> cache rows (row * n_ctx + pos); R/ldr carry the cache pointers
-      const int dq = p.qkv_d;
-      if (col < dq) {
-        static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+          for (int j = 0; j < 8; ++j)
+            af[m][j] = (ok && r < M) ? (_Float16)((xv[j] - mean) * rstd * ga[j] + be[j]) : (_Float16)0.0f;
+        }
       } else {
-        _Float16* cache = col < 2 * dq ? p.kc : p.vc;
-        cache[((int64_t)row * p.n_ctx + p.pos) * dq + (col % dq)] = (_Float16)v;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) af[m] = ah[g][m];
       }
-    } else {
-      static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[m] = mfma16(af[m], bw[g], acc[m]);
     }
+    if (k0 + 32 * G < kend) load(k0 + 32 * G);
+  }
+
+  // 16 partials -> LDS: waves 0-7 store, waves 8-15 add, then one output per thread
+  if (w < 8) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
+  }
+  __syncthreads();
+  if (w >= 8) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w - 8][m * 16 + 4 * (lane >> 4) + r][lane & 15] += acc[m][r];
+  }
+  __syncthreads();
+  float v = e_add;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v += red[i][erow][ec];
+  // thread -> (row tid>>4, col col0 + (tid&15)): 16 aligned lanes hold one row's columns
+  if constexpr (EPI == EPI_RESID_F32) {
+    if (eok) static_cast<float*>(p.C)[(int64_t)erow * p.ldc + ecol] = v;
+    if (p.ln_part) {  // block-uniform
+      const float y = eok ? v : 0.0f;
+      float sm = y;
+      sm += __shfl_xor(sm, 1); sm += __shfl_xor(sm, 2);
+      sm += __shfl_xor(sm, 4); sm += __shfl_xor(sm, 8);
+      const float mu = sm * (1.0f / 16.0f);
+      float q = (y - mu) * (y - mu);
+      q += __shfl_xor(q, 1); q += __shfl_xor(q, 2);
+      q += __shfl_xor(q, 4); q += __shfl_xor(q, 8);
+      if (ec == 0 && erow < M) p.ln_part[(int64_t)erow * (N / 16) + col0 / 16] = make_float2(sm, q);
+    }
+    return;
+  }
+  if (!eok) return;
+  if constexpr (EPI == EPI_F16) {
+    static_cast<_Float16*>(p.C)[(int64_t)erow * p.ldc + ecol] = (_Float16)v;
+  } else if constexpr (EPI == EPI_GELU_F16) {
+    static_cast<_Float16*>(p.C)[(int64_t)erow * p.ldc + ecol] = (_Float16)gelu_erf(v);
+  } else if constexpr (EPI == EPI_QKV) {
+    // q -> C; k, v -> cache rows (row * n_ctx + pos)
+    const int dq = p.qkv_d;
+    if (ecol < dq) {
+      static_cast<_Float16*>(p.C)[(int64_t)erow * p.ldc + ecol] = (_Float16)v;
+    } else {
+      _Float16* cache = ecol < 2 * dq ? p.kc : p.vc;
+      cache[((int64_t)erow * p.n_ctx + p.pos) * dq + (ecol % dq)] = (_Float16)v;
+    }
+  } else {
+    static_cast<float*>(p.C)[(int64_t)erow * p.ldc + ecol] = v;
   }
 }
 
-static void launch_skinny(int epi, const GemmArgs& p, hipStream_t s) {
+template <bool LNA>
+static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
   const int blocks = (p.N + 15) / 16;
   switch (epi) {
-    case EPI_F16: gemm_skinny_kernel<EPI_F16><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_RESID_F32: gemm_skinny_kernel<EPI_RESID_F32><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_F32: gemm_skinny_kernel<EPI_F32><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_QKV: gemm_skinny_kernel<EPI_QKV><<<blocks, 256, 0, s>>>(p); break;
+    case EPI_F16: gemm_skinny_kernel<EPI_F16, LNA><<<blocks, 1024, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16, LNA><<<blocks, 1024, 0, s>>>(p); break;
+    case EPI_QKV: gemm_skinny_kernel<EPI_QKV, LNA><<<blocks, 1024, 0, s>>>(p); break;
+    case EPI_RESID_F32:
+      if constexpr (!LNA) { gemm_skinny_kernel<EPI_RESID_F32, false><<<blocks, 1024, 0, s>>>(p); break; }
+      else throw Error("skinny LN gemm: bad epilogue");
+    case EPI_F32:
+      if constexpr (!LNA) { gemm_skinny_kernel<EPI_F32, false><<<blocks, 1024, 0, s>>>(p); break; }
+      else throw Error("skinny LN gemm: bad epilogue");
     default: throw Error("bad gemm epilogue");
   }
   JANUS_LAUNCH_CHECK();
 }
 
-// ------------------------------------------------------- skinny M + fused LN
-// C = epi( LN(x)[M,K] · W[N,K]^T + bias ), M <= 64, x fp32 (the residual stream). The
-// row statistics come from the K/16 LayerNorm pieces its producer wrote (SkinnyLnArgs):
-// thread (row tid/4, quarter tid%4) combines a quarter of the pieces, four lanes finish
-// the row (Chan: M2 = sum M2_i + 16 * sum (mu_i - mean)^2). A fragments are normalised
-// on load. Replaces the LayerNorm launch in front of every decoder projection.
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_skinny_ln_kernel(SkinnyLnArgs p) {
-  __shared__ float red[4][64][17];
-  __shared__ float s_mean[64], s_rstd[64];
-  const int M = p.M, N = p.N, K = p.K;
-  const int col0 = blockIdx.x * 16;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kq = ((K + 3) / 4 + 31) / 32 * 32;
-  const int kbeg = w * kq, kend = min(K, kbeg + kq);
-  const int bcol = col0 + (lane & 15);
-  const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
-  // the first weight fragment does not depend on the statistics: start it now
-  half8 b_next = (kbeg + 8 * (lane >> 4) < kend && bcol < N)
-                     ? *reinterpret_cast<const half8*>(wrow + kbeg + 8 * (lane >> 4)) : zero_half8();
-  {
-    const int r = tid >> 2, qd = tid & 3, np = K / 16;
-    float2 pc[8];
-    float sm = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int g = qd + 4 * j;
-      pc[j] = (r < M && g < np) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
-      sm += pc[j].x;
-    }
-    for (int g = qd + 32; g < np; g += 4) sm += (r < M) ? p.part[(int64_t)r * np + g].x : 0.f;
-    sm += __shfl_xor(sm, 1);
-    sm += __shfl_xor(sm, 2);
-    const float mean = sm / K;
-    float m2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int g = qd + 4 * j;
-      if (g < np) {
-        const float dm = pc[j].x * (1.0f / 16.0f) - mean;
-        m2 += pc[j].y + 16.0f * dm * dm;
-      }
-    }
-    for (int g = qd + 32; g < np; g += 4) {
-      const float2 q = (r < M) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
-      const float dm = q.x * (1.0f / 16.0f) - mean;
-      m2 += q.y + 16.0f * dm * dm;
-    }
-    m2 += __shfl_xor(m2, 1);
-    m2 += __shfl_xor(m2, 2);
-    if (qd == 0) { s_mean[r] = mean; s_rstd[r] = rsqrtf(m2 / K + p.eps); }
-  }
-  __syncthreads();
-  f32x4 acc[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const int kk = k0 + 8 * (lane >> 4);
-    const bool kok = kk < kend;
-    const half8 b = b_next;
-    const int kn = kk + 32;
-    b_next = (kn < kend && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kn) : zero_half8();
-    float g[8], be[8];
-    if (kok) {
-      const float4 g0 = *reinterpret_cast<const float4*>(p.gamma + kk);
-      const float4 g1 = *reinterpret_cast<const float4*>(p.gamma + kk + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(p.beta + kk);
-      const float4 b1 = *reinterpret_cast<const float4*>(p.beta + kk + 4);
-      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
-      be[0] = b0.x; be[1] = b0.y; be[2] = b0.z; be[3] = b0.w; be[4] = b1.x; be[5] = b1.y; be[6] = b1.z; be[7] = b1.w;
-    }
-    half8 a[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int r = m * 16 + (lane & 15);
-      a[m] = zero_half8();
-      if (kok && r < M) {
-        const float* xr = p.x + (int64_t)r * p.ldx + kk;
-        const float4 x0 = *reinterpret_cast<const float4*>(xr);
-        const float4 x1 = *reinterpret_cast<const float4*>(xr + 4);
-        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        const float mean = s_mean[r], rstd = s_rstd[r];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[m][j] = (_Float16)((xv[j] - mean) * rstd * g[j] + be[j]);
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
-  }
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
-  __syncthreads();
-  GemmArgs q{};
-  q.bias = p.bias; q.C = p.C; q.ldc = p.ldc;
-  q.kc = p.kc; q.vc = p.vc; q.pos = p.pos; q.n_ctx = p.n_ctx; q.qkv_d = p.qkv_d;
-  skinny_epilogue<EPI>(q, red, col0, M, N);
+static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
+  SkinnyArgs p{};
+  p.A = g.A; p.lda = g.lda; p.W = g.W; p.ldw = g.ldw; p.bias = g.bias; p.C = g.C; p.ldc = g.ldc;
+  p.R = g.R; p.ldr = g.ldr; p.M = g.M; p.N = g.N; p.K = g.K;
+  p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
+  p.ln_part = g.ln_part;
+  launch_skinny_t<false>(epi, p, s);
 }
 
-void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& p, hipStream_t s) {
-  JANUS_CHECK(p.M <= 64 && p.K % 16 == 0 && p.K <= 2048 && p.ldx % 4 == 0 && p.part,
-              "skinny LN gemm: M <= 64, K % 16 == 0, K <= 2048, LayerNorm pieces required");
-  if (p.M <= 0 || p.N <= 0) return;
-  const int blocks = (p.N + 15) / 16;
-  switch (epi) {
-    case EPI_F16: gemm_skinny_ln_kernel<EPI_F16><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_GELU_F16: gemm_skinny_ln_kernel<EPI_GELU_F16><<<blocks, 256, 0, s>>>(p); break;
-    case EPI_QKV: gemm_skinny_ln_kernel<EPI_QKV><<<blocks, 256, 0, s>>>(p); break;
-    default: throw Error("skinny LN gemm: bad epilogue");
-  }
-  JANUS_LAUNCH_CHECK();
+void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& g, hipStream_t s) {
+  JANUS_CHECK(g.M <= 64 && g.K % 16 == 0 && g.ldx % 4 == 0 && g.part,
+              "skinny LN gemm: M <= 64, K % 16 == 0, LayerNorm pieces required");
+  if (g.M <= 0 || g.N <= 0) return;
+  SkinnyArgs p{};
+  p.x = g.x; p.ldx = g.ldx; p.part = g.part; p.gamma = g.gamma; p.beta = g.beta; p.eps = g.eps;
+  p.W = g.W; p.ldw = g.ldw; p.bias = g.bias; p.C = g.C; p.ldc = g.ldc; p.M = g.M; p.N = g.N; p.K = g.K;
+  p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
+  launch_skinny_t<true>(epi, p, s);
 }
 
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {

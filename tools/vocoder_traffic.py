@@ -1,0 +1,62 @@
+"""HBM traffic of the vocoder's conv launches (the bench's roofline kernel).
+
+Run under two rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE):
+  rocprofv3 --kernel-trace --pmc FETCH_SIZE -d out/f -o run --output-format csv -- python3 tools/vocoder_traffic.py
+then ``python3 tools/vocoder_traffic.py --reduce out/f out/w profiles/traffic_r01.json`` sums the
+counters over the conv dispatches of the profiled forward (one 64 x 30 s batch, the bench
+workload) and writes bytes per launch, with the gfx950 correction (FETCH_SIZE reports half
+of the bytes of 16-B-per-lane streaming reads: MI355X_MICROARCH.md 'HBM').
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def run():
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from janus_amd.vocoder import VocoderEngine, emotion_id
+    eng = VocoderEngine()
+    B, F = 64, 2584
+    prompts = [b"(relaxed) traffic sample %d" % i for i in range(B)]
+    lat = eng.frontend(prompts, [emotion_id("relaxed")] * B, F)
+    eng.set_timing(True)
+    eng.forward(lat)
+    torch.cuda.synchronize()
+    flops, ms, launches = eng.conv_stats(reset=True)
+    print(json.dumps({"conv_flops": flops, "conv_ms": ms, "conv_launches": launches}))
+
+
+def counters(d):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    tot, n = 0.0, set()
+    for r in csv.DictReader(open(f)):
+        if "conv_kernel" in r["Kernel_Name"] or "resunit_kernel" in r["Kernel_Name"]:
+            tot += float(r["Counter_Value"])
+            n.add(r["Dispatch_Id"])
+    return tot, len(n)
+
+
+def reduce(fdir, wdir, out):
+    fetch_kb, nf = counters(fdir)
+    write_kb, nw = counters(wdir)
+    assert nf == nw and nf > 0, (nf, nw)
+    fetch = 2.0 * fetch_kb * 1024  # gfx950: FETCH_SIZE = half the streamed bytes (KB units)
+    write = write_kb * 1024
+    res = {"kernel": "conv_kernel + resunit_kernel (vocoder convs, all shapes of one 64 x 30 s "
+                     "forward: the launch set the bench's roofline averages over)",
+           "launches": nf, "fetch_bytes": fetch, "write_bytes": write,
+           "bytes_per_launch": (fetch + write) / nf,
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read under-count), KB -> bytes x1024",
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--reduce":
+        reduce(sys.argv[2], sys.argv[3], sys.argv[4])
+    else:
+        run()
