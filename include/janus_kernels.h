@@ -74,6 +74,20 @@ int janus_resunit_f16(const uint16_t* x, uint16_t* out, const uint16_t* w1, cons
                       const uint16_t* w2, const float* b2, int batch, int T, int C, int k,
                       int dilation, float scale, int accumulate, void* stream);
 
+/*
+ * Decoder cross-attention over the encoder output with absorbed K/V projections:
+ * for every utterance b and head h (H * 64 == D, D in {384, 512, 768}),
+ *   p = softmax_2(qk[b][h] . enc[b]^T)   (base-2 softmax: qk carries log2(e)/8),
+ *   out[b][h*D:(h+1)*D] = p . enc[b]
+ * qk fp16 [B][H*D], enc fp16 [B][Te][D], out fp16 [B][H*D]; nsplit key splits
+ * (1..63) with scratch part_c f32 [B][nsplit][H][D] and part_ml f32 [B][nsplit][H][2].
+ * Replaces the cross-attention K/V projections + attention of the Whisper decoder
+ * (transcriber.py:23-27); see janus_amd/csrc/xattn.hip for the re-association.
+ */
+int janus_cross_attention_f16(const uint16_t* qk, const uint16_t* enc, int batch, int Te, int D,
+                              int H, int nsplit, float* part_c, float* part_ml, uint16_t* out,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

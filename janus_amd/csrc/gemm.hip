@@ -159,6 +159,7 @@ struct SkinnyArgs {
   int M, N, K;
   _Float16* kc; _Float16* vc; int pos, n_ctx, qkv_d;
   float2* ln_part;
+  int a_group_cols;
 };
 
 constexpr int kSkWaves = 16;
@@ -176,6 +177,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   const int bcol = col0 + (lane & 15);
   const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
   const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const _Float16* Ab = p.A;
+  if constexpr (!LNA) {
+    if (p.a_group_cols > 0) Ab += (int64_t)(col0 / p.a_group_cols) * K;  // block-diagonal
+  }
 
   // epilogue operands independent of the product, in flight from the start
   const int erow = tid >> 4, ec = tid & 15, ecol = col0 + ec;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
           ax[g][m][0] = rok ? *reinterpret_cast<const float4*>(xr) : make_float4(0.f, 0.f, 0.f, 0.f);
           ax[g][m][1] = rok ? *reinterpret_cast<const float4*>(xr + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-          ah[g][m] = (ok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kk)
+          ah[g][m] = (ok && r < M) ? *reinterpret_cast<const half8*>(Ab + (int64_t)r * p.lda + kk)
                                    : zero_half8();
         }
       }
@@ -364,6 +369,7 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.R = g.R; p.ldr = g.ldr; p.M = g.M; p.N = g.N; p.K = g.K;
   p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
   p.ln_part = g.ln_part;
+  p.a_group_cols = g.a_group_cols;
   launch_skinny_t<false>(epi, p, s);
 }
 
@@ -384,6 +390,8 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return;
   JANUS_CHECK(p.M <= 64 || (epi != EPI_QKV && !p.ln_part),
               "gemm: the KV-cache and LayerNorm-piece epilogues need M <= 64");
+  JANUS_CHECK(p.a_group_cols == 0 || (p.M <= 64 && p.a_group_cols % 16 == 0),
+              "gemm: grouped A needs M <= 64 and 16-column groups");
   JANUS_CHECK(!p.ln_part || (epi == EPI_RESID_F32 && p.N % 16 == 0),
               "gemm: LayerNorm pieces come from a RESID epilogue with N % 16 == 0");
   if (p.M <= 64) launch_skinny(epi, p, s);

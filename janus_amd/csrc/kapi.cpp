@@ -115,3 +115,13 @@ extern "C" int janus_resunit_f16(const uint16_t* x, uint16_t* out, const uint16_
     resunit_launch(a, (hipStream_t)stream);
   });
 }
+
+extern "C" int janus_cross_attention_f16(const uint16_t* qk, const uint16_t* enc, int batch,
+                                         int Te, int D, int H, int nsplit, float* part_c,
+                                         float* part_ml, uint16_t* out, void* stream) {
+  return guarded([&] {
+    xattn_launch(reinterpret_cast<const _Float16*>(qk), reinterpret_cast<const _Float16*>(enc),
+                 batch, Te, D, H, nsplit, part_c, part_ml, reinterpret_cast<_Float16*>(out),
+                 (hipStream_t)stream);
+  });
+}

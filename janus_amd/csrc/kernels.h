@@ -19,6 +19,9 @@ struct GemmArgs {
   // EPI_RESID_F32 (M <= 64 only): also write the LayerNorm pieces of the new rows,
   // ln_part[row][col / 16] (see SkinnyLnArgs)
   float2* ln_part = nullptr;
+  // grouped (block-diagonal) product, M <= 64 only: output columns [g*a_group_cols,
+  // (g+1)*a_group_cols) read A columns [g*K, (g+1)*K) — per-head projections
+  int a_group_cols = 0;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
 
@@ -64,6 +67,18 @@ void decode_attention_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
 
 // Split-key (flash-decoding) variant for d <= 512: all heads of a row per block.
 // part_o: f32 [B][splits][d], part_ml: f32 [B][splits][H][2] workspaces.
+// Decoder cross-attention over the encoder output with absorbed K/V projections
+// (xattn.hip). xattn_absorb builds Wqk [H*D][D] fp16 and bqk [H*D] f32 (scores in the
+// exp2 domain) from the fp32 q/k projections; xattn_launch takes qk [B][H*D] fp16 and
+// enc [B][Te][D] fp16 and writes c [B][H*D] fp16 (softmax-weighted encoder rows per
+// head) via per-split partials part_c [B][nsplit][H][D] f32 and part_ml [B][nsplit][H][2].
+bool xattn_supported(int D, int H);
+int xattn_split_count(int Te, int requested);
+void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int H,
+                  _Float16* wqk, float* bqk, hipStream_t s);
+void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
+                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s);
+
 int decode_split_count(int Tkv);
 void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
                                    const _Float16* v, int64_t kv_bs, int64_t kv_rs, int Tkv,

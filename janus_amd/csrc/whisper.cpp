@@ -24,6 +24,7 @@ struct EncLayer {
 };
 struct DecLayer {
   DevMem wqkv, bqkv, wo, wq_c, wk_c, wv_c, wo_c, w1, w2;
+  DevMem wqk, bqk;  // absorbed cross-attention query weights (xattn.hip)
   const float *bo, *bq_c, *bv_c, *bo_c, *b1, *b2;
   const float *ln1g, *ln1b, *ln2g, *ln2b, *ln3g, *ln3b;
 };
@@ -42,7 +43,8 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp;
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp,
+      d_xqk, d_xc, d_xpc, d_xpml;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t side = nullptr;  // graph capture needs a non-null stream
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -147,6 +149,14 @@ static void prepare(janus_whisper* w, hipStream_t s) {
     L.ln2b = P.get(p + "encoder_attn_layer_norm.bias", d);
     L.ln3g = P.get(p + "final_layer_norm.weight", d);
     L.ln3b = P.get(p + "final_layer_norm.bias", d);
+    if (xattn_supported(d, c.n_heads)) {
+      const int64_t hd = (int64_t)c.n_heads * d;
+      L.wqk.ensure(sizeof(_Float16) * hd * d);
+      L.bqk.ensure(sizeof(float) * hd);
+      const std::string e = p + "encoder_attn.";
+      xattn_absorb(P.get(e + "q_proj.weight", dd), P.has(e + "q_proj.bias") ? P.get(e + "q_proj.bias", d) : nullptr,
+                   P.get(e + "k_proj.weight", dd), d, c.n_heads, L.wqk.as<_Float16>(), L.bqk.as<float>(), s);
+    }
   }
   JANUS_HIP(hipStreamSynchronize(s));
   w->prepared = true;
@@ -228,8 +238,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   w->d_f.ensure(sizeof(_Float16) * B * 4 * d);
   w->d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
   w->d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
-  w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
-  w->d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+
   w->d_smask.ensure(V);
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   w->d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
@@ -263,8 +272,21 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
                      n_tokens, B, s);
   rules_init_launch(w->d_rules.as<RowRules>(), B, s);
 
+  // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
+  const bool xabs = xattn_supported(d, H) && B <= 64 && std::getenv("JANUS_NO_XABSORB") == nullptr;
+  const int xsplit = xattn_split_count(Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : 0);
+  if (xabs) {
+    w->d_xqk.ensure(sizeof(_Float16) * B * H * d);
+    w->d_xc.ensure(sizeof(_Float16) * B * H * d);
+    w->d_xpc.ensure(sizeof(float) * (int64_t)B * xsplit * H * d);
+    w->d_xpml.ensure(sizeof(float) * (int64_t)B * xsplit * H * 2);
+  }
   // cross-attention keys/values, once per window
-  for (int l = 0; l < nl; ++l) {
+  if (!xabs) {
+    w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+    w->d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+  }
+  for (int l = 0; l < nl && !xabs; ++l) {
     DecLayer& L = w->dec[l];
     _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
     _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
@@ -329,16 +351,35 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s);
       resid(o, d, L.wo, L.bo);
-      if (fused_ln) {
-        gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
-                                              nullptr, nullptr, pos), s);
+      if (xabs) {
+        const int hd = H * d;
+        _Float16* xqk = w->d_xqk.as<_Float16>();
+        _Float16* xc = w->d_xc.as<_Float16>();
+        if (fused_ln) {
+          gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
+                                                xqk, hd, hd, nullptr, nullptr, pos), s);
+        } else {
+          layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          gemm_launch(EPI_F16, gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d), s);
+        }
+        xattn_launch(xqk, enc, B, Te, d, H, xsplit, w->d_xpc.as<float>(), w->d_xpml.as<float>(), xc, s);
+        // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
+        GemmArgs gv = gargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
+        gv.a_group_cols = 64;
+        gemm_launch(EPI_F16, gv, s);
+        resid(o, d, L.wo_c, L.bo_c);
       } else {
-        layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-        gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+        if (fused_ln) {
+          gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
+                                                nullptr, nullptr, pos), s);
+        } else {
+          layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+        }
+        decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
+                                      part_ml, s);
+        resid(o, d, L.wo_c, L.bo_c);
       }
-      decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
-                                    part_ml, s);
-      resid(o, d, L.wo_c, L.bo_c);
       if (fused_ln) {
         gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
@@ -363,7 +404,8 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
       (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
-      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
+      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
+      (int64_t)w->d_xc.p, (int64_t)w->d_xpc.p, (int64_t)w->d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
   if (w->graphs.size() > 512) {

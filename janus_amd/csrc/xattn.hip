@@ -1,0 +1,305 @@
+// Decoder cross-attention over the encoder output with the K/V projections absorbed.
+//
+// Whisper's cross-attention for head h (faster-whisper / CTranslate2 decoder,
+// transcriber.py:23-27 -> model.transcribe) is
+//   q_h = LN2(x) Wq_h^T + bq_h,  K_h = enc Wk_h^T,  V_h = enc Wv_h^T + bv_h,
+//   o_h = softmax(q_h K_h^T / 8) V_h,  x += concat_h(o_h) Wo^T + bo.
+// Re-associating the score side (k_proj has no bias) and the value side:
+//   q_h K_h^T = (q_h Wk_h) enc^T = qk_h enc^T          (qk_h: a D-vector per head)
+//   o_h = p_h V_h = (p_h enc) Wv_h^T + bv_h             (p_h sums to 1)
+// so per token the decoder streams the encoder output itself — D values per key shared by
+// all heads — instead of per-layer K and V: half the bytes per layer, one tensor for all
+// layers, and no per-window K/V projection GEMMs. The absorbed query weights
+//   Wqk[h*D + j][i] = s * sum_c Wq[h*64+c][i] Wk[h*64+c][j],  bqk[h*D + j] likewise from bq
+// (s = log2(e)/8: scores arrive in the exp2 domain) are built once on the device in fp32
+// and stored fp16; qk = LN2(x) Wqk^T + bqk runs on the skinny GEMM, and the value side is
+// the block-diagonal (per-head) skinny GEMM o = c Wv^T + bv followed by the usual
+// x += o Wo^T + bo. (Folding Wv into Wo as well measured slower: a K = H*D GEMM.)
+//
+// xattn_kernel: block = (key split, utterance), 4 waves, chunks of 32 keys:
+//   S[16 x 32]  = Qk[16 x D] . E^T        MFMA; heads padded to 16 rows; E fragments
+//                                           straight from HBM into registers
+//   online softmax per head (exp2), P -> fp16 LDS in a key order chosen so the
+//   transposed reads below are bank-conflict-free
+//   C[16 x D]  += P[16 x 32] . E[32 x D]   MFMA; E^T fragments by ds_read_b64_tr_b16
+// then per-split partial (C, m, l) in fp32; xattn_combine merges the splits into
+// c[b][h*D + j] fp16, the A operand of the per-head Wv GEMM.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+constexpr int kXKeys = 32;  // keys per chunk
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------ weight absorption
+__global__ void absorb_qk_kernel(const float* __restrict__ wq, const float* __restrict__ bq,
+                                 const float* __restrict__ wk, int D, int H, float s,
+                                 _Float16* __restrict__ wqk, float* __restrict__ bqk) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over H*D*D
+  const int64_t total = (int64_t)H * D * D;
+  if (idx < total) {
+    const int i = (int)(idx % D);
+    const int64_t rj = idx / D;  // h*D + j
+    const int j = (int)(rj % D), h = (int)(rj / D);
+    float acc = 0.f;
+    for (int c = 0; c < 64; ++c)
+      acc += wq[(int64_t)(h * 64 + c) * D + i] * wk[(int64_t)(h * 64 + c) * D + j];
+    wqk[idx] = (_Float16)(acc * s);
+  }
+  if (idx < (int64_t)H * D) {
+    const int j = (int)(idx % D), h = (int)(idx / D);
+    float acc = 0.f;
+    if (bq)
+      for (int c = 0; c < 64; ++c) acc += bq[h * 64 + c] * wk[(int64_t)(h * 64 + c) * D + j];
+    bqk[idx] = acc * s;
+  }
+}
+
+void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int H,
+                  _Float16* wqk, float* bqk, hipStream_t s) {
+  JANUS_CHECK(H * 64 == D, "xattn: head_dim must be 64");
+  const int64_t n = (int64_t)H * D * D;
+  const float sc = 1.4426950408889634f / 8.0f;  // log2(e) / sqrt(64)
+  absorb_qk_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(wq, bq, wk, D, H, sc, wqk, bqk);
+  JANUS_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------ attention over enc
+// Contraction order of a chunk's 32 keys in the P.E product: MFMA k index
+// k = 8g + 4hf + q (g = lane>>4, hf = which of the two transposed reads, q = row in
+// the read) takes key kappa(k) = 16(g>>1) + 8hf + 4(g&1) + q, so the 8 rows one
+// 32-lane half reads per ds_read_b64_tr_b16 are distinct mod 8 — with a row pitch of
+// D+16 halves (8 banks mod 64 per row) the half touches all 64 banks once.
+__device__ __forceinline__ int xkappa(int k) {
+  const int g = k >> 3, hf = (k >> 2) & 1, q = k & 3;
+  return 16 * (g >> 1) + 8 * hf + 4 * (g & 1) + q;
+}
+__device__ __forceinline__ int xkappa_inv(int key) {
+  const int g2 = key >> 4, hf = (key >> 3) & 1, g1 = (key >> 2) & 1, q = key & 3;
+  return 8 * (2 * g2 + g1) + 4 * hf + q;
+}
+
+template <int D>
+struct XGeo {
+  static constexpr int QP = D + 16;          // sE row pitch (halves)
+  static constexpr int PP = 48;              // sP pitch (halves), frag_pitch(32)
+  static constexpr int KH = D / 2;           // dims per S-phase k-half
+  static constexpr int KS = KH / 32;         // S-phase k-steps per wave
+  static constexpr int NT = D / 64;          // C-phase 16-col tiles per wave
+  static constexpr int LDS = (kXKeys * QP + 16 * PP) * 2 + 2 * 16 * kXKeys * 4 + 16 * 4;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Float16* __restrict__ qk,
+                                                    const _Float16* __restrict__ enc, int Te,
+                                                    int H, int kps, float* __restrict__ part_c,
+                                                    float* __restrict__ part_ml) {
+  using G = XGeo<D>;
+  constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT;
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* sE = smem;                         // [32][QP] keys x dims
+  _Float16* sP = sE + kXKeys * QP;             // [16][PP] heads x (permuted) keys
+  float* sS = reinterpret_cast<float*>(sP + 16 * PP);  // [2][16][32] partial scores
+  float* sA = sS + 2 * 16 * kXKeys;            // [16] rescale factors
+
+  const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int t0 = s * kps, t1 = min(Te, t0 + kps);
+  const _Float16* eb = enc + (int64_t)b * Te * D;
+
+  // S-phase role: key tile nt (16 keys), dims half kh; the wave's Qk fragments (rows =
+  // heads, zero rows >= H) stay in registers for the whole split
+  const int nt = w & 1, kh = w >> 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  half8 qa[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    qa[ks] = lr < H ? *reinterpret_cast<const half8*>(qk + ((int64_t)b * H + lr) * D + kh * KH + 32 * ks + 8 * lg)
+                    : zero_half8();
+  for (int i = tid; i < 16 * PP; i += 256) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
+
+  half8 ef[KS];
+  auto load_e = [&](int t) {
+    const int key = t + 16 * nt + lr;
+    const bool ok = key < t1;
+    const _Float16* src = eb + (int64_t)key * D + kh * KH + 8 * lg;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      ef[ks] = ok ? *reinterpret_cast<const half8*>(src + 32 * ks) : zero_half8();
+  };
+
+  f32x4 accc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) accc[n] = zero_f32x4();
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
+
+  if (t0 < t1) load_e(t0);
+  __syncthreads();
+  for (int t = t0; t < t1; t += kXKeys) {
+    // ---- S partial: rows = heads, cols = keys 16nt.., k = dims of half kh
+    f32x4 accs = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) accs = mfma16(qa[ks], ef[ks], accs);
+    // E rows -> LDS (row-major) for the P.E product
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = ef[ks];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sS[(kh * 16 + 4 * lg + r) * kXKeys + 16 * nt + lr] = accs[r];
+    if (t + kXKeys < t1) load_e(t + kXKeys);  // next chunk in flight during softmax + P.E
+    __syncthreads();
+
+    // ---- online softmax: wave w owns heads w, w+4, w+8, w+12; lane = key (lanes < 32)
+    const int nk = min(kXKeys, t1 - t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = w + 4 * i;
+      if (h >= H) break;  // wave-uniform
+      const bool valid = lane < nk;
+      const float sc = valid ? sS[h * kXKeys + lane] + sS[(16 + h) * kXKeys + lane] : -INFINITY;
+      float mc = sc;
+      for (int o = 32; o > 0; o >>= 1) mc = fmaxf(mc, __shfl_xor(mc, o));
+      const float m_new = fmaxf(m_run[i], mc);
+      const float alpha = exp2f(m_run[i] - m_new);  // 0 on the first chunk
+      const float p = valid ? exp2f(sc - m_new) : 0.f;
+      float ps = p;
+      for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
+      l_run[i] = l_run[i] * alpha + ps;
+      m_run[i] = m_new;
+      if (lane < kXKeys) sP[h * PP + xkappa_inv(lane)] = (_Float16)p;
+      if (lane == 0) sA[h] = alpha;
+    }
+    __syncthreads();
+
+    // ---- C += P . E over this chunk; wave w owns dims [w*D/4, (w+1)*D/4)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * lg + r;
+      const float al = row < H ? sA[row] : 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) accc[n][r] *= al;
+    }
+    const half8 pa = *reinterpret_cast<const half8*>(sP + lr * PP + 8 * lg);
+    const int q = lr >> 2, pcol = 4 * (lr & 3);
+    const int row0 = 16 * (lg >> 1) + 4 * (lg & 1) + q;  // kappa(8lg + q), hf = 0
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int c0 = w * (D / 4) + 16 * n + pcol;
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) short4v*)(sE + row0 * QP + c0));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) short4v*)(sE + (row0 + 8) * QP + c0));
+      half8 bv;
+      const _Float16* l4 = reinterpret_cast<const _Float16*>(&lo);
+      const _Float16* h4 = reinterpret_cast<const _Float16*>(&hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { bv[j] = l4[j]; bv[4 + j] = h4[j]; }
+      accc[n] = mfma16(pa, bv, accc[n]);
+    }
+    __syncthreads();  // sE / sS / sP are rewritten by the next chunk
+  }
+
+  // ---- per-split partials: C rows < H (fp32), (m, l) per head
+  float* pc = part_c + ((int64_t)b * nsplit + s) * H * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * lg + r;
+    if (row >= H) continue;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) pc[(int64_t)row * D + w * (D / 4) + 16 * n + lr] = accc[n][r];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = w + 4 * i;
+      if (h < H) {
+        float* pm = part_ml + (((int64_t)b * nsplit + s) * H + h) * 2;
+        pm[0] = m_run[i];
+        pm[1] = l_run[i];
+      }
+    }
+  }
+}
+
+// c[b][h*D + j] = sum_s 2^(m_s - M) C_s[h][j] / sum_s 2^(m_s - M) l_s   (fp16)
+__global__ __launch_bounds__(256) void xattn_combine_kernel(const float* __restrict__ part_c,
+                                                            const float* __restrict__ part_ml,
+                                                            int nsplit, int H, int D,
+                                                            _Float16* __restrict__ out) {
+  __shared__ float sw[16][64];  // per (head, split) weight, then 1/L in [h][63]... (nsplit <= 63)
+  __shared__ float sinv[16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* pml = part_ml + (int64_t)b * nsplit * H * 2;
+  if (tid < H) {
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, pml[(s * H + tid) * 2]);
+    float L = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float wgt = exp2f(pml[(s * H + tid) * 2] - M);  // empty split: m = -inf -> 0
+      sw[tid][s] = wgt;
+      L += wgt * pml[(s * H + tid) * 2 + 1];
+    }
+    sinv[tid] = 1.0f / L;
+  }
+  __syncthreads();
+  const float* pc = part_c + (int64_t)b * nsplit * H * D;
+  const int HD = H * D;
+  for (int e = tid * 4; e < HD; e += 256 * 4) {
+    const int h = e / D;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < nsplit; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(pc + (int64_t)s * HD + e);
+      const float wgt = sw[h][s];
+      acc.x += wgt * v.x; acc.y += wgt * v.y; acc.z += wgt * v.z; acc.w += wgt * v.w;
+    }
+    const float il = sinv[h];
+    _Float16* o = out + (int64_t)b * HD + e;
+    o[0] = (_Float16)(acc.x * il); o[1] = (_Float16)(acc.y * il);
+    o[2] = (_Float16)(acc.z * il); o[3] = (_Float16)(acc.w * il);
+  }
+}
+
+int xattn_split_count(int Te, int requested) {
+  int n = requested > 0 ? requested : 12;  // 768 blocks at batch 64: 3 per CU
+  n = std::min(n, 63);
+  n = std::min(n, (Te + kXKeys - 1) / kXKeys);
+  return std::max(n, 1);
+}
+
+template <int D>
+static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
+                      float* part_c, float* part_ml, hipStream_t s) {
+  const int chunks = (Te + kXKeys - 1) / kXKeys;
+  const int kps = (chunks + nsplit - 1) / nsplit * kXKeys;
+  auto kern = xattn_kernel<D>;
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr = true;
+  }
+  kern<<<dim3(nsplit, B), 256, XGeo<D>::LDS, s>>>(qk, enc, Te, H, kps, part_c, part_ml);
+  JANUS_LAUNCH_CHECK();
+}
+
+bool xattn_supported(int D, int H) {
+  return H * 64 == D && H <= 16 && (D == 384 || D == 512 || D == 768);
+}
+
+void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
+                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s) {
+  JANUS_CHECK(xattn_supported(D, H), "xattn: need D = 64 H in {384, 512, 768}");
+  if (B <= 0 || Te <= 0) return;
+  JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
+  if (D == 384) xattn_cfg<384>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  else if (D == 512) xattn_cfg<512>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  else xattn_cfg<768>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  xattn_combine_kernel<<<B, 256, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
+  JANUS_LAUNCH_CHECK();
+}
+
+}  // namespace janus

@@ -171,3 +171,25 @@ def test_resunit(gpu, C, k, d, acc):
              p2.data_ptr(), db2.data_ptr(), B, T, C, k, d, scale, acc, stream())
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 2e-3
+
+
+@pytest.mark.parametrize("B,Te,D,nsplit", [(2, 1500, 512, 8), (3, 100, 384, 3), (1, 77, 768, 1),
+                                            (4, 1500, 512, 63)])
+def test_cross_attention_absorbed(gpu, B, Te, D, nsplit):
+    """softmax_2(qk_h . enc^T) . enc per head vs a float64 torch reference."""
+    H = D // 64
+    g = torch.Generator().manual_seed(B * 1000 + Te + D)
+    enc = torch.randn(B, Te, D, generator=g).half()
+    qk = (torch.randn(B, H, D, generator=g) * 0.15).half()
+    s = torch.einsum("bhd,btd->bht", qk.double(), enc.double())
+    p = torch.softmax(s * math.log(2.0), dim=-1)
+    ref = torch.einsum("bht,btd->bhd", p, enc.double()).reshape(B, H * D)
+    dq, de = qk.to(gpu), enc.to(gpu)
+    pc = torch.empty(B * nsplit * H * D, dtype=torch.float32, device=gpu)
+    pml = torch.empty(B * nsplit * H * 2, dtype=torch.float32, device=gpu)
+    out = torch.empty(B, H * D, dtype=torch.float16, device=gpu)
+    nat.call("janus_cross_attention_f16", dq.data_ptr(), de.data_ptr(), B, Te, D, H, nsplit,
+             pc.data_ptr(), pml.data_ptr(), out.data_ptr(), stream())
+    torch.cuda.synchronize()
+    err = rel_err(out, ref)
+    assert err < 3e-3, err
