@@ -33,7 +33,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--units-only", action="store_true")
+    ap.add_argument("--xattn", action="store_true")
     a = ap.parse_args()
+    if a.xattn:
+        xattn_bench()
+        return
     if a.units_only:
         resunits(a.batch, a.reps)
         return
@@ -109,6 +113,36 @@ def resunits(B, reps):
         byts = 2.0 * B * T * C * 3  # read x, read+write the ParallelBlock accumulator
         print(f"unit C{C} k{k} d{d} B={B} T={T:8d} {ms:8.3f} ms {flops / ms / 1e9:8.1f} TF/s "
               f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
+
+
+
+
+def xattn_bench(reps=20):
+    """Absorbed cross-attention at the bench shape (64 x 1500 x 512, 8 heads) per split count."""
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    B, Te, D, H = 64, 1500, 512, 8
+    enc = torch.randn(B, Te, D, device=dev).half()
+    qk = (torch.randn(B, H, D, device=dev) * 0.1).half()
+    out = torch.empty(B, H * D, device=dev, dtype=torch.float16)
+    for ns in (4, 8, 12, 16, 24):
+        pc = torch.empty(B * ns * H * D, device=dev)
+        pml = torch.empty(B * ns * H * 2, device=dev)
+
+        def run():
+            nat.call("janus_cross_attention_f16", qk.data_ptr(), enc.data_ptr(), B, Te, D, H, ns,
+                     pc.data_ptr(), pml.data_ptr(), out.data_ptr(), s)
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        print(f"xattn nsplit={ns:3d} {ms * 1000:8.1f} us  {B * Te * D * 2 / ms / 1e6:8.1f} GB/s (enc, L2/MALL-warm)",
+              flush=True)
 
 
 if __name__ == "__main__":
