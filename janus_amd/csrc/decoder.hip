@@ -1,3 +1,4 @@
+#include <algorithm>
 // Small kernels of the greedy Whisper decoder loop (batched over utterances, one
 // token per step) and of the encoder/decoder glue.
 //
@@ -293,108 +294,129 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
   return v > bv || (v == bv && i < bi);
 }
 
-// grid (ceil(V/16), ceil(B/64)); each block: 16 vocab columns x 64 rows, K split over
-// the 4 waves (skinny MFMA GEMM), then rule-filtered statistics per row.
-__global__ __launch_bounds__(256) void logits_partial_kernel(
-    const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int K, int V, int B,
-    DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
-    LogitPart* __restrict__ parts) {
-  __shared__ float red[4][64][17];
-  const int nblk = gridDim.x;
-  const int col0 = blockIdx.x * 16, row0 = blockIdx.y * 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kq = ((K + 3) / 4 + 31) / 32 * 32;
-  const int kbeg = w * kq, kend = min(K, kbeg + kq);
-  f32x4 acc[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
-  const int bcol = col0 + (lane & 15);
-  const _Float16* wrow = W + (int64_t)min(bcol, V - 1) * K;
+// Vocabulary projection + rule-filtered statistics, per (row, 16-column tile):
+// logits = A[B<=64][K] . W[V][K]^T (W = the token embedding, tied). The 53 MB weight read
+// once per step is the cost: each block stages A (all rows) in LDS once, then its 8 waves
+// walk 16-column tiles independently — every tile's weight fragments (K/32 x 16 B per
+// lane) are issued before its MFMAs, so each wave keeps 16 KB of weights in flight — and
+// the tile's 64 x 16 logits go through a wave-private LDS patch so lane = row reduces its
+// 16 columns (rule filter, maxima, partition sums, argmaxes) without shuffles.
+constexpr int kLgWaves = 8;
 
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const int kk = k0 + 8 * (lane >> 4);
-    const bool kok = kk < kend;
-    const half8 b = (kok && bcol < V) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
-    half8 a[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int r = row0 + m * 16 + (lane & 15);
-      a[m] = (kok && r < B) ? *reinterpret_cast<const half8*>(A + (int64_t)r * lda + kk) : zero_half8();
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = mfma16(a[m], b, acc[m]);
+template <int NKS>  // K / 32
+__global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
+    const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
+    DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
+    LogitPart* __restrict__ parts, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
+  constexpr int K = NKS * 32;
+  constexpr int AP = K + 16;  // row pitch (halves): 16*AP bytes with AP/8 % 4 == 2 -> conflict-free
+  _Float16* sA = lg_smem;                                            // [64][AP]
+  float* sT = reinterpret_cast<float*>(sA + 64 * AP);                // [waves][64][17]
+  RowRules* sR = reinterpret_cast<RowRules*>(sT + kLgWaves * 64 * 17);  // [64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < 64 * (K / 8); i += kLgWaves * 64) {
+    const int r = i / (K / 8), c8 = (i % (K / 8)) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < B) v = *reinterpret_cast<const uint4*>(A + (int64_t)r * lda + c8);
+    *reinterpret_cast<uint4*>(sA + r * AP + c8) = v;
   }
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
+  if (tid < 64) {
+    RowRules rr;
+    if (tid < B) rr = rules[tid];
+    else { rr.sample_begin = 0; rr.suppress_all_ts = rr.suppress_text = 0; rr.ts_floor = -1; rr.last_stamp = -1; }
+    sR[tid] = rr;
+  }
   __syncthreads();
-  // thread -> (row = tid/4, 4 columns); rows reduce over 4 adjacent lanes
-  const int rl = tid >> 2, cq = (tid & 3) * 4;
-  const int row = row0 + rl;
-  RowRules rr;
-  if (row < B) rr = rules[row];
-  else { rr.sample_begin = 0; rr.suppress_all_ts = rr.suppress_text = 0; rr.ts_floor = -1; }
-  float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
-  float vals[4];
-  bool ok[4];
+  float* patch = sT + w * 64 * 17;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  RowRules rr;  // lane = row in the statistics pass (fields copied: no scratch for pad[])
+  rr.sample_begin = sR[lane].sample_begin; rr.suppress_all_ts = sR[lane].suppress_all_ts;
+  rr.suppress_text = sR[lane].suppress_text; rr.ts_floor = sR[lane].ts_floor;
+  for (int tile = blockIdx.x * kLgWaves + w; tile < ntiles; tile += gridDim.x * kLgWaves) {
+    const int col0 = tile * 16;
+    const int bcol = min(col0 + lr, V - 1);
+    const _Float16* wrow = W + (int64_t)bcol * K + kc8;
+    half8 bw[NKS];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = cq + j, t = col0 + c;
-    const float v = red[0][rl][c] + red[1][rl][c] + red[2][rl][c] + red[3][rl][c];
-    ok[j] = row < B && t < V && allowed(t, smask, R, rr, false);
-    vals[j] = v;
-    if (ok[j]) {
-      m_all = fmaxf(m_all, v);
-      if (R.ts_begin >= 0 && t >= R.ts_begin) m_ts = fmaxf(m_ts, v);
-      else m_text = fmaxf(m_text, v);
+    for (int ks = 0; ks < NKS; ++ks) bw[ks] = *reinterpret_cast<const half8*>(wrow + 32 * ks);
+    __builtin_amdgcn_sched_barrier(0);  // keep every weight load of the tile ahead of the MFMAs
+    f32x4 acc[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const half8 a = *reinterpret_cast<const half8*>(sA + (16 * m + lr) * AP + 32 * ks + kc8);
+        acc[m] = mfma16(a, bw[ks], acc[m]);
+      }
     }
-  }
 #pragma unroll
-  for (int o = 1; o < 4; o <<= 1) {
-    m_all = fmaxf(m_all, __shfl_xor(m_all, o));
-    m_text = fmaxf(m_text, __shfl_xor(m_text, o));
-    m_ts = fmaxf(m_ts, __shfl_xor(m_ts, o));
-  }
-  float s_all = 0.f, s_ts = 0.f, ba_v = -INFINITY, bt_v = -INFINITY;
-  int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!ok[j]) continue;
-    const int t = col0 + cq + j;
-    const float v = vals[j];
-    s_all += __expf(v - m_all);
-    if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
-    if (R.ts_begin >= 0 && t >= R.ts_begin) {
-      s_ts += __expf(v - m_ts);
-      if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+      for (int r = 0; r < 4; ++r) patch[(16 * m + 4 * (lane >> 4) + r) * 17 + lr] = acc[m][r];
+    // wave-private patch: the wave's own stores are visible to its loads in order
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    const int row = lane;
+    float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
+    float vals[16];
+    unsigned okm = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int t = col0 + c;
+      const float v = patch[row * 17 + c];
+      vals[c] = v;
+      const bool ok = row < B && t < V && allowed(t, smask, R, rr, false);
+      okm |= (unsigned)ok << c;
+      if (ok) {
+        m_all = fmaxf(m_all, v);
+        if (R.ts_begin >= 0 && t >= R.ts_begin) m_ts = fmaxf(m_ts, v);
+        else m_text = fmaxf(m_text, v);
+      }
     }
-  }
+    float s_all = 0.f, s_ts = 0.f, ba_v = -INFINITY, bt_v = -INFINITY;
+    int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
 #pragma unroll
-  for (int o = 1; o < 4; o <<= 1) {
-    s_all += __shfl_xor(s_all, o);
-    s_ts += __shfl_xor(s_ts, o);
-    const float ov = __shfl_xor(ba_v, o);
-    const int oi = __shfl_xor(ba_i, o);
-    if (better(ov, oi, ba_v, ba_i)) { ba_v = ov; ba_i = oi; }
-    const float tv = __shfl_xor(bt_v, o);
-    const int ti = __shfl_xor(bt_i, o);
-    if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; }
-  }
-  if ((tid & 3) == 0 && row < B) {
-    LogitPart p;
-    p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
-    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
-    parts[(int64_t)row * nblk + blockIdx.x] = p;
+    for (int c = 0; c < 16; ++c) {
+      if (!((okm >> c) & 1u)) continue;
+      const int t = col0 + c;
+      const float v = vals[c];
+      s_all += __expf(v - m_all);
+      if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
+      if (R.ts_begin >= 0 && t >= R.ts_begin) {
+        s_ts += __expf(v - m_ts);
+        if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+      }
+    }
+    if (row < B) {
+      LogitPart p;
+      p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
+      p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
+      parts[(int64_t)row * ntiles + tile] = p;
+    }
   }
 }
 
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s) {
-  JANUS_CHECK(K % 8 == 0, "logits: K must be a multiple of 8");
-  dim3 grid(logits_partial_blocks(V), (B + 63) / 64);
-  logits_partial_kernel<<<grid, 256, 0, s>>>(A, lda, W, K, V, B, R, smask, rules, parts);
+  JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
+  const int ntiles = logits_partial_blocks(V);
+  const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)kLgWaves * 64 * 17 * 4 + 64 * sizeof(RowRules);
+  auto kern = K == 384 ? logits_partial_kernel<12> : K == 512 ? logits_partial_kernel<16>
+                                                              : logits_partial_kernel<24>;
+  static bool attr[3] = {false, false, false};
+  const int ai = K == 384 ? 0 : K == 512 ? 1 : 2;
+  if (!attr[ai]) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr[ai] = true;
+  }
+  const int grid = std::min(256, (ntiles + kLgWaves - 1) / kLgWaves);
+  for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
+    kern<<<grid, kLgWaves * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
+                                          smask, rules + r0, parts + (int64_t)r0 * ntiles, ntiles);
   JANUS_LAUNCH_CHECK();
 }
 
