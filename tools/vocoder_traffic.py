@@ -39,6 +39,29 @@ def counters(d):
     return tot, len(n)
 
 
+def algorithmic_bytes(B=64, F=2584, latent=512, ch=512, ups=(8, 8, 2, 2, 2), n_k=3, n_d=3):
+    """Bytes each conv / fused-unit launch of one forward must move at least (fp16 tensors
+    read once, written once), following vocoder.cpp forward: (launches, total bytes)."""
+    n, tot = 0, 0
+    T = F
+    tot += 2 * B * (F * latent + F * ch); n += 1          # conv_pre
+    c = ch
+    for u in ups:
+        tot += 2 * B * (T * c + T * u * (c // 2)); n += 1  # ConvTranspose
+        T *= u
+        c //= 2
+        for kj in range(n_k):
+            for m in range(n_d):
+                last = m + 1 == n_d
+                acc = last and kj > 0
+                if c in (16, 32):                             # fused unit: x in, out (+ acc read)
+                    tot += 2 * B * T * c * (2 + (1 if acc else 0)); n += 1
+                else:                                         # c1: x -> S; c2: S, res x -> out
+                    tot += 2 * B * T * c * 2; n += 1
+                    tot += 2 * B * T * c * (3 + (1 if acc else 0)); n += 1
+    return n, tot
+
+
 def reduce(fdir, wdir, out):
     fetch_kb, nf = counters(fdir)
     write_kb, nw = counters(wdir)
@@ -49,6 +72,8 @@ def reduce(fdir, wdir, out):
                      "forward: the launch set the bench's roofline averages over)",
            "launches": nf, "fetch_bytes": fetch, "write_bytes": write,
            "bytes_per_launch": (fetch + write) / nf,
+           "algorithmic_bytes_per_launch": algorithmic_bytes()[1] / algorithmic_bytes()[0],
+           "algorithmic_launches": algorithmic_bytes()[0],
            "correction": "FETCH_SIZE x2 (gfx950 wide-read under-count), KB -> bytes x1024",
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes"}
     json.dump(res, open(out, "w"), indent=1)
