@@ -27,7 +27,15 @@ __global__ void resunit_pack_kernel(const float* __restrict__ w, _Float16* __res
 
 int resunit_kp(int C, int k) { return (k * C + 31) / 32 * 32; }
 
+bool resunit_wide_supported(int C, int k, int d);
+void resunit_wide_pack(const float* w, _Float16* out, int C, int k, hipStream_t s);
+void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s);
+
 void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
+  if (C >= 64) {  // resunit_wide.hip layout [kb][Cout][KB]
+    resunit_wide_pack(w, out, C, k, s);
+    return;
+  }
   const int KP = resunit_kp(C, k);
   resunit_pack_kernel<<<(C * KP + 255) / 256, 256, 0, s>>>(w, out, C, k, KP);
   JANUS_LAUNCH_CHECK();
@@ -255,12 +263,19 @@ static void resunit_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
-bool resunit_supported(int C, int k) { return (C == 16 || C == 32) && k >= 1 && k <= 11 && (k & 1); }
+bool resunit_supported(int C, int k) {
+  if (C >= 64) return resunit_wide_supported(C, k, 5);
+  return (C == 16 || C == 32) && k >= 1 && k <= 11 && (k & 1);
+}
 
 void resunit_launch(const ResUnitArgs& a, hipStream_t s) {
-  JANUS_CHECK(resunit_supported(a.C, a.k), "resunit: C must be 16 or 32, k odd <= 11");
+  JANUS_CHECK(resunit_supported(a.C, a.k), "resunit: C must be 16, 32, 64, 128 or 256, k odd <= 11");
   JANUS_CHECK(a.x != a.out, "resunit: out must not alias x");
   if (a.B <= 0 || a.T <= 0) return;
+  if (a.C >= 64) {
+    resunit_wide_launch(a, s);
+    return;
+  }
   // tile rows per block (JANUS_RU_BM overrides, for tuning sweeps)
   static const int bm = [] { const char* e = std::getenv("JANUS_RU_BM"); return e ? std::atoi(e) : 0; }();
   // measured (B=16, 30 s, accumulate): C16 BM 256 beats 512 by 1.8x (3 blocks/CU vs 2);

@@ -1,0 +1,336 @@
+// Fused ResBlock1 unit for the MFMA-width Firefly-GAN stages (C = 64, 128, 256):
+//   y = x + c2( silu( c1( silu(x) ) + b1 ) ) + b2 ;  out = (accumulate ? out : 0) + scale * y
+// (fish-speech ResBlock1.forward, one (convs1[m], convs2[m]) pair; same contract as the
+// narrow-stage kernel in resunit.hip).
+//
+// Why fused: run as two conv launches, a C = 128 unit moves ~1.3 KB of HBM per time row
+// (x read, intermediate written and re-read, residual read, output written) for
+// 4*C*C*k FLOP, which leaves the k = 3 / 7 units HBM-bound and the intermediate
+// round trip costs a launch boundary per conv. Here one block owns BM output rows:
+//   1. stage silu(x) rows [t0 - p2 - p1, t0 + MT1*16 - p2 + (k-1)d) for ALL C channels
+//      in LDS (every load of the tile in flight before the first store);
+//   2. c1 over MT1*16 rows (>= BM + k - 1: c2's halo) -> silu(. + b1) written as fp16
+//      into LDS over the dead sX tile (zero outside [0, T): c2's zero padding);
+//   3. c2 over BM rows from that LDS tile; the residual x and the ParallelBlock
+//      accumulator are loaded into registers at c2's start (in flight during its MFMAs);
+//   4. epilogue through an fp32 LDS tile, 16-byte coalesced loads/stores.
+// HBM per unit and time row: read x (+ residual re-read, L2-hot), write out (+ the
+// accumulator read on the last unit of a ResBlock1) = 2-3 x C x 2 B.
+//
+// Both convs are implicit GEMMs on v_mfma_f32_16x16x32_f16 with K = k*C ordered
+// tap-major: the 32-wide K step of a lane group lies inside one tap, so the A fragment is
+// the LDS tile row (m*16 + lane%16 + tap*dil) at channel offset ci. Weights stream from
+// L2 in [KB x C] k-blocks (packed [kb][Cout][KB]), double-buffered through LDS, one
+// barrier per k-block.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+// packed[(kb*C + co)*KB + j] = w[co][ci][tap] with kk = kb*KB + j, tap = kk / C, ci = kk % C
+__global__ void resunit_wide_pack_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
+                                         int C, int k, int KB) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)k * C * C;
+  if (idx >= total) return;
+  const int j = (int)(idx % KB);
+  const int co = (int)((idx / KB) % C);
+  const int kb = (int)(idx / ((int64_t)KB * C));
+  const int kk = kb * KB + j;
+  const int tap = kk / C, ci = kk % C;
+  out[idx] = (_Float16)w[((int64_t)co * C + ci) * k + tap];
+}
+
+template <int C> struct WideCfg;
+// BM output rows per block, WM x WN waves (wave tile: every WM-th m-tile x C/WN columns),
+// KB = K per weight k-block. LDS <= 80 KB for C <= 128 (two blocks per CU).
+template <> struct WideCfg<64> { static constexpr int BM = 240, WM = 4, WN = 1, KB = 32; };
+template <> struct WideCfg<128> { static constexpr int BM = 128, WM = 1, WN = 4, KB = 32; };
+template <> struct WideCfg<256> { static constexpr int BM = 112, WM = 2, WN = 4, KB = 32; };
+
+template <int C>
+struct WideGeo {
+  using Cfg = WideCfg<C>;
+  static constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN, KB = Cfg::KB;
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int LI = frag_pitch(C);        // activation row pitch (halves)
+  static constexpr int LW = frag_pitch(KB);       // weight row pitch (halves)
+  static constexpr int CPR = C / 8;               // 16-byte chunks per activation row
+  static constexpr int MT1 = (BM + 10 + 15) / 16; // c1 m-tiles (k <= 11)
+  static constexpr int MT2 = BM / 16;             // c2 m-tiles
+  static constexpr int MW1 = (MT1 + WM - 1) / WM; // c1 m-tiles per wave
+  static constexpr int MW2 = (MT2 + WM - 1) / WM; // c2 m-tiles per wave
+  static constexpr int NTW = C / 16 / WN;         // n-tiles per wave
+  static constexpr int R0MAX = MT1 * 16 + 50;     // staged x rows, (k-1)*d <= 50
+  static constexpr int NLD = (R0MAX * CPR + NT - 1) / NT;
+  static constexpr int ES = C + 4;                // fp32 epilogue row pitch
+  static constexpr int NE = (BM * CPR + NT - 1) / NT;
+  static constexpr int WCH = C * KB / 8 / NT;     // weight uint4 per thread per k-block
+  static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
+  static constexpr int ACT_H = (ACT + 7) / 8 * 8; // halves
+  // the fp32 epilogue tile spans the activation AND weight regions (both dead by then)
+  static constexpr size_t LDS = std::max(((size_t)ACT_H + 2 * (size_t)C * LW) * 2,
+                                         (size_t)BM * ES * 4);
+  static_assert(BM % 16 == 0 && C % (16 * WN) == 0, "tiling");
+  static_assert(C * KB / 8 % NT == 0, "weight k-block split");
+  static_assert(KB <= C && C % KB == 0 && KB % 32 == 0, "k-block inside one tap");
+  static_assert((C / KB) % 2 == 0, "even k-block count (two register slots)");
+};
+
+// EPF: load the residual / accumulator rows at c2's start (in flight during its MFMAs)
+// instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
+template <int C, bool EPF>
+__global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnitArgs a,
+                                                                         int tiles_per_utt) {
+  using G = WideGeo<C>;
+  constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
+  constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
+  constexpr int NTW = G::NTW, ES = G::ES;
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* sX = smem;                         // [R0][LI] silu(x)
+  _Float16* sS = smem;                         // [MT1*16][LI] silu(c1 + b1) (over sX)
+  float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS and sW)
+  _Float16* sW = smem + G::ACT_H;              // [2][C][LW]
+
+  const int k = a.k, d = a.d, T = a.T;
+  const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
+  const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
+  const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
+  const int b = blockIdx.x / tiles_per_utt, t0 = (blockIdx.x % tiles_per_utt) * BM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const _Float16* xb = a.x + (int64_t)b * T * C;
+  _Float16* ob = a.out + (int64_t)b * T * C;
+  const int nkb = k * C / KB;
+
+  // weight k-blocks: two register slots, each load issued two k-blocks before its LDS
+  // store (an L2 round trip is longer than one k-block of MFMAs at KB = 32). Plain
+  // locals + macros: captured by reference in lambdas they were left in scratch memory.
+  static_assert(G::WCH == 1 || G::WCH == 2, "weight slot width");
+  const int wsrc0 = (tid / (KB / 8)) * KB + (tid % (KB / 8)) * 8;
+  const int wdst0 = (tid / (KB / 8)) * LW + (tid % (KB / 8)) * 8;
+  const int wsrc1 = ((tid + NT) / (KB / 8)) * KB + ((tid + NT) % (KB / 8)) * 8;
+  const int wdst1 = ((tid + NT) / (KB / 8)) * LW + ((tid + NT) % (KB / 8)) * 8;
+  uint4 rwA0, rwA1, rwB0, rwB1;
+#define WIDE_WLOAD(R0_, R1_, WP, KBI)                                                   \
+  do {                                                                                  \
+    const _Float16* src_ = (WP) + (int64_t)(KBI) * C * KB;                              \
+    R0_ = *reinterpret_cast<const uint4*>(src_ + wsrc0);                                \
+    if constexpr (G::WCH == 2) R1_ = *reinterpret_cast<const uint4*>(src_ + wsrc1);      \
+  } while (0)
+#define WIDE_WSTORE(R0_, R1_, BUF)                                                      \
+  do {                                                                                  \
+    _Float16* dst_ = sW + (BUF) * C * LW;                                               \
+    *reinterpret_cast<uint4*>(dst_ + wdst0) = R0_;                                      \
+    if constexpr (G::WCH == 2) *reinterpret_cast<uint4*>(dst_ + wdst1) = R1_;            \
+  } while (0)
+
+  // ---- 1. stage silu(x): all loads in flight, then convert + store
+  {
+    const int xbase = t0 - p2 - p1;
+    uint4 pf[G::NLD];
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cc = idx % CPR;
+      const int t = xbase + r;
+      pf[i] = (r < R0 && t >= 0 && t < T)
+                  ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * C + cc * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+    WIDE_WLOAD(rwA0, rwA1, a.w1, 0);
+    WIDE_WLOAD(rwB0, rwB1, a.w1, 1);
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cc = idx % CPR;
+      if (r < R0) {
+        half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
+      }
+    }
+    WIDE_WSTORE(rwA0, rwA1, 0);
+  }
+  __syncthreads();
+
+  const int kq = 8 * (lane >> 4);
+  const int arow = lane & 15;
+  const _Float16* bbase = sW + (wn * NTW * 16 + arow) * LW + kq;
+
+  // one k-block of MFMAs: A rows (m*16 + lane%16 + tap*dil) of src, B from weight buffer buf
+  auto mma = [&](auto& acc, auto mw_tag, auto mt_tag, const _Float16* src, int dil, int kb,
+                 int buf) __attribute__((always_inline)) {
+    constexpr int MW = decltype(mw_tag)::value, MT = decltype(mt_tag)::value;
+    const _Float16* wb = bbase + buf * C * LW;
+#pragma unroll
+    for (int ks = 0; ks < KB / 32; ++ks) {
+      const int kk = kb * KB + ks * 32;  // wave-uniform: one tap
+      const int tap = kk / C, ci = kk % C;
+      half8 bw[NTW];
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) bw[n] = *reinterpret_cast<const half8*>(wb + n * 16 * LW + ks * 32);
+      const _Float16* ap = src + (wm * 16 + arow + tap * dil) * LI + ci + kq;
+#pragma unroll
+      for (int j = 0; j < MW; ++j) {
+        if (wm + j * WM >= MT) break;
+        const half8 av = *reinterpret_cast<const half8*>(ap + j * WM * 16 * LI);
+#pragma unroll
+        for (int n = 0; n < NTW; ++n) acc[j][n] = mfma16(av, bw[n], acc[j][n]);
+      }
+    }
+  };
+  // the K loop of one conv; on entry buffer 0 holds k-block 0 and slot B k-block 1
+  // (nkb = k*C/KB is even: two k-blocks per trip keep the register slots static; the
+  // loads are unconditional (clamped index) so the compiler's vmcnt for slot B never
+  // has to cover slot A's younger loads)
+#define WIDE_KLOOP(ACC, MWT, MTT, WP, SRC, DIL)                                         \
+  for (int kb = 0; kb < nkb; kb += 2) {                                                 \
+    WIDE_WLOAD(rwA0, rwA1, WP, min(kb + 2, nkb - 1));                                   \
+    mma(ACC, MWT{}, MTT{}, SRC, DIL, kb, 0);                                            \
+    WIDE_WSTORE(rwB0, rwB1, 1);                                                         \
+    __syncthreads();                                                                    \
+    WIDE_WLOAD(rwB0, rwB1, WP, min(kb + 3, nkb - 1));                                   \
+    mma(ACC, MWT{}, MTT{}, SRC, DIL, kb + 1, 1);                                        \
+    if (kb + 2 < nkb) WIDE_WSTORE(rwA0, rwA1, 0);                                       \
+    __syncthreads();                                                                    \
+  }
+  using MW1T = std::integral_constant<int, MW1>;
+  using MT1T = std::integral_constant<int, MT1>;
+  using MW2T = std::integral_constant<int, MW2>;
+  using MT2T = std::integral_constant<int, MT2>;
+
+  // ---- 2. c1 over MT1*16 rows (row r <-> time t0 - p2 + r): A = sX[r + tap*d]
+  {
+    f32x4 acc[MW1][NTW];
+#pragma unroll
+    for (int j = 0; j < MW1; ++j)
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) acc[j][n] = zero_f32x4();
+    WIDE_KLOOP(acc, MW1T, MT1T, a.w1, sX, d);
+    // sX is dead (last barrier of the loop): write silu(c1 + b1) over it
+    WIDE_WLOAD(rwA0, rwA1, a.w2, 0);
+    WIDE_WLOAD(rwB0, rwB1, a.w2, 1);
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) {
+      const int co = (wn * NTW + n) * 16 + arow;
+      const float bias = a.b1[co];
+#pragma unroll
+      for (int j = 0; j < MW1; ++j) {
+        const int m = wm + j * WM;
+        if (m >= MT1) break;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = m * 16 + 4 * (lane >> 4) + rr;
+          const int t = t0 - p2 + r;
+          const float v = (r < R1 && t >= 0 && t < T) ? silu(acc[j][n][rr] + bias) : 0.0f;
+          sS[r * LI + co] = (_Float16)v;
+        }
+      }
+    }
+    WIDE_WSTORE(rwA0, rwA1, 0);
+  }
+  __syncthreads();
+
+  // residual x and accumulator rows of this tile
+  uint4 rq[G::NE], pq[G::NE];
+  auto epi_load = [&]() {
+#pragma unroll
+    for (int i = 0; i < G::NE; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cg = (idx % CPR) * 8;
+      const bool ok = r < BM && t0 + r < T;
+      const int64_t o = (int64_t)(t0 + r) * C + cg;
+      rq[i] = ok ? *reinterpret_cast<const uint4*>(xb + o) : make_uint4(0, 0, 0, 0);
+      pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(ob + o) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if constexpr (EPF) epi_load();
+
+  // ---- 3. c2 over BM rows (row r <-> time t0 + r): A = sS[r + tap]
+  f32x4 acc2[MW2][NTW];
+#pragma unroll
+  for (int j = 0; j < MW2; ++j)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc2[j][n] = zero_f32x4();
+  WIDE_KLOOP(acc2, MW2T, MT2T, a.w2, sS, 1);
+  if constexpr (!EPF) epi_load();
+
+  // ---- 4. epilogue: c2 + b2 -> fp32 LDS tile (sS dead), then 16-byte row chunks
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    const int co = (wn * NTW + n) * 16 + arow;
+    const float bias = a.b2[co];
+#pragma unroll
+    for (int j = 0; j < MW2; ++j) {
+      const int m = wm + j * WM;
+      if (m >= MT2) break;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + co] = acc2[j][n][rr] + bias;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < G::NE; ++i) {
+    const int idx = tid + i * NT;
+    const int r = idx / CPR, cg = (idx % CPR) * 8;
+    if (r >= BM || t0 + r >= T) continue;
+    const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
+    const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const half8 xv = *reinterpret_cast<const half8*>(&rq[i]);
+    const half8 pv = *reinterpret_cast<const half8*>(&pq[i]);
+    half8 hv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+    *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+  }
+}
+
+#undef WIDE_WLOAD
+#undef WIDE_WSTORE
+#undef WIDE_KLOOP
+
+template <int C, bool EPF>
+static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
+  using G = WideGeo<C>;
+  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
+  static_assert(G::LDS <= 160 * 1024, "LDS");
+  auto kern = resunit_wide_kernel<C, EPF>;
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)G::LDS));
+    attr = true;
+  }
+  const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
+  JANUS_LAUNCH_CHECK();
+}
+
+bool resunit_wide_supported(int C, int k, int d) {
+  static const bool off = std::getenv("JANUS_NO_WIDE_UNITS") != nullptr;
+  return !off && (C == 64 || C == 128 || C == 256) && k >= 1 && k <= 11 && (k & 1) &&
+         (k - 1) * d <= 50;
+}
+
+void resunit_wide_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
+  const int KB = C == 64 ? WideCfg<64>::KB : C == 128 ? WideCfg<128>::KB : WideCfg<256>::KB;
+  const int64_t total = (int64_t)k * C * C;
+  resunit_wide_pack_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(w, out, C, k, KB);
+  JANUS_LAUNCH_CHECK();
+}
+
+void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
+  static const int epf = [] { const char* e = std::getenv("JANUS_WIDE_EPF"); return e ? std::atoi(e) : 1; }();
+  if (a.C == 64) epf ? wide_cfg<64, true>(a, s) : wide_cfg<64, false>(a, s);
+  else if (a.C == 128) epf ? wide_cfg<128, true>(a, s) : wide_cfg<128, false>(a, s);
+  else if (a.C == 256) epf ? wide_cfg<256, true>(a, s) : wide_cfg<256, false>(a, s);
+  else throw Error("resunit (wide): C must be 64, 128 or 256");
+}
+
+}  // namespace janus

@@ -141,10 +141,13 @@ def test_conv1d(gpu, case):
     assert err < 2e-3, err
 
 
-@pytest.mark.parametrize("C,k,d,acc", [(16, 3, 1, 0), (16, 11, 5, 1), (32, 7, 3, 0), (32, 11, 5, 1),
-                                       (16, 7, 1, 1), (32, 3, 3, 0)])
-def test_resunit(gpu, C, k, d, acc):
-    B, T = 2, 1500
+@pytest.mark.parametrize("C,k,d,acc,T", [(16, 3, 1, 0, 1500), (16, 11, 5, 1, 1500), (32, 7, 3, 0, 1500),
+                                         (32, 11, 5, 1, 1500), (16, 7, 1, 1, 1500), (32, 3, 3, 0, 1500),
+                                         (64, 3, 1, 0, 1500), (64, 11, 5, 1, 1500), (64, 7, 3, 1, 37),
+                                         (128, 7, 3, 1, 1500), (128, 11, 5, 0, 1500), (128, 3, 1, 1, 129),
+                                         (256, 3, 1, 1, 700), (256, 11, 5, 0, 700), (256, 7, 3, 1, 20)])
+def test_resunit(gpu, C, k, d, acc, T):
+    B = 2
     g = torch.Generator().manual_seed(C * 100 + k * 10 + d)
     x = torch.randn(B, T, C, generator=g).half()
     w1 = torch.randn(C, C, k, generator=g) / math.sqrt(C * k)

@@ -34,9 +34,13 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--units-only", action="store_true")
     ap.add_argument("--xattn", action="store_true")
+    ap.add_argument("--wide", action="store_true")
     a = ap.parse_args()
     if a.xattn:
         xattn_bench()
+        return
+    if a.wide:
+        wide_units(a.batch, a.reps)
         return
     if a.units_only:
         resunits(a.batch, a.reps)
@@ -115,6 +119,53 @@ def resunits(B, reps):
               f"{byts / ms / 1e6:8.1f} GB/s", flush=True)
 
 
+
+
+def _time(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def wide_units(B, reps):
+    """Fused ResBlock1 unit (resunit_wide.hip) vs the same unit as two conv launches."""
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    for (C, k, d, T) in [(256, 3, 1, 20672), (256, 11, 5, 20672), (128, 3, 1, 165376), (128, 7, 3, 165376),
+                         (128, 11, 5, 165376), (64, 3, 1, 330752), (64, 7, 3, 330752), (64, 11, 5, 330752)]:
+        x = torch.randn(B, T, C, device=dev).half()
+        out = torch.empty_like(x)
+        mid = torch.empty_like(x)
+        w = [(torch.randn(C, C, k, device=dev) / math.sqrt(C * k)).float() for _ in range(2)]
+        bias = torch.zeros(C, device=dev)
+        n = nat.lib().janus_resunit_packed_size(C, k)
+        pu = [torch.empty(n, dtype=torch.float16, device=dev) for _ in range(2)]
+        pc = [torch.empty(nat.lib().janus_conv1d_packed_size(C, C, k, 0, 1), dtype=torch.float16, device=dev)
+              for _ in range(2)]
+        for i in range(2):
+            nat.call("janus_resunit_pack", w[i].data_ptr(), pu[i].data_ptr(), C, k, s)
+            nat.call("janus_conv1d_pack", w[i].data_ptr(), pc[i].data_ptr(), C, C, k, 0, 1, s)
+
+        def fused():
+            nat.call("janus_resunit_f16", x.data_ptr(), out.data_ptr(), pu[0].data_ptr(), bias.data_ptr(),
+                     pu[1].data_ptr(), bias.data_ptr(), B, T, C, k, d, 1.0 / 3.0, 1, s)
+
+        def pair():
+            nat.call("janus_conv1d_f16", x.data_ptr(), B, T, C, pc[0].data_ptr(), bias.data_ptr(),
+                     mid.data_ptr(), T, C, k, 1, d * (k - 1) // 2, d, 0, 1, 1, None, 0, 1.0, 0, s)
+            nat.call("janus_conv1d_f16", mid.data_ptr(), B, T, C, pc[1].data_ptr(), bias.data_ptr(),
+                     out.data_ptr(), T, C, k, 1, (k - 1) // 2, 1, 0, 0, 0, x.data_ptr(), T * C,
+                     1.0 / 3.0, 1, s)
+        flops = 2 * 2.0 * C * C * k * T * B
+        mf, mp = _time(fused, reps), _time(pair, reps)
+        print(f"wide C{C:3d} k{k:2d} d{d} B={B} T={T:7d} fused {mf:7.3f} ms {flops / mf / 1e9:7.1f} TF/s | "
+              f"two convs {mp:7.3f} ms {flops / mp / 1e9:7.1f} TF/s", flush=True)
 
 
 def xattn_bench(reps=20):
