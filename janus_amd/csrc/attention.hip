@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const _Float16* __restri
   __shared__ __attribute__((aligned(16))) _Float16 sP[4][16 * kLS];
 
   const int b = blockIdx.z, h = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int d = H * kHd;
   const int64_t ld = 3 * (int64_t)d;
   const _Float16* base = qkv + (int64_t)b * T * ld;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void decode_split_kernel(
   __shared__ float acc_s[4][kMaxHeads * kHd];
   __shared__ float mh[kMaxHeads], lh[kMaxHeads];
   const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int d = H * kHd;
   const bool active = lane * 8 < d;
   const int head = lane >> 3;

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
   const int bm = bid / nbn, bn = bid % nbn;
   const int ph = blockIdx.y, b = blockIdx.z;
   const int r0 = bm * BM, co0 = bn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
   const int wm = wid / WN, wn = wid % WN;
 
   const int lo_tap = min(0, (a.taps - 1) * a.dil);

@@ -314,7 +314,7 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
   _Float16* sA = lg_smem;                                            // [64][AP]
   float* sT = reinterpret_cast<float*>(sA + 64 * AP);                // [waves][64][17]
   RowRules* sR = reinterpret_cast<RowRules*>(sT + kLgWaves * 64 * 17);  // [64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   for (int i = tid; i < 64 * (K / 8); i += kLgWaves * 64) {
     const int r = i / (K / 8), c8 = (i % (K / 8)) * 8;
     uint4 v = make_uint4(0, 0, 0, 0);
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
     float* __restrict__ sum_lp, int32_t* __restrict__ n_tok) {
   __shared__ LogitPart sh[4];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   int32_t* row_tok = tokens + (int64_t)b * ld;
   if (done[b]) {
     if (tid == 0) row_tok[pos + 1] = R.eot;

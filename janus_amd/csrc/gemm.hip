@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   const int bid = xcd_remap(blockIdx.x, nbm * nbn);
   const int bm = bid / nbn, bn = bid % nbn;
   const int row0 = bm * BM, col0 = bn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
   const int wm = wid / WN, wn = wid % WN;
 
   uint4 ra[A_CH], rb[B_CH];
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   __shared__ float s_mean[64], s_rstd[64];
   const int M = p.M, N = p.N, K = p.K;
   const int col0 = blockIdx.x * 16;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int kq = ((K + kSkWaves - 1) / kSkWaves + 31) / 32 * 32;
   const int kbeg = w * kq, kend = min(K, kbeg + kq);
   const int bcol = col0 + (lane & 15);

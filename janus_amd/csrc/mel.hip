@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void mel_kernel(const float* __restrict__ pcm,
   __shared__ float ps[kFT * kPS];
   __shared__ float redmax[4];
   const int b = blockIdx.y, f0 = blockIdx.x * kFT;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int64_t base = offsets[b];
   const int64_t n16 = (offsets[b + 1] - base + decim - 1) / decim;  // len(x[::decim])
   const float* x = pcm + base;

@@ -34,6 +34,11 @@ __device__ __forceinline__ half8 zero_half8() {
   return z;
 }
 
+// Wave index within the block as a wave-uniform (SGPR) value: tid >> 6 alone is a VGPR
+// to the compiler, so branches on it (m-tile / head ownership) became exec-masked
+// branches with accumulators shuttled through VGPRs around every MFMA.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ f32x4 zero_f32x4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 // LDS row pitch (in halves) for tiles read as MFMA fragments with ds_read_b128: a pitch

@@ -41,40 +41,56 @@ void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
-template <int C, int BM>
-struct ResUnitGeo {
-  // halves per activation row: conflict-free fragment pitch for C = 32; C = 16 keeps the
-  // 48-B pitch (its sS/sX store pattern measured 10% faster than the 32-B one)
-  static constexpr int LI = C == 16 ? 24 : frag_pitch(C);
-  static constexpr int CPR = C / 8;                         // 16-byte chunks per row
-  static constexpr int R0MAX = BM + 10 + 50;                // k <= 11, d <= 5
-  static constexpr int NPF = (R0MAX * CPR + 255) / 256;     // prefetch uint4 per thread
-  static constexpr int MT1 = ((BM + 10 + 15) / 16 + 3) / 4; // c1 M-tiles per wave
-  static constexpr int MT2 = BM / 64;                       // c2 M-tiles per wave
-  static constexpr int ES = C + 4;                          // fp32 epilogue row stride
-  static constexpr int NE = BM * CPR / 256;                 // epilogue uint4 per thread
+// Compile-time geometry: C channels, K taps, dilation D, BM output rows per tile.
+// c1 covers M1 = BM + 16 rows (>= BM + K - 1, c2's halo); a 16x16x32 MFMA k-step spans
+// TPK = 32 / C taps, so K rounds up to TP taps with zero weights on the padding tap;
+// every row a padding tap touches is staged (and finite), so the MFMA loop has no guards.
+template <int C, int K, int D, int BM>
+struct NarrowGeo {
+  static constexpr int NT = 256;
+  static constexpr int TPK = 32 / C;                    // taps per k-step
+  static constexpr int KS = (K + TPK - 1) / TPK;        // k-steps per conv
+  static constexpr int KP = KS * 32;                    // packed K (resunit_kp)
+  static constexpr int TP = KS * TPK;                   // taps incl. padding
+  static constexpr int P1 = D * (K - 1) / 2, P2 = (K - 1) / 2;
+  static constexpr int LI = frag_pitch(C);              // activation pitch (halves)
+  static constexpr int LW = frag_pitch(KP);             // weight pitch (halves)
+  static constexpr int CPR = C / 8;                     // 16-byte chunks per row
+  static constexpr int MT1 = BM / 16 + 1, M1 = MT1 * 16;
+  static constexpr int MT2 = BM / 16;
+  static constexpr int MW1 = (MT1 + 3) / 4, MW2 = (MT2 + 3) / 4;
+  static constexpr int NTL = C / 16;                    // n-tiles (all per wave)
+  static constexpr int R0 = M1 + (TP - 1) * D;          // staged x rows
+  static constexpr int NPF = (R0 * CPR + NT - 1) / NT;  // prefetch uint4 per thread
+  static constexpr int ES = C + 4;                      // fp32 epilogue pitch
+  static constexpr int NE = (BM * CPR + NT - 1) / NT;   // epilogue uint4 per thread
+  // LDS (halves): [sX | sS | sE alias] [sR] [sW1] [sW2]
+  static constexpr int ACT = std::max(std::max(R0 * LI, M1 * LI), BM * ES * 2);
+  static constexpr int ACT_H = (ACT + 7) / 8 * 8;
+  static constexpr int LDS_H = ACT_H + BM * LI + 2 * C * LW;
+  static constexpr size_t LDS = (size_t)LDS_H * 2;
+  static_assert(KP == (K * C + 31) / 32 * 32, "matches resunit_kp");
+  static_assert(BM % 16 == 0 && M1 >= BM + K - 1 && M1 >= BM + TP - 1, "c2 halo");
 };
 
-// Persistent: each block loads both weight matrices into LDS once, then walks tiles
-// (b, 16*BM-row blocks) with the next tile's input rows prefetched into registers
-// while the current tile computes, so HBM latency overlaps the MFMA/LDS work.
-template <int C, int BM>
-__global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int tiles_per_utt,
-                                                      int n_tiles, int act_halves) {
-  using G = ResUnitGeo<C, BM>;
-  constexpr int LI = G::LI, CPR = G::CPR, NT = C / 16, MT1 = G::MT1, MT2 = G::MT2, ES = G::ES;
+// Persistent: weights staged once; per tile the next tile's x rows are loaded into
+// registers while this tile computes. Edge tiles (the first and last of an utterance)
+// take the guarded epilogue path; interior tiles run unguarded.
+template <int C, int K, int D, int BM>
+__global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_per_utt, int n_tiles) {
+  using G = NarrowGeo<C, K, D, BM>;
+  constexpr int LI = G::LI, LW = G::LW, CPR = G::CPR, ES = G::ES, NTL = G::NTL;
+  constexpr int MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2, M1 = G::M1;
+  constexpr int P1 = G::P1, P2 = G::P2, R0 = G::R0, KS = G::KS, KP = G::KP;
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
-  const int k = a.k, d = a.d, T = a.T;
-  const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
-  const int R1 = BM + 2 * p2, R0 = R1 + 2 * p1;
-  const int LW = frag_pitch(KP);
-  _Float16* sX = smem;                        // [R0][LI]   silu(x)
-  _Float16* sS = sX + R0 * LI;                // [R1p][LI]  silu(c1(.) + b1)
-  float* sE = reinterpret_cast<float*>(smem); // [BM][ES] epilogue tile (aliases sX/sS)
-  _Float16* sR = smem + act_halves;           // [BM][LI]   raw x (the unit's residual)
+  _Float16* sX = smem;                        // [R0][LI]  silu(x)
+  _Float16* sS = smem;                        // [M1][LI]  silu(c1 + b1), over dead sX
+  float* sE = reinterpret_cast<float*>(smem); // [BM][ES]  c2 + b2, over dead sS
+  _Float16* sR = smem + G::ACT_H;             // [BM][LI]  raw x (the residual)
   _Float16* sW1 = sR + BM * LI;               // [C][LW]
   _Float16* sW2 = sW1 + C * LW;               // [C][LW]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
 
   for (int idx = tid; idx < C * (KP / 8); idx += 256) {
     const int co = idx / (KP / 8), cc = idx % (KP / 8);
@@ -83,34 +99,50 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
     *reinterpret_cast<uint4*>(sW2 + co * LW + cc * 8) =
         *reinterpret_cast<const uint4*>(a.w2 + (int64_t)co * KP + cc * 8);
   }
+  // per-lane bias of the lane's output column (one per n-tile)
+  float bias1[NTL], bias2[NTL];
+#pragma unroll
+  for (int n = 0; n < NTL; ++n) {
+    bias1[n] = a.b1[n * 16 + (lane & 15)];
+    bias2[n] = a.b2[n * 16 + (lane & 15)];
+  }
 
   uint4 pf[G::NPF];
-  auto prefetch = [&](int tile) {
-    const int b = tile / tiles_per_utt, t0 = (tile % tiles_per_utt) * BM;
-    const _Float16* xb = a.x + (int64_t)b * T * C;
-    const int xbase = t0 - p2 - p1;
-#pragma unroll
-    for (int i = 0; i < G::NPF; ++i) {
-      const int idx = tid + i * 256;
-      const int r = idx / CPR, cc = idx % CPR;
-      const int t = xbase + r;
-      pf[i] = (tile < n_tiles && r < R0 && t >= 0 && t < T)
-                  ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * C + cc * 8)
-                  : make_uint4(0, 0, 0, 0);
-    }
-  };
-  prefetch(blockIdx.x);
+#define NARROW_PREFETCH(TILE)                                                               \
+  do {                                                                                      \
+    const int tl_ = (TILE);                                                                 \
+    const int b_ = tl_ / tiles_per_utt, t0_ = (tl_ % tiles_per_utt) * BM;                   \
+    const _Float16* xb_ = a.x + (int64_t)b_ * T * C;                                        \
+    _Pragma("unroll") for (int i = 0; i < G::NPF; ++i) {                                    \
+      const int idx = tid + i * 256;                                                        \
+      const int r = idx / CPR, cc = idx % CPR;                                              \
+      const int t = t0_ - P2 - P1 + r;                                                      \
+      pf[i] = (tl_ < n_tiles && r < R0 && t >= 0 && t < T)                                 \
+                  ? *reinterpret_cast<const uint4*>(xb_ + (int64_t)t * C + cc * 8)          \
+                  : make_uint4(0, 0, 0, 0);                                                 \
+    }                                                                                       \
+  } while (0)
+  NARROW_PREFETCH(blockIdx.x);
+
+  // fragment addressing: lane row (lane & 15); k chunk 8*(lane >> 4) -> tap / channel
+  const int arow = lane & 15;
+  const int kq = 8 * (lane >> 4);
+  const int ltap = kq / C, lci = kq % C;      // tap offset and channel of this lane's chunk
+  const int a1_off = arow * LI + ltap * D * LI + lci;  // + (m*16 + 2*ks*D... ) below
+  const int a2_off = arow * LI + ltap * LI + lci;
+  const int b_off = arow * LW + kq;
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int b = tile / tiles_per_utt, t0 = (tile % tiles_per_utt) * BM;
-    __syncthreads();  // previous tile's epilogue reads of sE are done (and W staged)
+    const bool edge = (t0 - P2 < 0) || (t0 - P2 + M1 > T) || (t0 + BM > T);
+    __syncthreads();  // previous tile's epilogue is done with sE / sR
 #pragma unroll
     for (int i = 0; i < G::NPF; ++i) {
       const int idx = tid + i * 256;
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
-        const int rr = r - p2 - p1;
+        const int rr = r - P2 - P1;
         if (rr >= 0 && rr < BM) *reinterpret_cast<half8*>(sR + rr * LI + cc * 8) = v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
@@ -118,59 +150,60 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
       }
     }
     __syncthreads();
-    prefetch(tile + gridDim.x);  // in flight during this tile's compute
+    NARROW_PREFETCH(tile + gridDim.x);  // in flight during this tile's compute
     _Float16* ob = a.out + (int64_t)b * T * C;
-    uint4 acc_in[G::NE];         // accumulate target, also in flight during compute
-    if (a.accumulate) {
+    uint4 acc_in[G::NE];
 #pragma unroll
-      for (int i = 0; i < G::NE; ++i) {
-        const int idx = tid + i * 256;
-        const int r = idx / CPR, cg = (idx % CPR) * 8;
-        acc_in[i] = t0 + r < T ? *reinterpret_cast<const uint4*>(ob + (int64_t)(t0 + r) * C + cg)
-                               : make_uint4(0, 0, 0, 0);
-      }
+    for (int i = 0; i < G::NE; ++i) {
+      const int idx = tid + i * 256;
+      const int r = idx / CPR, cg = (idx % CPR) * 8;
+      acc_in[i] = (a.accumulate && r < BM && t0 + r < T)
+                      ? *reinterpret_cast<const uint4*>(ob + (int64_t)(t0 + r) * C + cg)
+                      : make_uint4(0, 0, 0, 0);
     }
 
-    // ---- c1 over R1 rows (c1 row r <-> time t0 - p2 + r): A = sX[r + tap*d]
+    // ---- c1 over M1 rows (row r <-> time t0 - P2 + r): A = sX[r + tap*D]
     {
-      f32x4 acc[MT1][NT];
+      f32x4 acc[MW1][NTL];
 #pragma unroll
-      for (int j = 0; j < MT1; ++j)
+      for (int j = 0; j < MW1; ++j)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[j][n] = zero_f32x4();
-      for (int ks = 0; ks < KP / 32; ++ks) {
-        const int kk = ks * 32 + 8 * (lane >> 4);
-        const int tap = kk / C, ci = kk % C;
-        const bool ok = tap < k;
-        half8 bw[NT];
+        for (int n = 0; n < NTL; ++n) acc[j][n] = zero_f32x4();
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-          bw[n] = *reinterpret_cast<const half8*>(sW1 + (n * 16 + (lane & 15)) * LW + kk);
+      for (int ks = 0; ks < KS; ++ks) {
+        half8 bw[NTL];
 #pragma unroll
-        for (int j = 0; j < MT1; ++j) {
-          const int m = w + 4 * j;
-          if (m * 16 >= R1) break;
-          const int r = m * 16 + (lane & 15);
-          half8 av = zero_half8();
-          if (ok && r < R1) av = *reinterpret_cast<const half8*>(sX + (r + tap * d) * LI + ci);
+        for (int n = 0; n < NTL; ++n)
+          bw[n] = *reinterpret_cast<const half8*>(sW1 + b_off + n * 16 * LW + ks * 32);
 #pragma unroll
-          for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(av, bw[n], acc[j][n]);
+        for (int j = 0; j < MW1; ++j) {
+          // a wave past the last m-tile recomputes it (result dropped in the epilogue):
+          // no branch around the MFMA — branches there made the compiler shuttle
+          // accumulators between AGPRs and overwrite a pending MFMA's srcC (gfx950)
+          const int m = min(w + 4 * j, MT1 - 1);
+          const half8 av = *reinterpret_cast<const half8*>(
+              sX + a1_off + (m * 16 + ks * G::TPK * D) * LI);
+#pragma unroll
+          for (int n = 0; n < NTL; ++n) acc[j][n] = mfma16(av, bw[n], acc[j][n]);
         }
       }
+      __syncthreads();  // every wave is done reading sX
 #pragma unroll
-      for (int j = 0; j < MT1; ++j) {
+      for (int j = 0; j < MW1; ++j) {
         const int m = w + 4 * j;
-        if (m * 16 >= R1) break;
+        if (j >= MT1 / 4 && m >= MT1) continue;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const int co = n * 16 + (lane & 15);
-          const float bias = a.b1[co];
+        for (int n = 0; n < NTL; ++n) {
+          const int co = n * 16 + arow;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int r = m * 16 + 4 * (lane >> 4) + rr;
-            const int t = t0 - p2 + r;
-            const float v = (r < R1 && t >= 0 && t < T) ? silu(acc[j][n][rr] + bias) : 0.0f;
-            sS[r * LI + co] = (_Float16)v;  // c2 zero-pads its input outside [0, T)
+            float v = silu(acc[j][n][rr] + bias1[n]);
+            if (edge) {  // c2 zero-pads its input outside [0, T)
+              const int t = t0 - P2 + r;
+              v = (t >= 0 && t < T) ? v : 0.0f;
+            }
+            sS[r * LI + co] = (_Float16)v;
           }
         }
       }
@@ -178,48 +211,42 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
     __syncthreads();
 
     // ---- c2 over BM rows (row r <-> time t0 + r): A = sS[r + tap]
-    f32x4 acc2[MT2][NT];
+    f32x4 acc2[MW2][NTL];
 #pragma unroll
-    for (int j = 0; j < MT2; ++j)
+    for (int j = 0; j < MW2; ++j)
 #pragma unroll
-      for (int n = 0; n < NT; ++n) acc2[j][n] = zero_f32x4();
-    for (int ks = 0; ks < KP / 32; ++ks) {
-      const int kk = ks * 32 + 8 * (lane >> 4);
-      const int tap = kk / C, ci = kk % C;
-      const bool ok = tap < k;
-      half8 bw[NT];
+      for (int n = 0; n < NTL; ++n) acc2[j][n] = zero_f32x4();
 #pragma unroll
-      for (int n = 0; n < NT; ++n)
-        bw[n] = *reinterpret_cast<const half8*>(sW2 + (n * 16 + (lane & 15)) * LW + kk);
+    for (int ks = 0; ks < KS; ++ks) {
+      half8 bw[NTL];
 #pragma unroll
-      for (int j = 0; j < MT2; ++j) {
-        const int r = (w * MT2 + j) * 16 + (lane & 15);
-        const half8 av = ok ? *reinterpret_cast<const half8*>(sS + (r + tap) * LI + ci) : zero_half8();
+      for (int n = 0; n < NTL; ++n)
+        bw[n] = *reinterpret_cast<const half8*>(sW2 + b_off + n * 16 * LW + ks * 32);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc2[j][n] = mfma16(av, bw[n], acc2[j][n]);
+      for (int j = 0; j < MW2; ++j) {
+        const int m = min(w + 4 * j, MT2 - 1);  // see c1
+        const half8 av = *reinterpret_cast<const half8*>(sS + a2_off + (m * 16 + ks * G::TPK) * LI);
+#pragma unroll
+        for (int n = 0; n < NTL; ++n) acc2[j][n] = mfma16(av, bw[n], acc2[j][n]);
       }
     }
-    __syncthreads();  // sX/sS dead: sE takes their place
+    __syncthreads();  // sS dead: sE takes its place
 #pragma unroll
-    for (int j = 0; j < MT2; ++j)
+    for (int j = 0; j < MW2; ++j) {
+      const int m = w + 4 * j;
+      if (j >= MT2 / 4 && m >= MT2) continue;
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const int co = n * 16 + (lane & 15);
-        const float bias = a.b2[co];
+      for (int n = 0; n < NTL; ++n)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int r = (w * MT2 + j) * 16 + 4 * (lane >> 4) + rr;
-          sE[r * ES + co] = acc2[j][n][rr] + bias;
-        }
-      }
+        for (int rr = 0; rr < 4; ++rr)
+          sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + n * 16 + arow] = acc2[j][n][rr] + bias2[n];
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < G::NE; ++i) {
       const int idx = tid + i * 256;
       const int r = idx / CPR, cg = (idx % CPR) * 8;
-      const int t = t0 + r;
-      if (t >= T) continue;
-      const int64_t o = (int64_t)t * C + cg;
+      if (r >= BM || t0 + r >= T) continue;
       const half8 xv = *reinterpret_cast<const half8*>(sR + r * LI + cg);
       const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
       const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
@@ -227,45 +254,52 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int KP, int
       const half8 pv = *reinterpret_cast<const half8*>(&acc_in[i]);
       half8 hv;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float y = (v[j] + (float)xv[j]) * a.scale;
-        if (a.accumulate) y += (float)pv[j];
-        hv[j] = (_Float16)y;
-      }
-      *reinterpret_cast<half8*>(ob + o) = hv;
+      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+      *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
     }
   }
+#undef NARROW_PREFETCH
 }
 
-template <int C, int BM>
-static void resunit_cfg(const ResUnitArgs& a, hipStream_t s) {
-  using G = ResUnitGeo<C, BM>;
-  const int KP = resunit_kp(C, a.k);
-  const int p1 = a.d * (a.k - 1) / 2, p2 = (a.k - 1) / 2;
-  const int R1 = BM + 2 * p2, R0 = R1 + 2 * p1, R1p = (R1 + 15) / 16 * 16;
-  JANUS_CHECK(R0 <= G::R0MAX, "resunit: (k-1)*(d+1) exceeds the prefetch budget");
-  const int act = std::max((R0 + R1p) * G::LI, BM * G::ES * 2);  // halves
-  const int act_halves = (act + 7) / 8 * 8;
-  const size_t lds = ((size_t)act_halves + (size_t)BM * G::LI + 2 * (size_t)C * frag_pitch(KP)) * 2;
-  JANUS_CHECK(lds <= 160 * 1024, "resunit: LDS tile too large");
-  auto kern = resunit_kernel<C, BM>;
+template <int C, int K, int D, int BM>
+static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
+  using G = NarrowGeo<C, K, D, BM>;
+  static_assert(G::LDS <= 160 * 1024, "LDS");
+  auto kern = resunit_kernel<C, K, D, BM>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024));
+                                  (int)G::LDS));
     attr = true;
   }
   const int tiles_per_utt = (a.T + BM - 1) / BM;
   const int n_tiles = tiles_per_utt * a.B;
-  const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / lds)));
+  const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / G::LDS)));
   const int grid = std::min(n_tiles, 256 * per_cu);
-  kern<<<grid, 256, lds, s>>>(a, KP, tiles_per_utt, n_tiles, act_halves);
+  kern<<<grid, 256, G::LDS, s>>>(a, tiles_per_utt, n_tiles);
   JANUS_LAUNCH_CHECK();
+}
+
+template <int C, int K>
+static void narrow_d(const ResUnitArgs& a, hipStream_t s) {
+  constexpr int BM = 240;
+  if (a.d == 1) narrow_cfg<C, K, 1, BM>(a, s);
+  else if (a.d == 3) narrow_cfg<C, K, 3, BM>(a, s);
+  else if (a.d == 5) narrow_cfg<C, K, 5, BM>(a, s);
+  else throw Error("resunit: dilation must be 1, 3 or 5");
+}
+
+template <int C>
+static void narrow_k(const ResUnitArgs& a, hipStream_t s) {
+  if (a.k == 3) narrow_d<C, 3>(a, s);
+  else if (a.k == 7) narrow_d<C, 7>(a, s);
+  else if (a.k == 11) narrow_d<C, 11>(a, s);
+  else throw Error("resunit: k must be 3, 7 or 11 for C <= 32");
 }
 
 bool resunit_supported(int C, int k) {
   if (C >= 64) return resunit_wide_supported(C, k, 5);
-  return (C == 16 || C == 32) && k >= 1 && k <= 11 && (k & 1);
+  return (C == 16 || C == 32) && (k == 3 || k == 7 || k == 11);
 }
 
 void resunit_launch(const ResUnitArgs& a, hipStream_t s) {
@@ -276,18 +310,8 @@ void resunit_launch(const ResUnitArgs& a, hipStream_t s) {
     resunit_wide_launch(a, s);
     return;
   }
-  // tile rows per block (JANUS_RU_BM overrides, for tuning sweeps)
-  static const int bm = [] { const char* e = std::getenv("JANUS_RU_BM"); return e ? std::atoi(e) : 0; }();
-  // measured (B=16, 30 s, accumulate): C16 BM 256 beats 512 by 1.8x (3 blocks/CU vs 2);
-  // C32 k<=7 is best at BM 128, k 11 at BM 64 (1.84 vs 2.23 ms)
-  if (a.C == 16) {
-    if (bm == 512) resunit_cfg<16, 512>(a, s);
-    else resunit_cfg<16, 256>(a, s);
-  } else {
-    if (bm == 256) resunit_cfg<32, 256>(a, s);
-    else if (bm == 64 || (bm == 0 && a.k > 7)) resunit_cfg<32, 64>(a, s);
-    else resunit_cfg<32, 128>(a, s);
-  }
+  if (a.C == 16) narrow_k<16>(a, s);
+  else narrow_k<32>(a, s);
 }
 
 }  // namespace janus

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
   const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
   const int b = blockIdx.x / tiles_per_utt, t0 = (blockIdx.x % tiles_per_utt) * BM;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
   const int wm = wid % WM, wn = wid / WM;
   const _Float16* xb = a.x + (int64_t)b * T * C;
   _Float16* ob = a.out + (int64_t)b * T * C;
@@ -177,8 +177,10 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
       const _Float16* ap = src + (wm * 16 + arow + tap * dil) * LI + ci + kq;
 #pragma unroll
       for (int j = 0; j < MW; ++j) {
-        if (wm + j * WM >= MT) break;
-        const half8 av = *reinterpret_cast<const half8*>(ap + j * WM * 16 * LI);
+        // a wave past the last m-tile recomputes it (dropped in the epilogue): no branch
+        // around the MFMA (see resunit.hip)
+        const int jj = (j < MT / WM) ? j : (wm + j * WM < MT ? j : (MT - 1 - wm) / WM);
+        const half8 av = *reinterpret_cast<const half8*>(ap + jj * WM * 16 * LI);
 #pragma unroll
         for (int n = 0; n < NTW; ++n) acc[j][n] = mfma16(av, bw[n], acc[j][n]);
       }
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
 #pragma unroll
       for (int j = 0; j < MW1; ++j) {
         const int m = wm + j * WM;
-        if (m >= MT1) break;
+        if (j >= MT1 / WM && m >= MT1) break;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int r = m * 16 + 4 * (lane >> 4) + rr;
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
 #pragma unroll
     for (int j = 0; j < MW2; ++j) {
       const int m = wm + j * WM;
-      if (m >= MT2) break;
+      if (j >= MT2 / WM && m >= MT2) break;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + co] = acc2[j][n][rr] + bias;
     }

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
   float* sA = sS + 2 * 16 * kXKeys;            // [16] rescale factors
 
   const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int t0 = s * kps, t1 = min(Te, t0 + kps);
   const _Float16* eb = enc + (int64_t)b * Te * D;
 

@@ -33,7 +33,8 @@ def counters(d):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     tot, n = 0.0, set()
     for r in csv.DictReader(open(f)):
-        if "conv_kernel" in r["Kernel_Name"] or "resunit_kernel" in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if "conv_kernel" in k or "resunit_kernel" in k or "resunit_wide_kernel" in k:
             tot += float(r["Counter_Value"])
             n.add(r["Dispatch_Id"])
     return tot, len(n)
@@ -54,7 +55,7 @@ def algorithmic_bytes(B=64, F=2584, latent=512, ch=512, ups=(8, 8, 2, 2, 2), n_k
             for m in range(n_d):
                 last = m + 1 == n_d
                 acc = last and kj > 0
-                if c in (16, 32):                             # fused unit: x in, out (+ acc read)
+                if c in (16, 32, 64, 128, 256):               # fused unit: x in, out (+ acc read)
                     tot += 2 * B * T * c * (2 + (1 if acc else 0)); n += 1
                 else:                                         # c1: x -> S; c2: S, res x -> out
                     tot += 2 * B * T * c * 2; n += 1
@@ -68,7 +69,7 @@ def reduce(fdir, wdir, out):
     assert nf == nw and nf > 0, (nf, nw)
     fetch = 2.0 * fetch_kb * 1024  # gfx950: FETCH_SIZE = half the streamed bytes (KB units)
     write = write_kb * 1024
-    res = {"kernel": "conv_kernel + resunit_kernel (vocoder convs, all shapes of one 64 x 30 s "
+    res = {"kernel": "conv_kernel + resunit_kernel + resunit_wide_kernel (vocoder convs, all shapes of one 64 x 30 s "
                      "forward: the launch set the bench's roofline averages over)",
            "launches": nf, "fetch_bytes": fetch, "write_bytes": write,
            "bytes_per_launch": (fetch + write) / nf,
