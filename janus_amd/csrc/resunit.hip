@@ -64,13 +64,22 @@ struct NarrowGeo {
   static constexpr int NPF = (R0 * CPR + NT - 1) / NT;  // prefetch uint4 per thread
   static constexpr int ES = C + 4;                      // fp32 epilogue pitch
   static constexpr int NE = (BM * CPR + NT - 1) / NT;   // epilogue uint4 per thread
+  // epilogue passes: at C = 32 the fp32 tile goes out in two row halves so that the
+  // block fits in 80 KB of LDS (two blocks per CU)
+  static constexpr int NP = C == 32 ? 2 : 1;
+  static constexpr int RP = 64 * (MW2 / NP);            // rows per epilogue pass
+  // the residual x rows: kept from the staging in an LDS tile where LDS allows (C = 16),
+  // else re-read from global memory (L2-hot) into registers during the convs
+  static constexpr bool RES_LDS = C == 16;
   // LDS (halves): [sX | sS | sE alias] [sR] [sW1] [sW2]
-  static constexpr int ACT = std::max(std::max(R0 * LI, M1 * LI), BM * ES * 2);
+  static constexpr int ACT = std::max(std::max(R0 * LI, M1 * LI), RP * ES * 2);
   static constexpr int ACT_H = (ACT + 7) / 8 * 8;
-  static constexpr int LDS_H = ACT_H + BM * LI + 2 * C * LW;
+  static constexpr int RES_H = RES_LDS ? BM * LI : 0;
+  static constexpr int LDS_H = ACT_H + RES_H + 2 * C * LW;
   static constexpr size_t LDS = (size_t)LDS_H * 2;
   static_assert(KP == (K * C + 31) / 32 * 32, "matches resunit_kp");
   static_assert(BM % 16 == 0 && M1 >= BM + K - 1 && M1 >= BM + TP - 1, "c2 halo");
+  static_assert(MW2 % NP == 0 && NE % NP == 0 && NE * NT / CPR / NP == RP, "epilogue passes");
 };
 
 // Persistent: weights staged once; per tile the next tile's x rows are loaded into
@@ -85,9 +94,9 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   _Float16* sX = smem;                        // [R0][LI]  silu(x)
   _Float16* sS = smem;                        // [M1][LI]  silu(c1 + b1), over dead sX
-  float* sE = reinterpret_cast<float*>(smem); // [BM][ES]  c2 + b2, over dead sS
-  _Float16* sR = smem + G::ACT_H;             // [BM][LI]  raw x (the residual)
-  _Float16* sW1 = sR + BM * LI;               // [C][LW]
+  float* sE = reinterpret_cast<float*>(smem); // [RP][ES]  c2 + b2, over dead sS
+  _Float16* sR = smem + G::ACT_H;             // [BM][LI]  raw x (RES_LDS only)
+  _Float16* sW1 = sR + G::RES_H;              // [C][LW]
   _Float16* sW2 = sW1 + C * LW;               // [C][LW]
   const int T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
@@ -142,8 +151,10 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
-        const int rr = r - P2 - P1;
-        if (rr >= 0 && rr < BM) *reinterpret_cast<half8*>(sR + rr * LI + cc * 8) = v;
+        if constexpr (G::RES_LDS) {
+          const int rr = r - P2 - P1;
+          if (rr >= 0 && rr < BM) *reinterpret_cast<half8*>(sR + rr * LI + cc * 8) = v;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
@@ -152,12 +163,19 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
     __syncthreads();
     NARROW_PREFETCH(tile + gridDim.x);  // in flight during this tile's compute
     _Float16* ob = a.out + (int64_t)b * T * C;
-    uint4 acc_in[G::NE];
+    // the residual x rows (re-read: L2-hot since this tile's prefetch) and the
+    // accumulator rows, in flight during the convs
+    const _Float16* xb = a.x + (int64_t)b * T * C;
+    uint4 xres[G::NE], acc_in[G::NE];
 #pragma unroll
     for (int i = 0; i < G::NE; ++i) {
       const int idx = tid + i * 256;
       const int r = idx / CPR, cg = (idx % CPR) * 8;
-      acc_in[i] = (a.accumulate && r < BM && t0 + r < T)
+      const bool ok = r < BM && t0 + r < T;
+      if constexpr (!G::RES_LDS)
+        xres[i] = ok ? *reinterpret_cast<const uint4*>(xb + (int64_t)(t0 + r) * C + cg)
+                     : make_uint4(0, 0, 0, 0);
+      acc_in[i] = (a.accumulate && ok)
                       ? *reinterpret_cast<const uint4*>(ob + (int64_t)(t0 + r) * C + cg)
                       : make_uint4(0, 0, 0, 0);
     }
@@ -230,32 +248,39 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
         for (int n = 0; n < NTL; ++n) acc2[j][n] = mfma16(av, bw[n], acc2[j][n]);
       }
     }
-    __syncthreads();  // sS dead: sE takes its place
+    // ---- epilogue in NP row passes: c2 + b2 -> fp32 LDS (over dead sS), then 16-byte
+    // row chunks out = (accumulate ? out : 0) + scale * (conv + x)
 #pragma unroll
-    for (int j = 0; j < MW2; ++j) {
-      const int m = w + 4 * j;
-      if (j >= MT2 / 4 && m >= MT2) continue;
+    for (int p = 0; p < G::NP; ++p) {
+      __syncthreads();  // sS reads (p = 0) / the previous pass's sE reads are done
 #pragma unroll
-      for (int n = 0; n < NTL; ++n)
+      for (int j = p * (MW2 / G::NP); j < (p + 1) * (MW2 / G::NP); ++j) {
+        const int m = w + 4 * j;
+        if (j >= MT2 / 4 && m >= MT2) continue;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + n * 16 + arow] = acc2[j][n][rr] + bias2[n];
-    }
-    __syncthreads();
+        for (int n = 0; n < NTL; ++n)
 #pragma unroll
-    for (int i = 0; i < G::NE; ++i) {
-      const int idx = tid + i * 256;
-      const int r = idx / CPR, cg = (idx % CPR) * 8;
-      if (r >= BM || t0 + r >= T) continue;
-      const half8 xv = *reinterpret_cast<const half8*>(sR + r * LI + cg);
-      const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
-      const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
-      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const half8 pv = *reinterpret_cast<const half8*>(&acc_in[i]);
-      half8 hv;
+          for (int rr = 0; rr < 4; ++rr)
+            sE[(m * 16 - p * G::RP + 4 * (lane >> 4) + rr) * ES + n * 16 + arow] = acc2[j][n][rr] + bias2[n];
+      }
+      __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
-      *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+      for (int i = p * (G::NE / G::NP); i < (p + 1) * (G::NE / G::NP); ++i) {
+        const int idx = tid + i * 256;
+        const int r = idx / CPR, cg = (idx % CPR) * 8;
+        if (r >= BM || t0 + r >= T) continue;
+        const int rl = r - p * G::RP;
+        const float4 v0 = *reinterpret_cast<const float4*>(sE + rl * ES + cg);
+        const float4 v1 = *reinterpret_cast<const float4*>(sE + rl * ES + cg + 4);
+        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const half8 xv = G::RES_LDS ? *reinterpret_cast<const half8*>(sR + r * LI + cg)
+                                    : *reinterpret_cast<const half8*>(&xres[i]);
+        const half8 pv = *reinterpret_cast<const half8*>(&acc_in[i]);
+        half8 hv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+        *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+      }
     }
   }
 #undef NARROW_PREFETCH
