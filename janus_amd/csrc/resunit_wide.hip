@@ -12,16 +12,19 @@
 //   2. c1 over MT1*16 rows (>= BM + k - 1: c2's halo) -> silu(. + b1) written as fp16
 //      into LDS over the dead sX tile (zero outside [0, T): c2's zero padding);
 //   3. c2 over BM rows from that LDS tile; the residual x and the ParallelBlock
-//      accumulator are loaded into registers at c2's start (in flight during its MFMAs);
+//      accumulator rows are loaded into registers at c2's start;
 //   4. epilogue through an fp32 LDS tile, 16-byte coalesced loads/stores.
 // HBM per unit and time row: read x (+ residual re-read, L2-hot), write out (+ the
 // accumulator read on the last unit of a ResBlock1) = 2-3 x C x 2 B.
 //
 // Both convs are implicit GEMMs on v_mfma_f32_16x16x32_f16 with K = k*C ordered
-// tap-major: the 32-wide K step of a lane group lies inside one tap, so the A fragment is
-// the LDS tile row (m*16 + lane%16 + tap*dil) at channel offset ci. Weights stream from
-// L2 in [KB x C] k-blocks (packed [kb][Cout][KB]), double-buffered through LDS, one
-// barrier per k-block.
+// tap-major: each 32-wide k-step lies inside one tap, so the A fragment is the LDS tile
+// row (m*16 + lane%16 + tap*dil) at channel offset ci. B (weights, packed
+// [k-step][Cout][32] so one n-tile fragment is 1 KB contiguous) streams from L2
+// straight into registers through an NPB-deep per-wave ring: the K loops carry no LDS
+// weight stores and no barriers. Every wave of a block owns distinct output columns
+// (WN) or distinct m-tiles (WM); weights are re-read per tile from L2 (~C*k*C*4 B per
+// tile, far below the L2's rate at the MFMA pace).
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -30,30 +33,272 @@
 
 namespace janus {
 
-// packed[(kb*C + co)*KB + j] = w[co][ci][tap] with kk = kb*KB + j, tap = kk / C, ci = kk % C
+// packed[(ks*C + co)*32 + j] = w[co][ci][tap] with kk = ks*32 + j, tap = kk / C, ci = kk % C
 __global__ void resunit_wide_pack_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
-                                         int C, int k, int KB) {
+                                         int C, int k) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)k * C * C;
   if (idx >= total) return;
-  const int j = (int)(idx % KB);
-  const int co = (int)((idx / KB) % C);
-  const int kb = (int)(idx / ((int64_t)KB * C));
-  const int kk = kb * KB + j;
+  const int j = (int)(idx % 32);
+  const int co = (int)((idx / 32) % C);
+  const int ks = (int)(idx / (32 * (int64_t)C));
+  const int kk = ks * 32 + j;
   const int tap = kk / C, ci = kk % C;
   out[idx] = (_Float16)w[((int64_t)co * C + ci) * k + tap];
 }
 
 template <int C> struct WideCfg;
 // BM output rows per block, WM x WN waves (wave tile: every WM-th m-tile x C/WN columns),
-// KB = K per weight k-block. LDS <= 80 KB for C <= 128 (two blocks per CU).
-template <> struct WideCfg<64> { static constexpr int BM = 240, WM = 4, WN = 1, KB = 32; };
-template <> struct WideCfg<128> { static constexpr int BM = 128, WM = 1, WN = 4, KB = 32; };
-template <> struct WideCfg<256> { static constexpr int BM = 112, WM = 2, WN = 4, KB = 32; };
+// NPB = weight k-steps in flight per wave (divides the k-step count k*C/32).
+// EPF: residual / accumulator rows loaded before c2 (in flight during it) where the
+// registers allow, else after it.
+template <> struct WideCfg<128> { static constexpr int BM = 128, WM = 1, WN = 4, NPB = 2; static constexpr bool EPF = false; };
 
 template <int C>
 struct WideGeo {
   using Cfg = WideCfg<C>;
+  static constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN, NPB = Cfg::NPB;
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int LI = frag_pitch(C);        // activation row pitch (halves)
+  static constexpr int CPR = C / 8;               // 16-byte chunks per activation row
+  static constexpr int MT1 = (BM + 10 + 15) / 16; // c1 m-tiles (k <= 11)
+  static constexpr int MT2 = BM / 16;             // c2 m-tiles
+  static constexpr int MW1 = (MT1 + WM - 1) / WM; // c1 m-tiles per wave
+  static constexpr int MW2 = (MT2 + WM - 1) / WM; // c2 m-tiles per wave
+  static constexpr int NTW = C / 16 / WN;         // n-tiles per wave
+  static constexpr int R0MAX = MT1 * 16 + 50;     // staged x rows, (k-1)*d <= 50
+  static constexpr int NLD = (R0MAX * CPR + NT - 1) / NT;
+  static constexpr int ES = C + 4;                // fp32 epilogue row pitch
+  static constexpr int NE = (BM * CPR + NT - 1) / NT;
+  static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
+  static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)BM * ES * 4);
+  static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
+};
+
+// A wave past the last m-tile of a conv recomputes its own last tile (result dropped in
+// the epilogue): no branch around an MFMA (branches there made the compiler shuttle
+// accumulators between AGPRs; see resunit.hip).
+template <int MT, int WM>
+__device__ __forceinline__ int own_tile(int j, int wm) {
+  if (j < MT / WM) return j;
+  return wm + j * WM < MT ? j : (MT - 1 - wm) / WM;
+}
+
+template <int C, int MW, int MT, class G>
+__device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float16* __restrict__ wp,
+                                          const _Float16* src, int dil, int nks, int wm,
+                                          int a_lane, int b_lane) {
+  constexpr int NTW = G::NTW, NPB = G::NPB, LI = G::LI, WM = G::WM;
+#pragma unroll
+  for (int j = 0; j < MW; ++j)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[j][n] = zero_f32x4();
+  // B ring: slot s holds k-step (ks0 + s); loads are unconditional (clamped index) so the
+  // compiler's vmcnt for a slot never has to cover younger slots' loads
+  half8 bq[NPB][NTW];
+  const _Float16* wl = wp + b_lane;
+#pragma unroll
+  for (int s = 0; s < NPB; ++s)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n)
+      bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)s * C + n * 16) * 32);
+  // A fragments double-buffered across k-steps: step ks+1's LDS reads are issued before
+  // step ks's MFMAs (NPB even keeps the buffer index static)
+  static_assert(NPB % 2 == 0, "even ring depth");
+  half8 av[2][MW];
+  auto a_addr = [&](int ks) __attribute__((always_inline)) {
+    const int kk = ks * 32;  // wave-uniform: one tap
+    return src + a_lane + (kk / C) * dil * LI + kk % C;
+  };
+  {
+    const _Float16* ap = a_addr(0);
+#pragma unroll
+    for (int j = 0; j < MW; ++j)
+      av[0][j] = *reinterpret_cast<const half8*>(ap + own_tile<MT, WM>(j, wm) * WM * 16 * LI);
+  }
+  for (int ks0 = 0; ks0 < nks; ks0 += NPB) {
+#pragma unroll
+    for (int s = 0; s < NPB; ++s) {
+      const int ks = ks0 + s;
+      const _Float16* ap = a_addr(min(ks + 1, nks - 1));
+#pragma unroll
+      for (int j = 0; j < MW; ++j)
+        av[(s + 1) & 1][j] = *reinterpret_cast<const half8*>(ap + own_tile<MT, WM>(j, wm) * WM * 16 * LI);
+#pragma unroll
+      for (int j = 0; j < MW; ++j)
+#pragma unroll
+        for (int n = 0; n < NTW; ++n) acc[j][n] = mfma16(av[s & 1][j], bq[s][n], acc[j][n]);
+      const int nx = min(ks + NPB, nks - 1);
+#pragma unroll
+      for (int n = 0; n < NTW; ++n)
+        bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)nx * C + n * 16) * 32);
+    }
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnitArgs a,
+                                                                         int tiles_per_utt) {
+  using G = WideGeo<C>;
+  constexpr int BM = G::BM, WM = G::WM, NT = G::NT, LI = G::LI;
+  constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
+  constexpr int NTW = G::NTW, ES = G::ES;
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* sX = smem;                         // [R0][LI] silu(x)
+  _Float16* sS = smem;                         // [MT1*16][LI] silu(c1 + b1) (over sX)
+  float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS)
+
+  const int k = a.k, d = a.d, T = a.T;
+  const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
+  const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
+  const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
+  const int b = blockIdx.x / tiles_per_utt, t0 = (blockIdx.x % tiles_per_utt) * BM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
+  const int wm = wid % WM, wn = wid / WM;
+  const _Float16* xb = a.x + (int64_t)b * T * C;
+  _Float16* ob = a.out + (int64_t)b * T * C;
+  const int nks = k * C / 32;
+
+  // ---- 1. stage silu(x): all loads in flight, then convert + store
+  {
+    const int xbase = t0 - p2 - p1;
+    uint4 pf[G::NLD];
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cc = idx % CPR;
+      const int t = xbase + r;
+      pf[i] = (r < R0 && t >= 0 && t < T)
+                  ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * C + cc * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cc = idx % CPR;
+      if (r < R0) {
+        half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int arow = lane & 15, kq = 8 * (lane >> 4);
+  const int a_lane = (wm * 16 + arow) * LI + kq;                 // A: row, k chunk
+  const int b_lane = ((wn * NTW) * 16 + arow) * 32 + kq;         // B: column, k chunk
+
+  // ---- 2. c1 over MT1*16 rows (row r <-> time t0 - p2 + r): A = sX[r + tap*d]
+  {
+    f32x4 acc[MW1][NTW];
+    wide_conv<C, MW1, MT1, G>(acc, a.w1, sX, d, nks, wm, a_lane, b_lane);
+    __syncthreads();  // every wave is done reading sX: write silu(c1 + b1) over it
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) {
+      const int co = (wn * NTW + n) * 16 + arow;
+      const float bias = a.b1[co];
+#pragma unroll
+      for (int j = 0; j < MW1; ++j) {
+        const int m = wm + j * WM;
+        if (j >= MT1 / WM && m >= MT1) break;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = m * 16 + 4 * (lane >> 4) + rr;
+          const int t = t0 - p2 + r;
+          const float v = (r < R1 && t >= 0 && t < T) ? silu(acc[j][n][rr] + bias) : 0.0f;
+          sS[r * LI + co] = (_Float16)v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // residual x and accumulator rows of this tile (before c2 when Cfg::EPF)
+  uint4 rq[G::NE], pq[G::NE];
+  auto epi_load = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < G::NE; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cg = (idx % CPR) * 8;
+      const bool ok = r < BM && t0 + r < T;
+      const int64_t o = (int64_t)(t0 + r) * C + cg;
+      rq[i] = ok ? *reinterpret_cast<const uint4*>(xb + o) : make_uint4(0, 0, 0, 0);
+      pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(ob + o) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if constexpr (G::Cfg::EPF) epi_load();
+
+  // ---- 3. c2 over BM rows (row r <-> time t0 + r): A = sS[r + tap]
+  f32x4 acc2[MW2][NTW];
+  wide_conv<C, MW2, MT2, G>(acc2, a.w2, sS, 1, nks, wm, a_lane, b_lane);
+  if constexpr (!G::Cfg::EPF) epi_load();
+  __syncthreads();  // sS dead: the fp32 epilogue tile takes its place
+
+  // ---- 4. epilogue: c2 + b2 -> fp32 LDS tile, then 16-byte row chunks
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    const int co = (wn * NTW + n) * 16 + arow;
+    const float bias = a.b2[co];
+#pragma unroll
+    for (int j = 0; j < MW2; ++j) {
+      const int m = wm + j * WM;
+      if (j >= MT2 / WM && m >= MT2) break;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + co] = acc2[j][n][rr] + bias;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < G::NE; ++i) {
+    const int idx = tid + i * NT;
+    const int r = idx / CPR, cg = (idx % CPR) * 8;
+    if (r >= BM || t0 + r >= T) continue;
+    const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
+    const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const half8 xv = *reinterpret_cast<const half8*>(&rq[i]);
+    const half8 pv = *reinterpret_cast<const half8*>(&pq[i]);
+    half8 hv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+    *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+  }
+}
+
+template <int C>
+static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
+  using G = WideGeo<C>;
+  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
+  JANUS_CHECK((a.k * C / 32) % G::NPB == 0, "resunit (wide): k-step count vs ring depth");
+  static_assert(G::LDS <= 160 * 1024, "LDS");
+  auto kern = resunit_wide_kernel<C>;
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)G::LDS));
+    attr = true;
+  }
+  const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
+  JANUS_LAUNCH_CHECK();
+}
+
+template <int C> struct LdsCfg;
+// ---------------------------------------------------------------------------------
+// Variant with the weights staged through LDS (one copy per block, double-buffered,
+// each k-block's loads issued two k-blocks ahead into registers): measured faster where
+// all waves share the weight columns (C = 64: 4 waves x 64 columns) or where the per-wave
+// column slice is wide (C = 256), i.e. where direct per-wave B loads would exceed the
+// L2 -> CU rate. Same packed layout ([k-step][Cout][32]).
+// BM output rows per block, WM x WN waves, KB = K per weight k-block.
+template <> struct LdsCfg<64> { static constexpr int BM = 240, WM = 4, WN = 1, KB = 32; };
+template <> struct LdsCfg<256> { static constexpr int BM = 112, WM = 2, WN = 4, KB = 32; };
+
+template <int C>
+struct LdsGeo {
+  using Cfg = LdsCfg<C>;
   static constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN, KB = Cfg::KB;
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int LI = frag_pitch(C);        // activation row pitch (halves)
@@ -83,9 +328,9 @@ struct WideGeo {
 // EPF: load the residual / accumulator rows at c2's start (in flight during its MFMAs)
 // instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
 template <int C, bool EPF>
-__global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnitArgs a,
+__global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt) {
-  using G = WideGeo<C>;
+  using G = LdsGeo<C>;
   constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
   constexpr int NTW = G::NTW, ES = G::ES;
@@ -298,11 +543,11 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
 #undef WIDE_KLOOP
 
 template <int C, bool EPF>
-static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
-  using G = WideGeo<C>;
+static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
+  using G = LdsGeo<C>;
   JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_wide_kernel<C, EPF>;
+  auto kern = resunit_wide_lds_kernel<C, EPF>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -321,17 +566,16 @@ bool resunit_wide_supported(int C, int k, int d) {
 }
 
 void resunit_wide_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
-  const int KB = C == 64 ? WideCfg<64>::KB : C == 128 ? WideCfg<128>::KB : WideCfg<256>::KB;
   const int64_t total = (int64_t)k * C * C;
-  resunit_wide_pack_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(w, out, C, k, KB);
+  resunit_wide_pack_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(w, out, C, k);
   JANUS_LAUNCH_CHECK();
 }
 
 void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
   static const int epf = [] { const char* e = std::getenv("JANUS_WIDE_EPF"); return e ? std::atoi(e) : 1; }();
-  if (a.C == 64) epf ? wide_cfg<64, true>(a, s) : wide_cfg<64, false>(a, s);
-  else if (a.C == 128) epf ? wide_cfg<128, true>(a, s) : wide_cfg<128, false>(a, s);
-  else if (a.C == 256) epf ? wide_cfg<256, true>(a, s) : wide_cfg<256, false>(a, s);
+  if (a.C == 64) epf ? lds_cfg<64, true>(a, s) : lds_cfg<64, false>(a, s);
+  else if (a.C == 128) wide_cfg<128>(a, s);
+  else if (a.C == 256) epf ? lds_cfg<256, true>(a, s) : lds_cfg<256, false>(a, s);
   else throw Error("resunit (wide): C must be 64, 128 or 256");
 }
 
