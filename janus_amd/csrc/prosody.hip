@@ -26,8 +26,9 @@ namespace janus {
 
 constexpr int kYinBuf = 4096;          // aubio pitch buffer (prosody.py:32)
 constexpr int kYinLen = kYinBuf / 2;   // yin fvec length
-constexpr int kYinThreads = 256;       // 4 waves; each lane owns 4 consecutive taus
-constexpr int kTauChunk = kYinThreads * 4;  // 1024 taus per pass
+constexpr int kYinThreads = 256;       // 4 waves; each lane owns 2 consecutive taus
+constexpr int kTauChunk = kYinThreads * 2;  // 512 taus per pass: voiced hops (F0 >= 95 Hz at
+                                            // 48 kHz: period <= 505) exit after one pass
 
 __device__ __forceinline__ int find_utt(const int64_t* offs, int B, int64_t g) {
   // largest b with offs[b] <= g (offs is non-decreasing, offs[0]=0, offs[B]=total)
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     int64_t total_hops) {
   __shared__ __attribute__((aligned(16))) float w[kYinBuf];
   __shared__ __attribute__((aligned(16))) float dd[kYinLen];   // d(tau), then yin(tau)
-  __shared__ float cum[kYinLen];                               // running sum (tmp2)
+  __shared__ float cum[kTauChunk];                             // running sum (tmp2) of a chunk
   __shared__ int s_found;
   __shared__ float s_level;
   __shared__ unsigned long long s_best;  // argmin key
@@ -73,6 +74,25 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     if (tid == 0) s_found = 0x7fffffff;
     __syncthreads();
 
+    // Silent hop: aubio_pitch_do forces f0 = 0 when the new hop's level is under the
+    // silence threshold, whatever YIN found, so YIN is skipped. The decision uses a
+    // parallel (reordered) level sum with a 1 dB margin, far outside float rounding: the
+    // sequential aubio level below then agrees (digital silence gives exactly 0 = -inf dB).
+    {
+      float e = 0.0f;
+      for (int j = kYinBuf - hop + tid; j < kYinBuf; j += kYinThreads) e += w[j] * w[j];
+      for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off);
+      if ((tid & 63) == 0) cum[tid >> 6] = e;
+      __syncthreads();
+      const float pe = (cum[0] + cum[1] + cum[2] + cum[3]) / (float)hop;
+      const bool silent = 10.0f * log10f(pe) < silence_db - 1.0f;
+      __syncthreads();  // cum[0..3] read by all before the tau passes reuse it
+      if (silent) {
+        if (tid == 0) f0_out[g] = 0.0f;
+        continue;
+      }
+    }
+
     // aubio_level_lin on the new hop (sequential float sum, as aubio).
     if (tid == kYinThreads - 1) {
       float e = 0.0f;
@@ -83,48 +103,43 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     float running = 0.0f;  // tmp2, carried across chunks (only lane 0 uses it)
     int found = 0x7fffffff;
     for (int chunk = 0; chunk < kYinLen / kTauChunk; ++chunk) {
-      const int tau0 = chunk * kTauChunk + 4 * tid;
-      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-#pragma unroll 2
+      const int tau0 = chunk * kTauChunk + 2 * tid;
+      float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 4
       for (int j = 0; j < kYinLen; j += 4) {
         const float4 a = *reinterpret_cast<const float4*>(&w[j]);
-        const float4 p = *reinterpret_cast<const float4*>(&w[j + tau0]);
-        const float4 q = *reinterpret_cast<const float4*>(&w[j + tau0 + 4]);
+        const float2 p0 = *reinterpret_cast<const float2*>(&w[j + tau0]);
+        const float2 p1 = *reinterpret_cast<const float2*>(&w[j + tau0 + 2]);
+        const float p2 = w[j + tau0 + 4];
         const float av[4] = {a.x, a.y, a.z, a.w};
-        const float bv[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+        const float bv[5] = {p0.x, p0.y, p1.x, p1.y, p2};
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           float t0 = __fsub_rn(av[jj], bv[jj + 0]);
           float t1 = __fsub_rn(av[jj], bv[jj + 1]);
-          float t2 = __fsub_rn(av[jj], bv[jj + 2]);
-          float t3 = __fsub_rn(av[jj], bv[jj + 3]);
           acc0 = __fadd_rn(acc0, __fmul_rn(t0, t0));
           acc1 = __fadd_rn(acc1, __fmul_rn(t1, t1));
-          acc2 = __fadd_rn(acc2, __fmul_rn(t2, t2));
-          acc3 = __fadd_rn(acc3, __fmul_rn(t3, t3));
         }
       }
       dd[tau0 + 0] = acc0;
       dd[tau0 + 1] = acc1;
-      dd[tau0 + 2] = acc2;
-      dd[tau0 + 3] = acc3;
       __syncthreads();
       // tmp2 += yin[tau] in tau order (pitchyin.c), one lane.
       if (tid == 0) {
         const int t_begin = chunk == 0 ? 1 : chunk * kTauChunk;
         for (int t = t_begin; t < (chunk + 1) * kTauChunk; ++t) {
           running = __fadd_rn(running, dd[t]);
-          cum[t] = running;
+          cum[t - chunk * kTauChunk] = running;
         }
       }
       __syncthreads();
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
+      for (int m = 0; m < 2; ++m) {
         const int t = tau0 + m;
         float y;
         if (t == 0) y = 1.0f;
         else {
-          const float s = cum[t];
+          const float s = cum[t - chunk * kTauChunk];
           y = (s != 0.0f) ? __fmul_rn(dd[t], __fdiv_rn((float)t, s)) : 1.0f;
         }
         dd[t] = y;
@@ -134,7 +149,7 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
       // yin[p] < tol && yin[p] < yin[p+1]. Periods whose p+1 lies in the next chunk wait.
       const int p_hi = min((chunk + 1) * kTauChunk - 2, kYinLen - 4);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
+      for (int m = 0; m < 2; ++m) {
         const int p = tau0 + m - (chunk == 0 ? 0 : 1);  // chunk>0 also re-checks its first-1
         if (p >= 2 && p <= p_hi && p >= chunk * kTauChunk - 1) {
           const float yp = dd[p];
