@@ -36,8 +36,12 @@ void cast_f16_f32_launch(const _Float16* in, float* out, int64_t n, hipStream_t 
 void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t s);
 // x[b] = tok_emb[token] + pos_emb[pos]; part (nullable): LayerNorm pieces of x
 // (SkinnyLnArgs), d % 16 == 0
+// x[b] = tok_emb[token] + pos_emb[pos]; optionally the first layer's LayerNorm of the
+// row into ln_out [B][d] fp16 (d <= 512, eps 1e-5).
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
-                  int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s);
+                  int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s,
+                  const float* ln_g = nullptr, const float* ln_b = nullptr,
+                  _Float16* ln_out = nullptr);
 void kv_store_launch(const _Float16* qkv, int d, int pos, int n_ctx, _Float16* kc, _Float16* vc,
                      int B, hipStream_t s);
 void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen, int32_t* done,

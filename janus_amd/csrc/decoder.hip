@@ -59,12 +59,17 @@ __global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__
                                                     const int32_t* __restrict__ tokens,
                                                     int ld_tokens, int pos, int d,
                                                     float* __restrict__ x,
-                                                    float2* __restrict__ part) {
+                                                    float2* __restrict__ part,
+                                                    const float* __restrict__ ln_g,
+                                                    const float* __restrict__ ln_b,
+                                                    _Float16* __restrict__ ln_out) {
+  __shared__ float red[2][4];
   const int b = blockIdx.x;
   const int tok = tokens[(int64_t)b * ld_tokens + pos];
+  float v0 = 0.f, v1 = 0.f;
   for (int base = 0; base < d; base += 512) {
     const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece
-    float v0 = 0.f, v1 = 0.f;
+    v0 = 0.f; v1 = 0.f;
     if (col < d) {
       v0 = (float)tok_emb[(int64_t)tok * d + col] + pos_emb[(int64_t)pos * d + col];
       v1 = (float)tok_emb[(int64_t)tok * d + col + 1] + pos_emb[(int64_t)pos * d + col + 1];
@@ -75,12 +80,33 @@ __global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__
       if (col < d && (threadIdx.x & 7) == 0) part[(int64_t)b * (d / 16) + col / 16] = pc;
     }
   }
+  if (ln_out) {  // the first layer's LayerNorm of this row (d <= 512: one pass above)
+    const int col = 2 * threadIdx.x, wv = threadIdx.x >> 6;
+    const bool ok = col < d;
+    float s = v0 + v1;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[0][wv] = s;
+    __syncthreads();
+    const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / d;
+    float q = ok ? (v0 - mean) * (v0 - mean) + (v1 - mean) * (v1 - mean) : 0.f;
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    if ((threadIdx.x & 63) == 0) red[1][wv] = q;
+    __syncthreads();
+    const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / d + 1e-5f);
+    if (ok) {
+      ln_out[(int64_t)b * d + col] = (_Float16)((v0 - mean) * rstd * ln_g[col] + ln_b[col]);
+      ln_out[(int64_t)b * d + col + 1] = (_Float16)((v1 - mean) * rstd * ln_g[col + 1] + ln_b[col + 1]);
+    }
+  }
 }
 
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
-                  int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s) {
+                  int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s,
+                  const float* ln_g, const float* ln_b, _Float16* ln_out) {
   JANUS_CHECK(d % 16 == 0, "embed: d % 16 != 0");
-  embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tokens, ld_tokens, pos, d, x, part);
+  JANUS_CHECK(!ln_out || d <= 512, "embed: fused LayerNorm needs d <= 512");
+  embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tokens, ld_tokens, pos, d, x, part, ln_g, ln_b,
+                                 ln_out);
   JANUS_LAUNCH_CHECK();
 }
 

@@ -160,6 +160,7 @@ struct SkinnyArgs {
   _Float16* kc; _Float16* vc; int pos, n_ctx, qkv_d;
   float2* ln_part;
   int a_group_cols;
+  const float* ln_g; const float* ln_b; float ln_eps; _Float16* ln_out; int* ln_cnt;
 };
 
 constexpr int kSkWaves = 16;
@@ -312,6 +313,23 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   for (int i = 0; i < 8; ++i) v += red[i][erow][ec];
   // thread -> (row tid>>4, col col0 + (tid&15)): 16 aligned lanes hold one row's columns
   if constexpr (EPI == EPI_RESID_F32) {
+    if (p.ln_out) {  // block-uniform: fused LayerNorm of the new rows (GemmArgs::ln_out)
+      __shared__ int s_last;
+      if (eok) __hip_atomic_store(static_cast<float*>(p.C) + (int64_t)erow * p.ldc + ecol, v,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores drained
+      __syncthreads();                                   // ... and every other wave's
+      if (tid == 0)
+        s_last = __hip_atomic_fetch_add(p.ln_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (int)gridDim.x - 1;
+      __syncthreads();
+      if (!s_last) return;
+      for (int r = w; r < M; r += kSkWaves)
+        ln_row_wave<true>(static_cast<const float*>(p.C) + (int64_t)r * p.ldc, p.ln_g, p.ln_b,
+                          p.ln_out + (int64_t)r * N, N, p.ln_eps, lane);
+      if (tid == 0) __hip_atomic_store(p.ln_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     if (eok) static_cast<float*>(p.C)[(int64_t)erow * p.ldc + ecol] = v;
     if (p.ln_part) {  // block-uniform
       const float y = eok ? v : 0.0f;
@@ -370,6 +388,7 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
   p.ln_part = g.ln_part;
   p.a_group_cols = g.a_group_cols;
+  p.ln_g = g.ln_g; p.ln_b = g.ln_b; p.ln_eps = g.ln_eps; p.ln_out = g.ln_out; p.ln_cnt = g.ln_cnt;
   launch_skinny_t<false>(epi, p, s);
 }
 
@@ -394,6 +413,9 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
               "gemm: grouped A needs M <= 64 and 16-column groups");
   JANUS_CHECK(!p.ln_part || (epi == EPI_RESID_F32 && p.N % 16 == 0),
               "gemm: LayerNorm pieces come from a RESID epilogue with N % 16 == 0");
+  JANUS_CHECK(!p.ln_out || (epi == EPI_RESID_F32 && p.M <= 64 && p.N <= 1024 && p.ln_cnt &&
+                            p.ln_g && p.ln_b && p.ldc == p.N),
+              "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 1024, ldc == N");
   if (p.M <= 64) launch_skinny(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }

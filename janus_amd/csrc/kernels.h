@@ -22,6 +22,12 @@ struct GemmArgs {
   // grouped (block-diagonal) product, M <= 64 only: output columns [g*a_group_cols,
   // (g+1)*a_group_cols) read A columns [g*K, (g+1)*K) — per-head projections
   int a_group_cols = 0;
+  // EPI_RESID_F32 (M <= 64 only): the LayerNorm of the NEW residual rows, fused: the
+  // output rows are stored write-through (sc1), every block adds to ln_cnt once its
+  // stores have drained, and the last block to arrive normalises all M rows (sc1 loads)
+  // into ln_out [M][N] fp16 with (ln_g, ln_b, ln_eps) and re-arms ln_cnt (zero on entry).
+  const float* ln_g = nullptr; const float* ln_b = nullptr; float ln_eps = 1e-5f;
+  _Float16* ln_out = nullptr; int* ln_cnt = nullptr;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
 

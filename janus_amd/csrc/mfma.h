@@ -62,4 +62,41 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// LayerNorm of one fp32 row of d <= 1024 columns by one wave (two-pass mean / variance
+// in fp32, as layernorm_kernel), fp16 out. SC1: read the row with agent-scope relaxed
+// (sc1) loads — for rows other workgroups of the same launch have just stored sc1.
+template <bool SC1>
+__device__ __forceinline__ void ln_row_wave(const float* xr, const float* __restrict__ g,
+                                            const float* __restrict__ b, _Float16* out, int d,
+                                            float eps, int lane) {
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    float t = 0.f;
+    if (c < d) {
+      if constexpr (SC1) t = __hip_atomic_load(xr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else t = xr[c];
+    }
+    v[i] = t;
+    s += t;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    if (c < d) q += (v[i] - mean) * (v[i] - mean);
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q / d + eps);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    if (c < d) out[c] = (_Float16)((v[i] - mean) * rstd * g[c] + b[c]);
+  }
+}
+
 }  // namespace janus

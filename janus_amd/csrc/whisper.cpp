@@ -43,7 +43,7 @@ struct janus_whisper {
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp,
+      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt,
       d_xqk, d_xc, d_xpc, d_xpml;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t side = nullptr;  // graph capture needs a non-null stream
@@ -320,14 +320,27 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
     p.kc = kcp; p.vc = vcp; p.pos = pos; p.n_ctx = NC; p.qkv_d = d;
     return p;
   };
-  auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias) {
+  // JANUS_LN_FUSE (opt-in, B <= 64): LayerNorm handed off inside the producing kernel —
+  // the residual GEMM's last block normalises the new rows (GemmArgs::ln_out, sc1 stores
+  // + arrival counter), the embedding kernel normalises its row; no LayerNorm launches.
+  // Measured slower than the separate launches (616.8 vs 536.5 ms per bench step): the
+  // write-through stores and the serial tail cost more than the launch they save.
+  const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && std::getenv("JANUS_LN_FUSE") != nullptr;
+  w->d_lncnt.ensure(sizeof(int));
+  JANUS_HIP(hipMemsetAsync(w->d_lncnt.p, 0, sizeof(int), s));
+  const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
+  const float* fin_b = w->params.get("decoder.layer_norm.bias", d);
+  auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias, const float* ng,
+                   const float* nb) {
     GemmArgs g = gargs(A, K, W.as<_Float16>(), K, bias, x, d, B, d, K, x, d);
     if (fused_ln) g.ln_part = lnp;
+    if (ln_fuse) { g.ln_g = ng; g.ln_b = nb; g.ln_out = a; g.ln_cnt = w->d_lncnt.as<int>(); }
     gemm_launch(EPI_RESID_F32, g, s);
   };
   auto step = [&](int pos) {
     embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
-                 fused_ln ? lnp : nullptr, B, s);
+                 fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
+                 ln_fuse ? a : nullptr);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = w->d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
@@ -338,7 +351,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
-        layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
+        if (!ln_fuse) layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
         if (B <= 64) {
           GemmArgs g = gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
@@ -350,7 +363,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s);
-      resid(o, d, L.wo, L.bo);
+      resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
       if (xabs) {
         const int hd = H * d;
         _Float16* xqk = w->d_xqk.as<_Float16>();
@@ -359,7 +372,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
         } else {
-          layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d), s);
         }
         xattn_launch(xqk, enc, B, Te, d, H, xsplit, w->d_xpc.as<float>(), w->d_xpml.as<float>(), xc, s);
@@ -367,31 +380,32 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
         GemmArgs gv = gargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
         gv.a_group_cols = 64;
         gemm_launch(EPI_F16, gv, s);
-        resid(o, d, L.wo_c, L.bo_c);
+        resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
       } else {
         if (fused_ln) {
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
                                                 nullptr, nullptr, pos), s);
         } else {
-          layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
         }
         decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                       part_ml, s);
-        resid(o, d, L.wo_c, L.bo_c);
+        resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
       }
       if (fused_ln) {
         gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
-        layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+        if (!ln_fuse) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
         gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
       }
-      resid(f, 4 * d, L.w2, L.b2);
+      // next LayerNorm: the following layer's LN1, or the decoder's final LN
+      resid(f, 4 * d, L.w2, L.b2, l + 1 < nl ? w->dec[l + 1].ln1g : fin_g,
+            l + 1 < nl ? w->dec[l + 1].ln1b : fin_b);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
-    layernorm_launch(x, w->params.get("decoder.layer_norm.weight", d),
-                     w->params.get("decoder.layer_norm.bias", d), a, B, d, 1e-5f, s);
+    if (!ln_fuse) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, w->d_smask.as<uint8_t>(),
                           w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s);
     select_partials_launch(w->d_parts.as<LogitPart>(), nblk, R, w->d_rules.as<RowRules>(), tokens,
@@ -404,7 +418,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
       (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
-      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
+      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)w->d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
       (int64_t)w->d_xc.p, (int64_t)w->d_xpc.p, (int64_t)w->d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
