@@ -359,6 +359,45 @@ __global__ __launch_bounds__(512) void decode_combine_kernel(const float* __rest
   out[(int64_t)b * o_bs + i] = (_Float16)(o / l);
 }
 
+// nsplit <= 8 (self-attention up to 512 cached keys): each thread's split partials and
+// the (m, l) pairs are loaded up front (one memory latency instead of two dependent ones)
+constexpr int kCombRegs = 8;
+__global__ __launch_bounds__(512) void decode_combine_reg_kernel(const float* __restrict__ part_o,
+                                                                 const float* __restrict__ part_ml,
+                                                                 int nsplit, int H,
+                                                                 _Float16* __restrict__ out,
+                                                                 int64_t o_bs) {
+  const int b = blockIdx.x, i = threadIdx.x;
+  const int d = H * kHd;
+  if (i >= d) return;
+  const int h = i / kHd;
+  const float* pml = part_ml + (int64_t)b * nsplit * H * 2;
+  const float* po = part_o + (int64_t)b * nsplit * d + i;
+  float2 ml[kCombRegs];
+  float ov[kCombRegs];
+#pragma unroll
+  for (int s = 0; s < kCombRegs; ++s) {
+    if (s < nsplit) {
+      ml[s] = *reinterpret_cast<const float2*>(pml + ((int64_t)s * H + h) * 2);
+      ov[s] = po[(int64_t)s * d];
+    }
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kCombRegs; ++s)
+    if (s < nsplit) m = fmaxf(m, ml[s].x);
+  float l = 0.f, o = 0.f;
+#pragma unroll
+  for (int s = 0; s < kCombRegs; ++s) {
+    if (s < nsplit) {
+      const float f = exp2f(ml[s].x - m);
+      l += ml[s].y * f;
+      o += ov[s] * f;
+    }
+  }
+  out[(int64_t)b * o_bs + i] = (_Float16)(o / l);
+}
+
 int decode_split_count(int Tkv) {
   int n = (Tkv + kSplitKeys - 1) / kSplitKeys;
   return n < 1 ? 1 : n;
@@ -376,7 +415,10 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
   decode_split_kernel<<<dim3(nsplit, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, H, chunk,
                                                       scale * 1.4426950408889634f, part_o, part_ml);
   JANUS_LAUNCH_CHECK();
-  decode_combine_kernel<<<B, H * kHd, 0, s>>>(part_o, part_ml, nsplit, H, out, o_bs);
+  if (nsplit <= kCombRegs)
+    decode_combine_reg_kernel<<<B, H * kHd, 0, s>>>(part_o, part_ml, nsplit, H, out, o_bs);
+  else
+    decode_combine_kernel<<<B, H * kHd, 0, s>>>(part_o, part_ml, nsplit, H, out, o_bs);
   JANUS_LAUNCH_CHECK();
 }
 

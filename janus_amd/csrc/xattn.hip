@@ -263,6 +263,48 @@ __global__ __launch_bounds__(256) void xattn_combine_kernel(const float* __restr
   }
 }
 
+// Same merge, one block per (head, utterance) and every load issued up front: each
+// thread holds its float4 of all (<= 16) split partials plus the head's (m, l) pairs, so
+// the merge pays one memory latency, spread over B*H blocks instead of B.
+constexpr int kXCombMax = 16;
+__global__ __launch_bounds__(128) void xattn_combine_wide_kernel(const float* __restrict__ part_c,
+                                                                 const float* __restrict__ part_ml,
+                                                                 int nsplit, int H, int D,
+                                                                 _Float16* __restrict__ out) {
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int HD = H * D;
+  const float* pml = part_ml + (int64_t)b * nsplit * H * 2;
+  const float* pc = part_c + (int64_t)b * nsplit * HD + (int64_t)h * D;
+  float2 ml[kXCombMax];
+  float4 v[kXCombMax];
+  const int e = tid * 4;  // D <= 512: 128 threads x 4 dims
+#pragma unroll
+  for (int s = 0; s < kXCombMax; ++s) {
+    if (s < nsplit) {
+      ml[s] = *reinterpret_cast<const float2*>(pml + ((int64_t)s * H + h) * 2);
+      v[s] = e < D ? *reinterpret_cast<const float4*>(pc + (int64_t)s * HD + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kXCombMax; ++s)
+    if (s < nsplit) M = fmaxf(M, ml[s].x);
+  float L = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < kXCombMax; ++s) {
+    if (s < nsplit) {
+      const float wgt = exp2f(ml[s].x - M);  // empty split: m = -inf -> 0
+      L += wgt * ml[s].y;
+      acc.x += wgt * v[s].x; acc.y += wgt * v[s].y; acc.z += wgt * v[s].z; acc.w += wgt * v[s].w;
+    }
+  }
+  if (e >= D) return;
+  const float il = 1.0f / L;
+  half4 o = {(_Float16)(acc.x * il), (_Float16)(acc.y * il), (_Float16)(acc.z * il), (_Float16)(acc.w * il)};
+  *reinterpret_cast<half4*>(out + (int64_t)b * HD + (int64_t)h * D + e) = o;
+}
+
 int xattn_split_count(int Te, int requested) {
   int n = requested > 0 ? requested : 12;  // 768 blocks at batch 64: 3 per CU
   n = std::min(n, 63);
@@ -298,7 +340,10 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   if (D == 384) xattn_cfg<384>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
   else if (D == 512) xattn_cfg<512>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
   else xattn_cfg<768>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
-  xattn_combine_kernel<<<B, 256, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
+  if (nsplit <= kXCombMax && D <= 512)
+    xattn_combine_wide_kernel<<<dim3(H, B), 128, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
+  else
+    xattn_combine_kernel<<<B, 256, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
   JANUS_LAUNCH_CHECK();
 }
 
