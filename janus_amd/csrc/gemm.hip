@@ -9,6 +9,7 @@
 // double-buffered LDS (one barrier per 64-deep K step; next tile's global loads issued
 // before the current tile's MFMAs), rows padded to a 160-B pitch so the ds_read_b128
 // lane groups are conflict-free (frag_pitch), XCD-aware tile order (blocks sharing an A panel on one L2).
+#include <cstdlib>
 #include "mfma.h"
 #include "kernels.h"
 
@@ -165,13 +166,16 @@ struct SkinnyArgs {
 
 constexpr int kSkWaves = 16;
 
-template <int EPI, bool LNA>
+// MTB: 16-row m-tiles per block (4: all 64 rows; 1: rows split over gridDim.y, for narrow
+// outputs whose N / 16 column tiles alone would leave most CUs idle).
+template <int EPI, bool LNA, int MTB>
 __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   constexpr int G = LNA ? 1 : 2;  // k-steps in flight per wave (128-VGPR budget at 1024 threads)
-  __shared__ float red[8][64][17];
+  static_assert(!LNA || MTB == 4, "LayerNorm-on-load needs all rows per block");
+  __shared__ float red[8][16 * MTB][17];
   __shared__ float s_mean[64], s_rstd[64];
   const int M = p.M, N = p.N, K = p.K;
-  const int col0 = blockIdx.x * 16;
+  const int col0 = blockIdx.x * 16, r0 = blockIdx.y * 16 * MTB;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int kq = ((K + kSkWaves - 1) / kSkWaves + 31) / 32 * 32;
   const int kbeg = w * kq, kend = min(K, kbeg + kq);
@@ -184,13 +188,13 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   }
 
   // epilogue operands independent of the product, in flight from the start
-  const int erow = tid >> 4, ec = tid & 15, ecol = col0 + ec;
-  const bool eok = erow < M && ecol < N;
+  const int elr = tid >> 4, erow = r0 + elr, ec = tid & 15, ecol = col0 + ec;
+  const bool eok = elr < 16 * MTB && erow < M && ecol < N;
   float e_add = (p.bias && eok) ? p.bias[ecol] : 0.0f;
   if constexpr (EPI == EPI_RESID_F32) e_add += eok ? p.R[(int64_t)erow * p.ldr + ecol] : 0.0f;
 
   half8 bw[G];
-  half8 ah[LNA ? 1 : G][4];
+  half8 ah[LNA ? 1 : G][MTB];
   float4 ax[LNA ? G : 1][4][2];
   auto load = [&](int k0) {
 #pragma unroll
@@ -199,8 +203,8 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
       const bool ok = kk < kend;
       bw[g] = (ok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int r = m * 16 + lr;
+      for (int m = 0; m < MTB; ++m) {
+        const int r = r0 + m * 16 + lr;
         if constexpr (LNA) {
           const float* xr = p.x + (int64_t)r * p.ldx + kk;
           const bool rok = ok && r < M;
@@ -253,15 +257,15 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
     __syncthreads();
   }
 
-  f32x4 acc[4];
+  f32x4 acc[MTB];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+  for (int m = 0; m < MTB; ++m) acc[m] = zero_f32x4();
   for (int k0 = kbeg; k0 < kend; k0 += 32 * G) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int kk = k0 + 32 * g + kc8;
       if (k0 + 32 * g >= kend) break;  // wave-uniform
-      half8 af[4];
+      half8 af[MTB];
       if constexpr (LNA) {
         const bool ok = kk < kend;
         float ga[8], be[8];
@@ -285,10 +289,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < 4; ++m) af[m] = ah[g][m];
+        for (int m = 0; m < MTB; ++m) af[m] = ah[g][m];
       }
 #pragma unroll
-      for (int m = 0; m < 4; ++m) acc[m] = mfma16(af[m], bw[g], acc[m]);
+      for (int m = 0; m < MTB; ++m) acc[m] = mfma16(af[m], bw[g], acc[m]);
     }
     if (k0 + 32 * G < kend) load(k0 + 32 * G);
   }
@@ -296,21 +300,23 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   // 16 partials -> LDS: waves 0-7 store, waves 8-15 add, then one output per thread
   if (w < 8) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < MTB; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[w][m * 16 + 4 * (lane >> 4) + r][lane & 15] = acc[m][r];
   }
   __syncthreads();
   if (w >= 8) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < MTB; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[w - 8][m * 16 + 4 * (lane >> 4) + r][lane & 15] += acc[m][r];
   }
   __syncthreads();
   float v = e_add;
+  if (elr < 16 * MTB) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v += red[i][erow][ec];
+    for (int i = 0; i < 8; ++i) v += red[i][elr][ec];
+  }
   // thread -> (row tid>>4, col col0 + (tid&15)): 16 aligned lanes hold one row's columns
   if constexpr (EPI == EPI_RESID_F32) {
     if (p.ln_out) {  // block-uniform: fused LayerNorm of the new rows (GemmArgs::ln_out)
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
       __syncthreads();                                   // ... and every other wave's
       if (tid == 0)
         s_last = __hip_atomic_fetch_add(p.ln_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (int)gridDim.x - 1;
+                 (int)(gridDim.x * gridDim.y) - 1;
       __syncthreads();
       if (!s_last) return;
       for (int r = w; r < M; r += kSkWaves)
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
       float q = (y - mu) * (y - mu);
       q += __shfl_xor(q, 1); q += __shfl_xor(q, 2);
       q += __shfl_xor(q, 4); q += __shfl_xor(q, 8);
-      if (ec == 0 && erow < M) p.ln_part[(int64_t)erow * (N / 16) + col0 / 16] = make_float2(sm, q);
+      if (ec == 0 && eok) p.ln_part[(int64_t)erow * (N / 16) + col0 / 16] = make_float2(sm, q);
     }
     return;
   }
@@ -363,22 +369,36 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   }
 }
 
-template <bool LNA>
-static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
-  const int blocks = (p.N + 15) / 16;
+template <bool LNA, int MTB>
+static void launch_skinny_m(int epi, const SkinnyArgs& p, hipStream_t s) {
+  const dim3 grid((p.N + 15) / 16, (p.M + 16 * MTB - 1) / (16 * MTB));
   switch (epi) {
-    case EPI_F16: gemm_skinny_kernel<EPI_F16, LNA><<<blocks, 1024, 0, s>>>(p); break;
-    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16, LNA><<<blocks, 1024, 0, s>>>(p); break;
-    case EPI_QKV: gemm_skinny_kernel<EPI_QKV, LNA><<<blocks, 1024, 0, s>>>(p); break;
+    case EPI_F16: gemm_skinny_kernel<EPI_F16, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
+    case EPI_QKV: gemm_skinny_kernel<EPI_QKV, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
     case EPI_RESID_F32:
-      if constexpr (!LNA) { gemm_skinny_kernel<EPI_RESID_F32, false><<<blocks, 1024, 0, s>>>(p); break; }
+      if constexpr (!LNA) { gemm_skinny_kernel<EPI_RESID_F32, false, MTB><<<grid, 1024, 0, s>>>(p); break; }
       else throw Error("skinny LN gemm: bad epilogue");
     case EPI_F32:
-      if constexpr (!LNA) { gemm_skinny_kernel<EPI_F32, false><<<blocks, 1024, 0, s>>>(p); break; }
+      if constexpr (!LNA) { gemm_skinny_kernel<EPI_F32, false, MTB><<<grid, 1024, 0, s>>>(p); break; }
       else throw Error("skinny LN gemm: bad epilogue");
     default: throw Error("bad gemm epilogue");
   }
   JANUS_LAUNCH_CHECK();
+}
+
+template <bool LNA>
+static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
+  // narrow outputs (N <= JANUS_SKINNY_MSPLIT_N, default 2048: <= 128 column tiles) split the
+  // rows over 16-row blocks as well, so 4x as many CUs share the latency-bound product
+  static const int msplit_n = [] {
+    const char* e = std::getenv("JANUS_SKINNY_MSPLIT_N");
+    return e ? std::atoi(e) : 2048;
+  }();
+  if constexpr (!LNA) {
+    if (p.N <= msplit_n && p.ln_part == nullptr) { launch_skinny_m<false, 1>(epi, p, s); return; }
+  }
+  launch_skinny_m<LNA, 4>(epi, p, s);
 }
 
 static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {

@@ -16,6 +16,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   if (row >= rows) return;
   const int nv = d / 4;
   const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * d);
+  // gamma / beta are independent of the row: in flight with it (one memory latency)
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4 gg[MAXV], bb[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int i = lane + k * 64;
+    gg[k] = i < nv ? g4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bb[k] = i < nv ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float4 v[MAXV];
   float s = 0.f;
 #pragma unroll
@@ -37,18 +47,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
   const float rstd = rsqrtf(q / d + eps);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  const float4* b4 = reinterpret_cast<const float4*>(b);
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int i = lane + k * 64;
     if (i >= nv) continue;
-    const float4 gg = g4[i], bb = b4[i];
     float4 y;
-    y.x = (v[k].x - mean) * rstd * gg.x + bb.x;
-    y.y = (v[k].y - mean) * rstd * gg.y + bb.y;
-    y.z = (v[k].z - mean) * rstd * gg.z + bb.z;
-    y.w = (v[k].w - mean) * rstd * gg.w + bb.w;
+    y.x = (v[k].x - mean) * rstd * gg[k].x + bb[k].x;
+    y.y = (v[k].y - mean) * rstd * gg[k].y + bb[k].y;
+    y.z = (v[k].z - mean) * rstd * gg[k].z + bb[k].z;
+    y.w = (v[k].w - mean) * rstd * gg[k].w + bb[k].w;
     if constexpr (F32OUT) {
       reinterpret_cast<float4*>(static_cast<float*>(out) + (int64_t)row * d)[i] = y;
     } else {
