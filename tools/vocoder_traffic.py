@@ -34,7 +34,7 @@ def counters(d):
     tot, n = 0.0, set()
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "conv_kernel" in k or "resunit_kernel" in k or "resunit_wide_kernel" in k:
+        if "conv_kernel" in k or ("resunit" in k and "pack" not in k):
             tot += float(r["Counter_Value"])
             n.add(r["Dispatch_Id"])
     return tot, len(n)
@@ -69,7 +69,7 @@ def reduce(fdir, wdir, out):
     assert nf == nw and nf > 0, (nf, nw)
     fetch = 2.0 * fetch_kb * 1024  # gfx950: FETCH_SIZE = half the streamed bytes (KB units)
     write = write_kb * 1024
-    res = {"kernel": "conv_kernel + resunit_kernel + resunit_wide_kernel (vocoder convs, all shapes of one 64 x 30 s "
+    res = {"kernel": "conv_kernel + resunit_kernel + resunit_wide[_lds]_kernel (vocoder convs, all shapes of one 64 x 30 s "
                      "forward: the launch set the bench's roofline averages over)",
            "launches": nf, "fetch_bytes": fetch, "write_bytes": write,
            "bytes_per_launch": (fetch + write) / nf,
