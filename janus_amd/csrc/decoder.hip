@@ -333,7 +333,8 @@ template <int NKS>  // K / 32
 __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
-    LogitPart* __restrict__ parts, int ntiles) {
+    LogitPart* __restrict__ parts, int ntiles, const float* __restrict__ lnx, int ldx,
+    const float* __restrict__ ln_g, const float* __restrict__ ln_b) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   constexpr int K = NKS * 32;
   constexpr int AP = K + 16;  // row pitch (halves): 16*AP bytes with AP/8 % 4 == 2 -> conflict-free
@@ -341,11 +342,18 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
   float* sT = reinterpret_cast<float*>(sA + 64 * AP);                // [waves][64][17]
   RowRules* sR = reinterpret_cast<RowRules*>(sT + kLgWaves * 64 * 17);  // [64]
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
-  for (int i = tid; i < 64 * (K / 8); i += kLgWaves * 64) {
-    const int r = i / (K / 8), c8 = (i % (K / 8)) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < B) v = *reinterpret_cast<const uint4*>(A + (int64_t)r * lda + c8);
-    *reinterpret_cast<uint4*>(sA + r * AP + c8) = v;
+  if (lnx) {  // A = the decoder's final LayerNorm of x, computed here (one wave per row)
+    for (int r = w; r < 64; r += kLgWaves) {
+      if (r < B) ln_row_wave<false>(lnx + (int64_t)r * ldx, ln_g, ln_b, sA + r * AP, K, 1e-5f, lane);
+      else for (int c = lane; c < K; c += 64) sA[r * AP + c] = (_Float16)0.0f;
+    }
+  } else {
+    for (int i = tid; i < 64 * (K / 8); i += kLgWaves * 64) {
+      const int r = i / (K / 8), c8 = (i % (K / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < B) v = *reinterpret_cast<const uint4*>(A + (int64_t)r * lda + c8);
+      *reinterpret_cast<uint4*>(sA + r * AP + c8) = v;
+    }
   }
   if (tid < 64) {
     RowRules rr;
@@ -426,7 +434,8 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
 
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
-                           LogitPart* parts, hipStream_t s) {
+                           LogitPart* parts, hipStream_t s, const float* lnx, int ldx,
+                           const float* ln_g, const float* ln_b) {
   JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
   const int ntiles = logits_partial_blocks(V);
   const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)kLgWaves * 64 * 17 * 4 + 64 * sizeof(RowRules);
@@ -442,7 +451,8 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   const int grid = std::min(256, (ntiles + kLgWaves - 1) / kLgWaves);
   for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
     kern<<<grid, kLgWaves * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
-                                          smask, rules + r0, parts + (int64_t)r0 * ntiles, ntiles);
+                                          smask, rules + r0, parts + (int64_t)r0 * ntiles, ntiles,
+                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b);
   JANUS_LAUNCH_CHECK();
 }
 

@@ -162,15 +162,23 @@ struct SkinnyArgs {
   float2* ln_part;
   int a_group_cols;
   const float* ln_g; const float* ln_b; float ln_eps; _Float16* ln_out; int* ln_cnt;
+  const float* lnin_g; const float* lnin_b;  // AM_LNX: A = LayerNorm(x) computed in-block
 };
+
+// A operand modes: fp16 from global memory; LayerNorm-on-load from producer pieces
+// (JANUS_FUSED_LN); LayerNorm of the block's fp32 rows computed in the block's prologue
+// into an fp16 LDS tile (no separate LayerNorm launch).
+enum SkinnyAMode { AM_F16 = 0, AM_LNA = 1, AM_LNX = 2 };
 
 constexpr int kSkWaves = 16;
 
 // MTB: 16-row m-tiles per block (4: all 64 rows; 1: rows split over gridDim.y, for narrow
 // outputs whose N / 16 column tiles alone would leave most CUs idle).
-template <int EPI, bool LNA, int MTB>
+template <int EPI, int AM, int MTB>
 __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
+  constexpr bool LNA = AM == AM_LNA, LNX = AM == AM_LNX;
   constexpr int G = LNA ? 1 : 2;  // k-steps in flight per wave (128-VGPR budget at 1024 threads)
+  extern __shared__ __attribute__((aligned(16))) _Float16 sk_smem[];  // LNX: [16*MTB][AP]
   static_assert(!LNA || MTB == 4, "LayerNorm-on-load needs all rows per block");
   __shared__ float red[8][16 * MTB][17];
   __shared__ float s_mean[64], s_rstd[64];
@@ -183,9 +191,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
   const int lr = lane & 15, kc8 = 8 * (lane >> 4);
   const _Float16* Ab = p.A;
-  if constexpr (!LNA) {
+  if constexpr (AM == AM_F16) {
     if (p.a_group_cols > 0) Ab += (int64_t)(col0 / p.a_group_cols) * K;  // block-diagonal
   }
+  const int AP = frag_pitch(K);  // LNX tile pitch (halves)
 
   // epilogue operands independent of the product, in flight from the start
   const int elr = tid >> 4, erow = r0 + elr, ec = tid & 15, ecol = col0 + ec;
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
           const bool rok = ok && r < M;
           ax[g][m][0] = rok ? *reinterpret_cast<const float4*>(xr) : make_float4(0.f, 0.f, 0.f, 0.f);
           ax[g][m][1] = rok ? *reinterpret_cast<const float4*>(xr + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {
+        } else if constexpr (!LNX) {
           ah[g][m] = (ok && r < M) ? *reinterpret_cast<const half8*>(Ab + (int64_t)r * p.lda + kk)
                                    : zero_half8();
         }
@@ -218,6 +227,20 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
     }
   };
   load(kbeg);
+
+  if constexpr (LNX) {
+    // this block's rows of LN(x) -> fp16 LDS tile, one wave per row (weights in flight)
+    for (int r = w; r < 16 * MTB; r += kSkWaves) {
+      const int gr = r0 + r;
+      if (gr < M) {
+        ln_row_wave<false>(p.x + (int64_t)gr * p.ldx, p.lnin_g, p.lnin_b, sk_smem + r * AP, K,
+                           p.eps, lane);
+      } else {
+        for (int c = lane; c < K; c += 64) sk_smem[r * AP + c] = (_Float16)0.0f;
+      }
+    }
+    __syncthreads();
+  }
 
   if constexpr (LNA) {
     // row statistics from the producer's pieces: waves 0-3, thread = (row, quarter)
@@ -287,6 +310,11 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
           for (int j = 0; j < 8; ++j)
             af[m][j] = (ok && r < M) ? (_Float16)((xv[j] - mean) * rstd * ga[j] + be[j]) : (_Float16)0.0f;
         }
+      } else if constexpr (LNX) {
+        const bool ok = kk < kend;
+#pragma unroll
+        for (int m = 0; m < MTB; ++m)
+          af[m] = ok ? *reinterpret_cast<const half8*>(sk_smem + (m * 16 + lr) * AP + kk) : zero_half8();
       } else {
 #pragma unroll
         for (int m = 0; m < MTB; ++m) af[m] = ah[g][m];
@@ -369,25 +397,41 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   }
 }
 
-template <bool LNA, int MTB>
+template <int AM, int EPI, int MTB>
+static void skinny_go(const SkinnyArgs& p, dim3 grid, hipStream_t s) {
+  auto kern = gemm_skinny_kernel<EPI, AM, MTB>;
+  size_t lds = 0;
+  if constexpr (AM == AM_LNX) {
+    lds = (size_t)16 * MTB * frag_pitch(p.K) * 2;
+    static bool attr = false;
+    if (!attr) {
+      JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    100 * 1024));
+      attr = true;
+    }
+  }
+  kern<<<grid, 1024, lds, s>>>(p);
+}
+
+template <int AM, int MTB>
 static void launch_skinny_m(int epi, const SkinnyArgs& p, hipStream_t s) {
   const dim3 grid((p.N + 15) / 16, (p.M + 16 * MTB - 1) / (16 * MTB));
   switch (epi) {
-    case EPI_F16: gemm_skinny_kernel<EPI_F16, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
-    case EPI_GELU_F16: gemm_skinny_kernel<EPI_GELU_F16, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
-    case EPI_QKV: gemm_skinny_kernel<EPI_QKV, LNA, MTB><<<grid, 1024, 0, s>>>(p); break;
+    case EPI_F16: skinny_go<AM, EPI_F16, MTB>(p, grid, s); break;
+    case EPI_GELU_F16: skinny_go<AM, EPI_GELU_F16, MTB>(p, grid, s); break;
+    case EPI_QKV: skinny_go<AM, EPI_QKV, MTB>(p, grid, s); break;
     case EPI_RESID_F32:
-      if constexpr (!LNA) { gemm_skinny_kernel<EPI_RESID_F32, false, MTB><<<grid, 1024, 0, s>>>(p); break; }
+      if constexpr (AM == AM_F16) { skinny_go<AM, EPI_RESID_F32, MTB>(p, grid, s); break; }
       else throw Error("skinny LN gemm: bad epilogue");
     case EPI_F32:
-      if constexpr (!LNA) { gemm_skinny_kernel<EPI_F32, false, MTB><<<grid, 1024, 0, s>>>(p); break; }
+      if constexpr (AM == AM_F16) { skinny_go<AM, EPI_F32, MTB>(p, grid, s); break; }
       else throw Error("skinny LN gemm: bad epilogue");
     default: throw Error("bad gemm epilogue");
   }
   JANUS_LAUNCH_CHECK();
 }
 
-template <bool LNA>
+template <int AM>
 static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
   // narrow outputs (N <= JANUS_SKINNY_MSPLIT_N, default 2048: <= 128 column tiles) split the
   // rows over 16-row blocks as well, so 4x as many CUs share the latency-bound product
@@ -395,10 +439,10 @@ static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
     const char* e = std::getenv("JANUS_SKINNY_MSPLIT_N");
     return e ? std::atoi(e) : 2048;
   }();
-  if constexpr (!LNA) {
-    if (p.N <= msplit_n && p.ln_part == nullptr) { launch_skinny_m<false, 1>(epi, p, s); return; }
+  if constexpr (AM != AM_LNA) {
+    if (p.N <= msplit_n && p.ln_part == nullptr) { launch_skinny_m<AM, 1>(epi, p, s); return; }
   }
-  launch_skinny_m<LNA, 4>(epi, p, s);
+  launch_skinny_m<AM, 4>(epi, p, s);
 }
 
 static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
@@ -409,7 +453,12 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.ln_part = g.ln_part;
   p.a_group_cols = g.a_group_cols;
   p.ln_g = g.ln_g; p.ln_b = g.ln_b; p.ln_eps = g.ln_eps; p.ln_out = g.ln_out; p.ln_cnt = g.ln_cnt;
-  launch_skinny_t<false>(epi, p, s);
+  if (g.lnin_x) {  // A = LayerNorm(x) in the block's prologue
+    p.x = g.lnin_x; p.ldx = g.lnin_ldx; p.lnin_g = g.lnin_g; p.lnin_b = g.lnin_b; p.eps = g.lnin_eps;
+    launch_skinny_t<AM_LNX>(epi, p, s);
+    return;
+  }
+  launch_skinny_t<AM_F16>(epi, p, s);
 }
 
 void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& g, hipStream_t s) {
@@ -420,7 +469,7 @@ void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& g, hipStream_t s) {
   p.x = g.x; p.ldx = g.ldx; p.part = g.part; p.gamma = g.gamma; p.beta = g.beta; p.eps = g.eps;
   p.W = g.W; p.ldw = g.ldw; p.bias = g.bias; p.C = g.C; p.ldc = g.ldc; p.M = g.M; p.N = g.N; p.K = g.K;
   p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
-  launch_skinny_t<true>(epi, p, s);
+  launch_skinny_t<AM_LNA>(epi, p, s);
 }
 
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
@@ -433,6 +482,9 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
               "gemm: grouped A needs M <= 64 and 16-column groups");
   JANUS_CHECK(!p.ln_part || (epi == EPI_RESID_F32 && p.N % 16 == 0),
               "gemm: LayerNorm pieces come from a RESID epilogue with N % 16 == 0");
+  JANUS_CHECK(!p.lnin_x || (p.M <= 64 && p.K <= 1024 && p.K % 32 == 0 && p.a_group_cols == 0 &&
+                            p.lnin_g && p.lnin_b && epi != EPI_RESID_F32 && epi != EPI_F32),
+              "gemm: LayerNorm-prologue A needs M <= 64, K <= 1024 (multiple of 32), no groups");
   JANUS_CHECK(!p.ln_out || (epi == EPI_RESID_F32 && p.M <= 64 && p.N <= 1024 && p.ln_cnt &&
                             p.ln_g && p.ln_b && p.ldc == p.N),
               "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 1024, ldc == N");

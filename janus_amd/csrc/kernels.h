@@ -28,6 +28,11 @@ struct GemmArgs {
   // into ln_out [M][N] fp16 with (ln_g, ln_b, ln_eps) and re-arms ln_cnt (zero on entry).
   const float* ln_g = nullptr; const float* ln_b = nullptr; float ln_eps = 1e-5f;
   _Float16* ln_out = nullptr; int* ln_cnt = nullptr;
+  // M <= 64 only: A = LayerNorm(lnin_x) (fp32 [M][K], row stride lnin_ldx) computed in
+  // every block's prologue into an fp16 LDS tile — the pre-LN block needs no separate
+  // LayerNorm launch (A / lda are then unused).
+  const float* lnin_x = nullptr; int64_t lnin_ldx = 0;
+  const float* lnin_g = nullptr; const float* lnin_b = nullptr; float lnin_eps = 1e-5f;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
 

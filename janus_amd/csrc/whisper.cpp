@@ -326,6 +326,16 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   // Measured slower than the separate launches (616.8 vs 536.5 ms per bench step): the
   // write-through stores and the serial tail cost more than the launch they save.
   const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && std::getenv("JANUS_LN_FUSE") != nullptr;
+  // JANUS_LN_PROLOGUE (opt-in, B <= 64): every pre-LN projection computes LayerNorm(x)
+  // for its rows in the block prologue (GemmArgs::lnin_x), the vocabulary projection the
+  // final LayerNorm — no LayerNorm launches. Measured slower than the separate launches
+  // (503.9 vs 483.8 ms per bench step): every block re-reads its x rows in fp32 and runs
+  // the row reductions ahead of its MFMAs.
+  const bool ln_pro = B <= 64 && !fused_ln && !ln_fuse && std::getenv("JANUS_LN_PROLOGUE") != nullptr;
+  auto with_ln = [&](GemmArgs g, const float* lg, const float* lb) {
+    if (ln_pro) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
+    return g;
+  };
   w->d_lncnt.ensure(sizeof(int));
   JANUS_HIP(hipMemsetAsync(w->d_lncnt.p, 0, sizeof(int), s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
@@ -351,9 +361,10 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
-        if (!ln_fuse) layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
+        if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
         if (B <= 64) {
-          GemmArgs g = gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d);
+          GemmArgs g = with_ln(gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
+                               L.ln1g, L.ln1b);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
           gemm_launch(EPI_QKV, g, s);
         } else {
@@ -372,8 +383,9 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-          gemm_launch(EPI_F16, gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d), s);
+          if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          gemm_launch(EPI_F16, with_ln(gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
+                                       L.ln2g, L.ln2b), s);
         }
         xattn_launch(xqk, enc, B, Te, d, H, xsplit, w->d_xpc.as<float>(), w->d_xpml.as<float>(), xc, s);
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
@@ -386,8 +398,9 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
                                                 nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-          gemm_launch(EPI_F16, gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d), s);
+          if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          gemm_launch(EPI_F16, with_ln(gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d),
+                                       L.ln2g, L.ln2b), s);
         }
         decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                       part_ml, s);
@@ -397,17 +410,19 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
         gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
-        if (!ln_fuse) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
-        gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d), s);
+        if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+        gemm_launch(EPI_GELU_F16, with_ln(gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d),
+                                          L.ln3g, L.ln3b), s);
       }
       // next LayerNorm: the following layer's LN1, or the decoder's final LN
       resid(f, 4 * d, L.w2, L.b2, l + 1 < nl ? w->dec[l + 1].ln1g : fin_g,
             l + 1 < nl ? w->dec[l + 1].ln1b : fin_b);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
-    if (!ln_fuse) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
+    if (!ln_fuse && !ln_pro) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, w->d_smask.as<uint8_t>(),
-                          w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s);
+                          w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s,
+                          ln_pro ? x : nullptr, d, fin_g, fin_b);
     select_partials_launch(w->d_parts.as<LogitPart>(), nblk, R, w->d_rules.as<RowRules>(), tokens,
                            maxlen, pos, done, sum_lp, n_tokens, B, s);
   };
@@ -418,7 +433,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
       (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
-      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)w->d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
+      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)w->d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
       (int64_t)w->d_xc.p, (int64_t)w->d_xpc.p, (int64_t)w->d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
