@@ -50,6 +50,26 @@ int janus_prosody_analyze(const float* pcm, const int64_t* sample_offsets,
                           float* rms_out, float* mean_f0_out, int32_t* n_voiced_out,
                           void* stream);
 
+/* ------------------------------------------------- receiver / streaming --- */
+/*
+ * Playback ducking, in place on int16 PCM [device] (n samples): replaces
+ * apply_ducking_if_needed (backend/services/engine.py:94-134) for level in [0, 1):
+ * s = int16(trunc(clip(float32(s) * level, -32768, 32767))), numpy's
+ * np.clip(s.astype(np.float32) * level, -32768, 32767).astype(np.int16) bit for bit.
+ * (level >= 1 and ducking-off / not-talking are pass-throughs the caller skips.)
+ */
+int janus_duck_pcm16(int16_t* pcm, int64_t n, float level, void* stream);
+
+/*
+ * Speech-gate probability per chunk: pcm [device] f32 [n_chunks][chunk_len] (e.g. the
+ * 1536-sample 48 kHz capture chunks, audio_io.py:28-31), prob_out [device] f32[n_chunks].
+ * Stands in for VoiceActivityDetector.is_speech (backend/services/vad.py:40-77: x[::3]
+ * -> silero -> prob > threshold), whose weights are a remote torch.hub download:
+ * prob = sigmoid((10 log10(mean(x[::decim]^2)) - center_db) / width_db).
+ */
+int janus_vad_energy(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
+                     float center_db, float width_db, float* prob_out, void* stream);
+
 /* -------------------------------------------------------- packet codec --- */
 enum {
   JANUS_VAL_NIL = 0,

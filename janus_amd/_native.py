@@ -46,6 +46,8 @@ _F32 = ctypes.c_float
 # name -> (argtypes). Every entry point returns int status.
 SIGNATURES = {
     "janus_version": [],
+    "janus_duck_pcm16": [_P, _I64, _F32, _P],
+    "janus_vad_energy": [_P, _I64, _I32, _I32, _F32, _F32, _P, _P],
     "janus_prosody_analyze": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
                               _P, _P, _P],
     "janus_pack_packet": [ctypes.POINTER(janus_packet), _P, ctypes.c_size_t,

@@ -12,6 +12,10 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
                     const float* state_in, float* state_out, float* f0_out, float* rms_out,
                     float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream);
 
+void duck_pcm16_launch(int16_t* pcm, int64_t n, float level, hipStream_t s);
+void vad_energy_launch(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
+                       float center_db, float width_db, float* prob, hipStream_t s);
+
 }  // namespace janus
 
 using namespace janus;
@@ -30,5 +34,23 @@ extern "C" int janus_prosody_analyze(const float* pcm, const int64_t* sample_off
     prosody_launch(pcm, sample_offsets, hop_offsets, batch, total_hops, sample_rate, hop_size,
                    tolerance, silence_db, state_in, state_out, f0_out, rms_out, mean_f0_out,
                    n_voiced_out, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_duck_pcm16(int16_t* pcm, int64_t n, float level, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(pcm || n == 0, "null argument");
+    JANUS_CHECK(level >= 0.0f && level < 1.0f, "ducking level must be in [0, 1) (callers skip 1.0)");
+    duck_pcm16_launch(pcm, n, level, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_vad_energy(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
+                                float center_db, float width_db, float* prob_out, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK((pcm && prob_out) || n_chunks == 0, "null argument");
+    JANUS_CHECK(chunk_len > 0 && decim > 0 && width_db > 0.0f, "bad VAD geometry");
+    vad_energy_launch(pcm, n_chunks, chunk_len, decim, center_db, width_db, prob_out,
+                      (hipStream_t)stream);
   });
 }

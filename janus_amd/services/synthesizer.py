@@ -49,6 +49,25 @@ def emotion_prompt(packet: JanusPacket) -> tuple:
     return f"({tag}) {packet.text}", tag
 
 
+MORSE_CODE = {  # synthesizer.py:57-65
+    'A': '.-', 'B': '-...', 'C': '-.-.', 'D': '-..', 'E': '.', 'F': '..-.',
+    'G': '--.', 'H': '....', 'I': '..', 'J': '.---', 'K': '-.-', 'L': '.-..',
+    'M': '--', 'N': '-.', 'O': '---', 'P': '.--.', 'Q': '--.-', 'R': '.-.',
+    'S': '...', 'T': '-', 'U': '..-', 'V': '...-', 'W': '.--', 'X': '-..-',
+    'Y': '-.--', 'Z': '--..',
+    '0': '-----', '1': '.----', '2': '..---', '3': '...--', '4': '....-',
+    '5': '.....', '6': '-....', '7': '--...', '8': '---..', '9': '----.',
+    ' ': ' ',
+}
+
+
+def morse_audio(text: str) -> bytes:
+    """Synthesizer._generate_morse_audio without building a Synthesizer (no vocoder)."""
+    class _Codes:
+        morse_code_dict = MORSE_CODE
+    return Synthesizer._generate_morse_audio(_Codes(), text)
+
+
 class Synthesizer:
     def __init__(self, api_key: str, reference_audio_path: str | None = None):
         self.api_key = api_key
@@ -58,16 +77,7 @@ class Synthesizer:
         self._reference_audio_path = reference_audio_path
         if self._reference_audio_path:
             self._load_reference_audio(self._reference_audio_path)
-        self.morse_code_dict = {
-            'A': '.-', 'B': '-...', 'C': '-.-.', 'D': '-..', 'E': '.', 'F': '..-.',
-            'G': '--.', 'H': '....', 'I': '..', 'J': '.---', 'K': '-.-', 'L': '.-..',
-            'M': '--', 'N': '-.', 'O': '---', 'P': '.--.', 'Q': '--.-', 'R': '.-.',
-            'S': '...', 'T': '-', 'U': '..-', 'V': '...-', 'W': '.--', 'X': '-..-',
-            'Y': '-.--', 'Z': '--..',
-            '0': '-----', '1': '.----', '2': '..---', '3': '...--', '4': '....-',
-            '5': '.....', '6': '-....', '7': '--...', '8': '---..', '9': '----.',
-            ' ': ' ',
-        }
+        self.morse_code_dict = dict(MORSE_CODE)
 
     def _load_reference_audio(self, audio_path: str) -> None:
         try:

@@ -1,0 +1,199 @@
+"""Streaming encode for many concurrent capture channels (SURVEY.md §8(f) rows 1-2;
+BASELINE config 5: 128 channels x 320 ms chunks over 8 GPUs, per-chunk p50 latency).
+
+The reference runs ONE channel: ``smart_ear_loop`` (backend/services/engine.py:382-575)
+pulls 1536-sample 48 kHz chunks (audio_io.py:28-31), gates them with silero VAD
+(engine.py:474, vad.py:40-77), segments phrases (pre-roll 10 chunks, > 15 silent chunks
+ends a phrase, phrases under 9216 samples dropped, push-to-talk hold/release:
+engine.py:438-506), then transcribes + analyses prosody + packs each phrase
+(process_audio_blocking / transmit_packet_blocking, engine.py:510-552) with ONE stateful
+aubio detector (prosody.py:32). Here S channels advance together:
+
+* the speech gate runs for every chunk of every channel in one launch
+  (``janus_vad_energy``; silero's weights are a remote download, so the gate is the
+  documented energy stand-in of include/janus.h — swap in real probabilities through
+  ``push(..., speech=...)``);
+* ``PhraseSegmenter`` is the engine's per-chunk state machine, one per channel;
+* phrases that complete on the same tick are encoded as ONE batch on the GPU (log-mel,
+  encoder, greedy decoder, YIN + RMS) with each channel's persistent 4096-sample detector
+  buffer gathered in and scattered back, exactly one aubio object per channel.
+"""
+import time
+from collections import deque
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .common.protocol import JanusMode, JanusPacket
+from .services.prosody import YIN_BUF, energy_tag, pitch_tag, prosody_launch
+
+CHUNK = 1536                  # audio_io.py:28-31 (48 kHz int16 -> f32 chunks)
+PRE_ROLL_CHUNKS = 10          # engine.py:439
+SILENCE_THRESHOLD_CHUNKS = 15  # engine.py:441
+MIN_PHRASE_SAMPLES = CHUNK * 6  # engine.py:504
+CAPTURE_RATE = 48000
+
+# energy stand-in for silero (vad.py:40-77): P(speech) = sigmoid((dB - center) / width)
+VAD_CENTER_DB = -45.0
+VAD_WIDTH_DB = 3.0
+
+
+class PhraseSegmenter:
+    """engine.py:438-506 for one channel: feed every chunk with its gate decision; returns
+    the phrase audio when one completes (and is long enough), else None."""
+
+    def __init__(self):
+        self.audio_buffer = []
+        self.pre_roll_buffer = deque(maxlen=PRE_ROLL_CHUNKS)
+        self.silence_counter = 0
+        self.previous_hold_state = False
+        self.is_talking = False
+        self.skipped = 0  # phrases dropped as shorter than MIN_PHRASE_SAMPLES
+
+    def push(self, chunk: np.ndarray, is_speech: bool, streaming: bool = True,
+             recording: bool = False, non_vad_mode: bool = False):
+        trigger = False
+        if recording:                                  # :458-463 push-to-talk hold
+            self.is_talking = True
+            self.audio_buffer.append(chunk)
+            self.previous_hold_state = True
+            return None
+        if self.previous_hold_state:                   # :466-469 release (chunk dropped)
+            trigger = True
+            self.previous_hold_state = False
+            self.is_talking = False
+        elif streaming:                                # :471-495
+            if is_speech or non_vad_mode:
+                if not self.audio_buffer:
+                    self.audio_buffer.extend(list(self.pre_roll_buffer))  # pre-roll kept
+                self.is_talking = True
+                self.audio_buffer.append(chunk)
+                self.silence_counter = 0
+            else:
+                self.silence_counter += 1
+                if self.audio_buffer:
+                    self.audio_buffer.append(chunk)
+                else:
+                    self.pre_roll_buffer.append(chunk)
+                if self.silence_counter > SILENCE_THRESHOLD_CHUNKS:
+                    trigger = True
+                    self.is_talking = False
+        else:                                          # :497-499
+            self.is_talking = False
+        if trigger and self.audio_buffer:              # :501-506
+            combined = np.concatenate(self.audio_buffer)
+            self.audio_buffer = []
+            self.silence_counter = 0
+            if len(combined) < MIN_PHRASE_SAMPLES:
+                self.skipped += 1
+                return None
+            return combined
+        return None
+
+
+class VoiceActivityDetector:
+    """Same constructor / is_speech / reset as vad.py:10-88 plus the batched GPU form;
+    probabilities from the energy stand-in (janus_vad_energy), threshold as the reference."""
+
+    def __init__(self, threshold: float = 0.5, sample_rate: int = 48000) -> None:
+        self.device = nat.require_gpu()
+        self.threshold = threshold
+        self.sample_rate = sample_rate
+        self.decim = 3 if sample_rate in (48000, 44100) else 1  # vad.py:54-61
+
+    def probabilities(self, chunks: torch.Tensor) -> torch.Tensor:
+        """chunks: [N][L] f32 on the GPU -> [N] speech probabilities (device)."""
+        assert chunks.is_cuda and chunks.dtype == torch.float32 and chunks.is_contiguous()
+        n, L = chunks.shape
+        prob = torch.empty(max(n, 1), dtype=torch.float32, device=chunks.device)
+        nat.call("janus_vad_energy", chunks.data_ptr(), n, L, self.decim, VAD_CENTER_DB,
+                 VAD_WIDTH_DB, prob.data_ptr(), nat.stream_ptr(chunks.device))
+        return prob[:n]
+
+    def is_speech_batch(self, chunks: torch.Tensor) -> np.ndarray:
+        return (self.probabilities(chunks) > self.threshold).cpu().numpy()
+
+    def is_speech(self, audio_chunk) -> bool:
+        x = torch.as_tensor(np.ascontiguousarray(audio_chunk, np.float32)).to(self.device)
+        return bool(self.is_speech_batch(x.reshape(1, -1))[0])
+
+    def reset(self) -> None:
+        pass
+
+
+class StreamingEncoder:
+    """S channels x one JanusPipeline-style encode per completed phrase batch.
+
+    push(block) takes the next [S][n*1536] capture samples of every channel (numpy f32 or
+    a GPU tensor) and returns the phrases completed by it as dicts
+    {stream, text, tags, packet} (packet None when the text is empty, engine.py:536)."""
+
+    def __init__(self, n_streams: int, whisper, max_length: int = 448,
+                 mode: JanusMode = JanusMode.SEMANTIC_VOICE, override="auto",
+                 vad_threshold: float = 0.5, hop: int = 512):
+        self.device = nat.require_gpu()
+        self.S = n_streams
+        self.whisper = whisper
+        self.max_length = max_length
+        self.mode, self.override, self.hop = mode, override, hop
+        self.vad = VoiceActivityDetector(vad_threshold, CAPTURE_RATE)
+        self.segmenters = [PhraseSegmenter() for _ in range(n_streams)]
+        # one aubio detector buffer per channel (prosody.py:32), persistent across phrases
+        self.yin_state = torch.zeros(n_streams, YIN_BUF, dtype=torch.float32, device=self.device)
+        self.latencies = []  # seconds per push (chunk block of all channels)
+
+    def push(self, block, speech=None, timestamp=None):
+        t0 = time.perf_counter()
+        host = block.cpu().numpy() if isinstance(block, torch.Tensor) else np.asarray(block, np.float32)
+        S, L = host.shape
+        assert S == self.S and L % CHUNK == 0, "push [S][n*1536] samples"
+        n = L // CHUNK
+        if speech is None:
+            dev = block if isinstance(block, torch.Tensor) and block.is_cuda else \
+                torch.from_numpy(np.ascontiguousarray(host)).to(self.device)
+            speech = self.vad.is_speech_batch(dev.reshape(S * n, CHUNK).contiguous()).reshape(S, n)
+        done = []
+        for s in range(S):
+            for j in range(n):
+                ph = self.segmenters[s].push(host[s, j * CHUNK:(j + 1) * CHUNK], bool(speech[s, j]))
+                if ph is not None:
+                    done.append((s, ph))
+        out = self._encode(done, timestamp) if done else []
+        torch.cuda.synchronize(self.device)
+        self.latencies.append(time.perf_counter() - t0)
+        return out
+
+    def _encode(self, done, timestamp):
+        streams = [s for s, _ in done]
+        lengths = [len(p) for _, p in done]
+        pcm_np = np.concatenate([p for _, p in done] + [np.zeros(1, np.float32)]).astype(np.float32)
+        pcm = torch.from_numpy(pcm_np).to(self.device)
+        offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(self.device)
+        B = len(done)
+        w = self.whisper
+        mel = w.logmel(pcm, offs, B, 3)                 # transcriber.py:51 [::3]
+        tokens, _, _ = w.decode(w.encode(mel), self.max_length)
+        idx = torch.tensor(streams, dtype=torch.int64, device=self.device)
+        st_in = self.yin_state.index_select(0, idx).contiguous()
+        st_out = torch.empty_like(st_in)
+        try:
+            tags = prosody_launch(pcm, offs, lengths, CAPTURE_RATE, self.hop,
+                                  state_in=st_in, state_out=st_out).tags()
+            self.yin_state.index_copy_(0, idx, st_out)
+        except Exception:                               # engine.py:520-525
+            tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
+        texts = w.texts(tokens)
+        ts = time.time() if timestamp is None else timestamp
+        res = []
+        for s, t, g in zip(streams, texts, tags):
+            pkt = JanusPacket(t, self.mode, g, self.override, ts).serialize() if t.strip() else None
+            res.append({"stream": s, "text": t, "tags": g, "packet": pkt})
+        return res
+
+    def p50_ms(self) -> float:
+        return float(np.median(self.latencies) * 1000.0) if self.latencies else float("nan")
+
+
+__all__ = ["PhraseSegmenter", "VoiceActivityDetector", "StreamingEncoder", "energy_tag",
+           "pitch_tag", "CHUNK", "MIN_PHRASE_SAMPLES"]

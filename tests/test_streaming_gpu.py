@@ -1,0 +1,113 @@
+"""Streaming encode (config 5) and receiver glue on the GPU."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from janus_amd.common.wire import frame_batch
+from janus_amd.receiver import ReceiverBatch, apply_ducking_if_needed, duck_pcm16_
+from janus_amd.streaming import CHUNK, VAD_CENTER_DB, VAD_WIDTH_DB, StreamingEncoder, VoiceActivityDetector
+from janus_amd.whisper import CONFIGS, WhisperEngine
+from janus_amd.workload import synth_speech
+from oracle import packet as opk
+from oracle.prosody import OracleProsody
+from oracle.segmenter import duck, segment
+
+pytestmark = pytest.mark.gpu
+
+
+class _State:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+@pytest.mark.parametrize("level", [0.0, 0.25, 0.5, 0.999])
+def test_duck_bit_exact(gpu, level):
+    rng = np.random.default_rng(int(level * 1000))
+    s = rng.integers(-32768, 32768, 100003, dtype=np.int64).astype(np.int16)
+    s[:4] = [-32768, 32767, -1, 1]
+    ref = np.frombuffer(duck(s.tobytes(), True, True, level), np.int16)
+    t = torch.from_numpy(s.copy()).to(gpu)
+    duck_pcm16_(t, level)
+    assert np.array_equal(t.cpu().numpy(), ref)
+    st = _State(ducking_enabled=True, is_talking=True, ducking_level=level)
+    assert apply_ducking_if_needed(s.tobytes(), st) == ref.tobytes()
+
+
+def test_duck_pass_through(gpu):
+    b = np.arange(-50, 50, dtype=np.int16).tobytes()
+    assert apply_ducking_if_needed(b, _State(ducking_enabled=False, is_talking=True)) == b
+    assert apply_ducking_if_needed(b, _State(ducking_enabled=True, is_talking=False)) == b
+    assert apply_ducking_if_needed(b, _State(ducking_enabled=True, is_talking=True, ducking_level=1.5)) == b
+    assert apply_ducking_if_needed(b"", _State(ducking_enabled=True, is_talking=True)) == b""
+
+
+def test_vad_energy(gpu):
+    rng = np.random.default_rng(3)
+    amp = np.array([0.0, 1e-4, 1e-3, 5e-3, 0.01, 0.1, 0.5], np.float32)
+    x = (rng.standard_normal((len(amp), CHUNK)).astype(np.float32) * amp[:, None]).astype(np.float32)
+    vad = VoiceActivityDetector()
+    prob = vad.probabilities(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    ms = (x[:, ::3].astype(np.float64) ** 2).mean(1)
+    db = 10 * np.log10(ms + 1e-12)
+    ref = 1 / (1 + np.exp(-(db - VAD_CENTER_DB) / VAD_WIDTH_DB))
+    assert np.allclose(prob, ref, atol=1e-4)
+    assert vad.is_speech(x[-1]) and not vad.is_speech(x[0])
+
+
+def test_streaming_encoder_matches_oracle(gpu):
+    S, ticks, per_tick = 2, 14, 10                 # 320 ms chunks (10 x 1536 @ 48 kHz)
+    w = WhisperEngine(CONFIGS["tiny.en"], seed=0)
+    enc = StreamingEncoder(S, w, max_length=8)
+    total = ticks * per_tick * CHUNK
+    audio = np.zeros((S, total), np.float32)
+    for s in range(S):  # speech / silence / speech so phrases complete mid-run
+        a = synth_speech(300 + s, 2.0)
+        b = synth_speech(400 + s, 1.2)
+        audio[s, 5000:5000 + len(a)] = a
+        audio[s, 5000 + len(a) + 48000:5000 + len(a) + 48000 + len(b)] = b
+    vad = VoiceActivityDetector()
+    dec = vad.is_speech_batch(torch.from_numpy(audio.reshape(-1, CHUNK)).to(gpu)).reshape(S, -1)
+    got = []
+    for t in range(ticks):
+        blk = audio[:, t * per_tick * CHUNK:(t + 1) * per_tick * CHUNK]
+        got += [(t, r) for r in enc.push(blk, timestamp=1700000000.25)]
+    for s in range(S):
+        chunks = [audio[s, i * CHUNK:(i + 1) * CHUNK] for i in range(ticks * per_tick)]
+        ref = segment(chunks, list(dec[s]))
+        mine = [r for _, r in got if r["stream"] == s]
+        assert len(mine) == len(ref) and len(ref) >= 1
+        op = OracleProsody(48000)  # one stateful detector per channel
+        for r, (_, ph) in zip(mine, ref):
+            tags = op.analyze_buffer(ph)[0]
+            assert r["tags"] == tags
+            if r["text"].strip():
+                assert r["packet"] == opk.serialize(r["text"], 0, tags, "auto", 1700000000.25)
+            else:
+                assert r["packet"] is None
+    assert enc.p50_ms() > 0
+
+
+def test_receiver_batch(gpu):
+    from janus_amd.pipeline import JanusPipeline
+    from janus_amd.common.protocol import JanusMode, JanusPacket
+    pipe = JanusPipeline("tiny.en", max_length=8)
+    pk = [JanusPacket("hello there", JanusMode.SEMANTIC_VOICE, {"energy": "Loud", "pitch": "High"}, "Auto", 1.0),
+          JanusPacket("sos", JanusMode.MORSE_CODE, {}, "Auto", 2.0),
+          JanusPacket("fast one", JanusMode.TEXT_ONLY, {}, "happy", 3.0)]
+    raw = [p.serialize() for p in pk]
+    stream = frame_batch(raw[:2]) + frame_batch([b"\x93garbage"]) + frame_batch(raw[2:])
+    st = _State(ducking_enabled=True, is_talking=True, ducking_level=0.25)
+    rb = ReceiverBatch(pipe, 12, st)
+    for i in range(0, len(stream), 7):
+        rb.feed(stream[i:i + 7])
+    out = rb.synthesize()
+    assert len(out) == 4 and out[2] == b""
+    plain = ReceiverBatch(pipe, 12, None)
+    plain.feed(stream)
+    ref = plain.synthesize()
+    for k in (0, 3):
+        assert out[k][:44] == ref[k][:44] and len(out[k]) == 44 + 12 * 512 * 2
+        assert out[k][44:] == duck(ref[k][44:], True, True, 0.25)
+    assert out[1] == duck(ref[1], True, True, 0.25)

@@ -1,0 +1,66 @@
+"""Phrase segmentation (engine.py:438-506) against the oracle restatement, host only."""
+import numpy as np
+import pytest
+
+from janus_amd.streaming import CHUNK, PhraseSegmenter
+from oracle.segmenter import segment
+
+
+def run_product(chunks, speech, recording, streaming, non_vad):
+    seg = PhraseSegmenter()
+    out = []
+    for i, c in enumerate(chunks):
+        p = seg.push(c, speech[i], streaming=streaming[i], recording=recording[i], non_vad_mode=non_vad[i])
+        if p is not None:
+            out.append((i, p))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_segmenter_matches_oracle(seed):
+    rng = np.random.default_rng(seed)
+    n = 600
+    chunks = [rng.standard_normal(CHUNK).astype(np.float32) * 0.01 + i for i in range(n)]
+    # bursts of speech / silence of random lengths (incl. runs of exactly 15/16 silent chunks)
+    speech, cur = [], bool(rng.integers(2))
+    while len(speech) < n:
+        run = int(rng.choice([1, 2, 5, 15, 16, 17, 30, 80]))
+        speech += [cur] * run
+        cur = not cur
+    speech = speech[:n]
+    recording = [False] * n
+    streaming = [True] * n
+    non_vad = [False] * n
+    if seed % 3 == 1:   # push-to-talk holds
+        for a in rng.integers(0, n - 40, 4):
+            for k in range(int(a), int(a) + int(rng.integers(1, 30))):
+                recording[k] = True
+    if seed % 3 == 2:   # streaming toggled off, non-VAD (Morse/Text) mode stretches
+        for a in rng.integers(0, n - 40, 3):
+            for k in range(int(a), int(a) + 20):
+                streaming[k] = False
+        for a in rng.integers(0, n - 40, 3):
+            for k in range(int(a), int(a) + 10):
+                non_vad[k] = True
+    got = run_product(chunks, speech, recording, streaming, non_vad)
+    ref = segment(chunks, speech, recording, streaming, non_vad)
+    assert [i for i, _ in got] == [i for i, _ in ref]
+    for (_, a), (_, b) in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+def test_short_phrase_dropped_and_preroll_kept():
+    seg = PhraseSegmenter()
+    z = np.zeros(CHUNK, np.float32)
+    # 3 silent chunks (pre-roll), 1 speech chunk, 16 silent -> 20 chunks >= 9216: emitted
+    for _ in range(3):
+        assert seg.push(z, False) is None
+    assert seg.push(z + 1, True) is None
+    outs = [seg.push(z, False) for _ in range(16)]
+    assert outs[-1] is not None and len(outs[-1]) == (3 + 1 + 16) * CHUNK
+    # the deque is not cleared by a phrase (engine.py:481): its 3 old chunks + new ones
+    seg2 = PhraseSegmenter()
+    for _ in range(16):
+        seg2.push(z, False)          # fills pre-roll (last 10 kept), counter 16 > 15
+    p = seg2.push(z + 1, True)
+    assert p is None and len(seg2.audio_buffer) == 11
