@@ -52,7 +52,8 @@ template <int C> struct WideCfg;
 // NPB = weight k-steps in flight per wave (divides the k-step count k*C/32).
 // EPF: residual / accumulator rows loaded before c2 (in flight during it) where the
 // registers allow, else after it.
-template <> struct WideCfg<128> { static constexpr int BM = 128, WM = 1, WN = 4, NPB = 2; static constexpr bool EPF = false; };
+// NP: epilogue passes (the fp32 tile in NP row slices so the block fits 3 per CU)
+template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 4, NP = 2; static constexpr bool EPF = false; };
 
 template <int C>
 struct WideGeo {
@@ -70,8 +71,10 @@ struct WideGeo {
   static constexpr int NLD = (R0MAX * CPR + NT - 1) / NT;
   static constexpr int ES = C + 4;                // fp32 epilogue row pitch
   static constexpr int NE = (BM * CPR + NT - 1) / NT;
+  static constexpr int NP = Cfg::NP;
+  static constexpr int RP = 16 * ((MW2 + NP - 1) / NP);  // rows per epilogue pass
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
-  static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)BM * ES * 4);
+  static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)RP * ES * 4);
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
 };
 
@@ -236,34 +239,44 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
   if constexpr (!G::Cfg::EPF) epi_load();
   __syncthreads();  // sS dead: the fp32 epilogue tile takes its place
 
-  // ---- 4. epilogue: c2 + b2 -> fp32 LDS tile, then 16-byte row chunks
+  // ---- 4. epilogue in NP row passes (WM == 1: every wave owns all m-tiles): c2 + b2 ->
+  // fp32 LDS tile of RP rows, then 16-byte row chunks
+  static_assert(G::NP == 1 || WM == 1, "multi-pass epilogue needs WM == 1");
 #pragma unroll
-  for (int n = 0; n < NTW; ++n) {
-    const int co = (wn * NTW + n) * 16 + arow;
-    const float bias = a.b2[co];
+  for (int p = 0; p < G::NP; ++p) {
+    if (p > 0) __syncthreads();  // the previous pass's sE reads are done
+    constexpr int JP = (MW2 + G::NP - 1) / G::NP;  // m-tiles per pass
 #pragma unroll
-    for (int j = 0; j < MW2; ++j) {
-      const int m = wm + j * WM;
-      if (j >= MT2 / WM && m >= MT2) break;
+    for (int n = 0; n < NTW; ++n) {
+      const int co = (wn * NTW + n) * 16 + arow;
+      const float bias = a.b2[co];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) sE[(m * 16 + 4 * (lane >> 4) + rr) * ES + co] = acc2[j][n][rr] + bias;
+      for (int j = p * JP; j < (p + 1) * JP && j < MW2; ++j) {
+        const int m = wm + j * WM;
+        if (j >= MT2 / WM && m >= MT2) break;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          sE[(m * 16 - p * G::RP + 4 * (lane >> 4) + rr) * ES + co] = acc2[j][n][rr] + bias;
+      }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < G::NE; ++i) {
-    const int idx = tid + i * NT;
-    const int r = idx / CPR, cg = (idx % CPR) * 8;
-    if (r >= BM || t0 + r >= T) continue;
-    const float4 v0 = *reinterpret_cast<const float4*>(sE + r * ES + cg);
-    const float4 v1 = *reinterpret_cast<const float4*>(sE + r * ES + cg + 4);
-    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const half8 xv = *reinterpret_cast<const half8*>(&rq[i]);
-    const half8 pv = *reinterpret_cast<const half8*>(&pq[i]);
-    half8 hv;
+    for (int i = 0; i < G::NE; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / CPR, cg = (idx % CPR) * 8;
+      if (r < p * G::RP || r >= (p + 1) * G::RP) continue;  // compile-time per (i, p)
+      if (r >= BM || t0 + r >= T) continue;
+      const int rl = r - p * G::RP;
+      const float4 v0 = *reinterpret_cast<const float4*>(sE + rl * ES + cg);
+      const float4 v1 = *reinterpret_cast<const float4*>(sE + rl * ES + cg + 4);
+      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      const half8 xv = *reinterpret_cast<const half8*>(&rq[i]);
+      const half8 pv = *reinterpret_cast<const half8*>(&pq[i]);
+      half8 hv;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
-    *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+      *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+    }
   }
 }
 
@@ -293,7 +306,7 @@ template <int C> struct LdsCfg;
 // column slice is wide (C = 256), i.e. where direct per-wave B loads would exceed the
 // L2 -> CU rate. Same packed layout ([k-step][Cout][32]).
 // BM output rows per block, WM x WN waves, KB = K per weight k-block.
-template <> struct LdsCfg<64> { static constexpr int BM = 240, WM = 4, WN = 1, KB = 32; };
+template <> struct LdsCfg<64> { static constexpr int BM = 176, WM = 4, WN = 1, KB = 32; };
 template <> struct LdsCfg<256> { static constexpr int BM = 112, WM = 2, WN = 4, KB = 32; };
 
 template <int C>
