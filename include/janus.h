@@ -49,6 +49,17 @@ int janus_prosody_analyze(const float* pcm, const int64_t* sample_offsets,
                           const float* state_in, float* state_out, float* f0_out,
                           float* rms_out, float* mean_f0_out, int32_t* n_voiced_out,
                           void* stream);
+/*
+ * Same, with the YIN grid capped at max_blocks workgroups (0 = one per hop): a batch run
+ * beside other latency-bound work (the greedy decoder) leaves that work CUs to dispatch
+ * onto. Results are identical for every max_blocks.
+ */
+int janus_prosody_analyze_ex(const float* pcm, const int64_t* sample_offsets,
+                             const int64_t* hop_offsets, int batch, int64_t total_hops,
+                             int sample_rate, int hop_size, float tolerance, float silence_db,
+                             const float* state_in, float* state_out, float* f0_out,
+                             float* rms_out, float* mean_f0_out, int32_t* n_voiced_out,
+                             int max_blocks, void* stream);
 
 /* ------------------------------------------------- receiver / streaming --- */
 /*

@@ -10,7 +10,8 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
                     int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,
                     const float* state_in, float* state_out, float* f0_out, float* rms_out,
-                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream);
+                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream,
+                    int max_blocks = 0);
 
 void duck_pcm16_launch(int16_t* pcm, int64_t n, float level, hipStream_t s);
 void vad_energy_launch(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
@@ -34,6 +35,20 @@ extern "C" int janus_prosody_analyze(const float* pcm, const int64_t* sample_off
     prosody_launch(pcm, sample_offsets, hop_offsets, batch, total_hops, sample_rate, hop_size,
                    tolerance, silence_db, state_in, state_out, f0_out, rms_out, mean_f0_out,
                    n_voiced_out, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_prosody_analyze_ex(const float* pcm, const int64_t* sample_offsets,
+                                        const int64_t* hop_offsets, int batch, int64_t total_hops,
+                                        int sample_rate, int hop_size, float tolerance,
+                                        float silence_db, const float* state_in, float* state_out,
+                                        float* f0_out, float* rms_out, float* mean_f0_out,
+                                        int32_t* n_voiced_out, int max_blocks, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(max_blocks >= 0, "max_blocks must be >= 0");
+    prosody_launch(pcm, sample_offsets, hop_offsets, batch, total_hops, sample_rate, hop_size,
+                   tolerance, silence_db, state_in, state_out, f0_out, rms_out, mean_f0_out,
+                   n_voiced_out, (hipStream_t)stream, max_blocks);
   });
 }
 

@@ -20,6 +20,8 @@
 //
 // Roofline: VALU-bound (fp32 non-contracted sub/mul/add), ≈3·2048 flop per tau,
 // up to 2047 taus per hop; HBM traffic is 16 KB window per hop (L2-served overlap).
+#include <algorithm>
+#include <cstdlib>
 #include "common.h"
 
 namespace janus {
@@ -271,14 +273,18 @@ __global__ void prosody_state_kernel(const float* __restrict__ pcm, const int64_
 void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
                     int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,
                     const float* state_in, float* state_out, float* f0_out, float* rms_out,
-                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream) {
+                    float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream,
+                    int max_blocks) {
   JANUS_CHECK(B >= 0, "batch must be >= 0");
   JANUS_CHECK(hop > 0 && hop <= kYinBuf, "hop_size must be in [1, 4096]");
   JANUS_CHECK(sample_rate > 0, "sample_rate must be > 0");
   if (B == 0) return;
   JANUS_CHECK(state_in != state_out || state_in == nullptr, "state_in and state_out must not alias");
   if (total_hops > 0) {
-    const int64_t grid = total_hops < (1ll << 30) ? total_hops : (1ll << 30);
+    // max_blocks > 0 caps the grid (blocks loop over hops): the pipeline runs prosody
+    // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
+    const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
+    const int64_t grid = std::min<int64_t>(total_hops, cap);
     yin_hops_kernel<<<dim3((unsigned)grid), dim3(kYinThreads), 0, stream>>>(
         pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate, f0_out,
         total_hops);

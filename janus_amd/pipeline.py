@@ -46,18 +46,41 @@ class JanusPipeline:
                override="auto", timestamp=None) -> EncodeResult:
         B = len(lengths)
         w = self.whisper
-        mel = w.logmel(pcm, offsets, B, 3)
-        enc = w.encode(mel)
-        tokens, ntok, _ = w.decode(enc, self.max_length)
+        # prosody (YIN + RMS) does not depend on the transcript: it is enqueued first on
+        # the caller's stream and runs beside the Whisper chain, which goes to a
+        # high-priority stream — the greedy decoder is latency-bound and leaves most CUs
+        # idle for YIN to fill (the decoder's early-exit checks block the host, so the
+        # YIN launch must precede it)
+        main = torch.cuda.current_stream(pcm.device)
+        hi = self._hi_stream(pcm.device)
+        hi.wait_stream(main)
+        with torch.cuda.stream(hi):
+            mel = w.logmel(pcm, offsets, B, 3)
+            enc = w.encode(mel)
+        main.wait_stream(hi)  # YIN after the (compute-bound) encoder, beside the decoder
         try:
-            tags = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512).tags()
+            pres = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=256)
         except Exception:  # engine.py:520-525
+            pres = None
+        with torch.cuda.stream(hi):
+            tokens, ntok, _ = w.decode(enc, self.max_length)
+        main.wait_stream(hi)
+        try:
+            tags = pres.tags() if pres is not None else None
+        except Exception:
+            tags = None
+        if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
         texts = w.texts(tokens)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
         return EncodeResult(texts, tags, packets, tokens, ntok)
+
+    def _hi_stream(self, device):
+        if getattr(self, "_hi", None) is None:
+            self._hi = torch.cuda.Stream(device=device, priority=-1)
+        return self._hi
 
     # ------------------------------------------------------------------ decode
     def decode(self, packets, frames: int):

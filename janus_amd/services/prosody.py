@@ -61,7 +61,8 @@ class ProsodyResult:
 
 def prosody_launch(pcm: torch.Tensor, sample_offsets: torch.Tensor, lengths, sample_rate: int,
                    hop: int, tolerance: float = DEFAULT_TOLERANCE, silence_db: float = SILENCE_DB,
-                   state_in: torch.Tensor = None, state_out: torch.Tensor = None) -> ProsodyResult:
+                   state_in: torch.Tensor = None, state_out: torch.Tensor = None,
+                   max_blocks: int = 0) -> ProsodyResult:
     """Enqueue janus_prosody_analyze on the current stream; all tensors on the GPU."""
     B = len(lengths)
     dev = pcm.device
@@ -76,12 +77,12 @@ def prosody_launch(pcm: torch.Tensor, sample_offsets: torch.Tensor, lengths, sam
     for t in (state_in, state_out):
         if t is not None:
             assert t.is_cuda and t.dtype == torch.float32 and t.numel() == B * YIN_BUF
-    nat.call("janus_prosody_analyze", pcm.data_ptr(), sample_offsets.data_ptr(), hop_off.data_ptr(),
+    nat.call("janus_prosody_analyze_ex", pcm.data_ptr(), sample_offsets.data_ptr(), hop_off.data_ptr(),
              B, total, int(sample_rate), int(hop), float(tolerance), float(silence_db),
              state_in.data_ptr() if state_in is not None else None,
              state_out.data_ptr() if state_out is not None else None,
              f0.data_ptr(), rms.data_ptr(), mean_f0.data_ptr(), n_voiced.data_ptr(),
-             nat.stream_ptr(dev))
+             int(max_blocks), nat.stream_ptr(dev))
     return ProsodyResult(f0[:total], rms[:B], mean_f0[:B], n_voiced[:B], ho_np)
 
 

@@ -100,3 +100,18 @@ def test_per_hop_call_api(gpu):
     got = [ex.pitch_detector(np.pad(x[i:i + 512], (0, max(0, i + 512 - len(x)))))[0]
            for i in range(0, len(x), 512)]
     assert np.array_equal(np.array(got, np.float32), ref)
+
+
+@pytest.mark.parametrize("max_blocks", [1, 7, 256])
+def test_grid_cap_identical(gpu, max_blocks):
+    """janus_prosody_analyze_ex with a capped grid (the pipeline's prosody-beside-decoder
+    launch) gives per-hop f0 bit-identical to one block per hop."""
+    bufs = [synth_speech(900 + k, 0.7 + 0.3 * k) for k in range(4)]
+    lengths = [len(b) for b in bufs]
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(gpu)
+    pcm = torch.from_numpy(np.concatenate(bufs + [np.zeros(1, np.float32)])).to(gpu)
+    a = prosody_launch(pcm, offs, lengths, 48000, 512)
+    b = prosody_launch(pcm, offs, lengths, 48000, 512, max_blocks=max_blocks)
+    torch.cuda.synchronize()
+    assert np.array_equal(a.f0.cpu().numpy().view(np.uint32), b.f0.cpu().numpy().view(np.uint32))
+    assert a.tags() == b.tags()
