@@ -179,7 +179,6 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   constexpr bool LNA = AM == AM_LNA, LNX = AM == AM_LNX;
   constexpr int G = LNA ? 1 : 2;  // k-steps in flight per wave (128-VGPR budget at 1024 threads)
   extern __shared__ __attribute__((aligned(16))) _Float16 sk_smem[];  // LNX: [16*MTB][AP]
-  static_assert(!LNA || MTB == 4, "LayerNorm-on-load needs all rows per block");
   __shared__ float red[8][16 * MTB][17];
   __shared__ float s_mean[64], s_rstd[64];
   const int M = p.M, N = p.N, K = p.K;
@@ -244,19 +243,20 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
 
   if constexpr (LNA) {
     // row statistics from the producer's pieces: waves 0-3, thread = (row, quarter)
-    if (tid < 256) {
-      const int r = tid >> 2, qd = tid & 3, np = K / 16;
+    if (tid < 64 * MTB) {
+      const int r = tid >> 2, qd = tid & 3, np = K / 16;  // r: local row
+      const int gr = r0 + r;
       constexpr int NPQ = 12;  // pieces per thread held in registers (K <= 768)
       float2 pc[NPQ];
       float sm = 0.f;
 #pragma unroll
       for (int j = 0; j < NPQ; ++j) {
         const int g = qd + 4 * j;
-        pc[j] = (r < M && g < np) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+        pc[j] = (gr < M && g < np) ? p.part[(int64_t)gr * np + g] : make_float2(0.f, 0.f);
       }
 #pragma unroll
       for (int j = 0; j < NPQ; ++j) sm += pc[j].x;
-      for (int g = qd + 4 * NPQ; g < np; g += 4) sm += (r < M) ? p.part[(int64_t)r * np + g].x : 0.f;
+      for (int g = qd + 4 * NPQ; g < np; g += 4) sm += (gr < M) ? p.part[(int64_t)gr * np + g].x : 0.f;
       sm += __shfl_xor(sm, 1);
       sm += __shfl_xor(sm, 2);
       const float mean = sm / K;
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
         }
       }
       for (int g = qd + 4 * NPQ; g < np; g += 4) {
-        const float2 q = (r < M) ? p.part[(int64_t)r * np + g] : make_float2(0.f, 0.f);
+        const float2 q = (gr < M) ? p.part[(int64_t)gr * np + g] : make_float2(0.f, 0.f);
         const float dm = q.x * (1.0f / 16.0f) - mean;
         m2 += q.y + 16.0f * dm * dm;
       }
@@ -301,14 +301,14 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
           be[0] = b0.x; be[1] = b0.y; be[2] = b0.z; be[3] = b0.w; be[4] = b1.x; be[5] = b1.y; be[6] = b1.z; be[7] = b1.w;
         }
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < MTB; ++m) {
           const int r = m * 16 + lr;
           const float mean = s_mean[r], rstd = s_rstd[r];
           const float xv[8] = {ax[g][m][0].x, ax[g][m][0].y, ax[g][m][0].z, ax[g][m][0].w,
                                ax[g][m][1].x, ax[g][m][1].y, ax[g][m][1].z, ax[g][m][1].w};
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            af[m][j] = (ok && r < M) ? (_Float16)((xv[j] - mean) * rstd * ga[j] + be[j]) : (_Float16)0.0f;
+            af[m][j] = (ok && r0 + r < M) ? (_Float16)((xv[j] - mean) * rstd * ga[j] + be[j]) : (_Float16)0.0f;
         }
       } else if constexpr (LNX) {
         const bool ok = kk < kend;
@@ -439,9 +439,7 @@ static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
     const char* e = std::getenv("JANUS_SKINNY_MSPLIT_N");
     return e ? std::atoi(e) : 2048;
   }();
-  if constexpr (AM != AM_LNA) {
-    if (p.N <= msplit_n && p.ln_part == nullptr) { launch_skinny_m<AM, 1>(epi, p, s); return; }
-  }
+  if (p.N <= msplit_n) { launch_skinny_m<AM, 1>(epi, p, s); return; }
   launch_skinny_m<AM, 4>(epi, p, s);
 }
 
