@@ -88,6 +88,19 @@ int janus_cross_attention_f16(const uint16_t* qk, const uint16_t* enc, int batch
                               int H, int nsplit, float* part_c, float* part_ml, uint16_t* out,
                               void* stream);
 
+/* Decoder self-attention, one query per (utterance, head) against a KV cache:
+ *   out[b][h*64:(h+1)*64] = softmax(q_h . K_h[0:Tkv]^T * scale) . V_h[0:Tkv]
+ * q fp16 rows of stride q_bs; k/v fp16 [B][>=Tkv][H*64] with batch stride kv_bs and row
+ * stride kv_rs (elements); out fp16 rows of stride o_bs. Tkv <= 512 runs one block per
+ * (head, utterance); longer caches split keys over blocks with scratch part_o f32
+ * [B][ceil(Tkv/64)][H*64] and part_ml f32 [B][ceil(Tkv/64)][H][2] (may be NULL when
+ * Tkv <= 512). The per-step self-attention of the greedy decoder (transcriber.py:53-57
+ * -> model.transcribe, CTranslate2 decoder with KV cache). */
+int janus_decode_attention_f16(const uint16_t* q, int64_t q_bs, const uint16_t* k,
+                               const uint16_t* v, int64_t kv_bs, int64_t kv_rs, int Tkv,
+                               uint16_t* out, int64_t o_bs, int batch, int H, float scale,
+                               float* part_o, float* part_ml, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

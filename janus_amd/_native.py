@@ -81,6 +81,8 @@ SIGNATURES = {
     "janus_resunit_pack": [_P, _P, _I32, _I32, _P],
     "janus_resunit_f16": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F32, _I32, _P],
     "janus_cross_attention_f16": [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P],
+    "janus_decode_attention_f16": [_P, _I64, _P, _P, _I64, _I64, _I32, _P, _I64, _I32, _I32, _F32,
+                                   _P, _P, _P],
 }
 RESTYPES = {"janus_conv1d_packed_size": ctypes.c_int64}
 

@@ -398,6 +398,108 @@ __global__ __launch_bounds__(512) void decode_combine_reg_kernel(const float* __
   out[(int64_t)b * o_bs + i] = (_Float16)(o / l);
 }
 
+// -------------------------------------------------------- per-head decode
+// Self-attention over a KV cache of at most kHeadKeys keys: one block per (head,
+// utterance), so the B*H blocks fill the chip without splitting keys and no combine
+// launch follows. A wave-instruction reads 8 keys x one head's 128-byte row segment
+// (lane l: key l>>3, dims 8(l&7)..+7); every K and V load of the wave is issued up front
+// (<= 8 + 8 x 16 B per lane). Each wave keeps its own (max, sum, P.V) and the 8 waves
+// merge through LDS at the end.
+constexpr int kHeadWaves = 8;
+constexpr int kHeadRounds = 8;                               // key groups per wave
+constexpr int kHeadKeys = 8 * kHeadWaves * kHeadRounds;      // 512
+
+__global__ __launch_bounds__(512) void decode_head_kernel(
+    const _Float16* __restrict__ q, int64_t q_bs, const _Float16* __restrict__ k,
+    const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv, float scale_log2,
+    _Float16* __restrict__ out, int64_t o_bs) {
+  __shared__ float wo[kHeadWaves][kHd];
+  __shared__ float wm[kHeadWaves], wl[kHeadWaves];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int kg = lane >> 3, dg = lane & 7;
+  float qv[8];
+  {
+    const uint4 u = *reinterpret_cast<const uint4*>(q + (int64_t)b * q_bs + h * kHd + dg * 8);
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = (float)h8[j] * scale_log2;
+  }
+  const _Float16* kb = k + (int64_t)b * kv_bs + h * kHd + dg * 8;
+  const _Float16* vb = v + (int64_t)b * kv_bs + h * kHd + dg * 8;
+  // key of round i: 8 (i * kHeadWaves + w) + kg; rows past the cache clamp to its last
+  // row (finite values, weight 0) so every load is unconditional
+  const int tl = Tkv - 1;
+  uint4 kr[kHeadRounds], vr[kHeadRounds];
+#pragma unroll
+  for (int i = 0; i < kHeadRounds; ++i) {
+    const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
+    kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs);
+  }
+#pragma unroll
+  for (int i = 0; i < kHeadRounds; ++i) {
+    const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
+    vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs);
+  }
+  float sc[kHeadRounds];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kHeadRounds; ++i) {
+    const _Float16* h8 = reinterpret_cast<const _Float16*>(&kr[i]);
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dot += (float)h8[j] * qv[j];
+    dot += __shfl_xor(dot, 1);
+    dot += __shfl_xor(dot, 2);
+    dot += __shfl_xor(dot, 4);
+    const bool ok = 8 * (i * kHeadWaves + w) + kg < Tkv;
+    sc[i] = ok ? dot : -INFINITY;
+    m = fmaxf(m, sc[i]);
+  }
+  m = fmaxf(m, __shfl_xor(m, 8));
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float l = 0.f, a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  if (m != -INFINITY) {  // wave-uniform: this wave holds at least one key
+#pragma unroll
+    for (int i = 0; i < kHeadRounds; ++i) {
+      const float p = exp2f(sc[i] - m);  // -inf -> 0
+      l += p;
+      const _Float16* h8 = reinterpret_cast<const _Float16*>(&vr[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += p * (float)h8[j];
+    }
+  }
+  // sum over the 8 key groups (lanes sharing dg); l is replicated over dg
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    l += __shfl_xor(l, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += __shfl_xor(a[j], o);
+  }
+  if (kg == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wo[w][dg * 8 + j] = a[j];
+  }
+  if (lane == 0) { wm[w] = m; wl[w] = l; }
+  __syncthreads();
+  if (threadIdx.x < kHd) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < kHeadWaves; ++i) M = fmaxf(M, wm[i]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int i = 0; i < kHeadWaves; ++i) {
+      const float f = exp2f(wm[i] - M);  // empty wave: -inf -> 0
+      L += wl[i] * f;
+      O += wo[i][threadIdx.x] * f;
+    }
+    out[(int64_t)b * o_bs + h * kHd + threadIdx.x] = (_Float16)(O / L);
+  }
+}
+
 int decode_split_count(int Tkv) {
   int n = (Tkv + kSplitKeys - 1) / kSplitKeys;
   return n < 1 ? 1 : n;
@@ -409,9 +511,17 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
                                    float* part_o, float* part_ml, hipStream_t s) {
   JANUS_CHECK(H <= kMaxHeads, "split decode attention: at most 8 heads (d <= 512)");
   if (B <= 0 || Tkv <= 0) return;
+  static const bool force_split = std::getenv("JANUS_DEC_SPLIT") != nullptr;
+  if (Tkv <= kHeadKeys && (!force_split || part_o == nullptr)) {
+    decode_head_kernel<<<dim3(H, B), 64 * kHeadWaves, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv,
+                                                              scale * 1.4426950408889634f, out, o_bs);
+    JANUS_LAUNCH_CHECK();
+    return;
+  }
   const int nsplit = decode_split_count(Tkv);
   const int chunk = (Tkv + nsplit - 1) / nsplit;
   JANUS_CHECK(chunk <= kSplitKeys && nsplit <= 64, "split decode attention: too many keys");
+  JANUS_CHECK(part_o != nullptr && part_ml != nullptr, "split decode attention: scratch missing");
   decode_split_kernel<<<dim3(nsplit, B), 256, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, H, chunk,
                                                       scale * 1.4426950408889634f, part_o, part_ml);
   JANUS_LAUNCH_CHECK();

@@ -125,3 +125,18 @@ extern "C" int janus_cross_attention_f16(const uint16_t* qk, const uint16_t* enc
                  (hipStream_t)stream);
   });
 }
+
+extern "C" int janus_decode_attention_f16(const uint16_t* q, int64_t q_bs, const uint16_t* k,
+                                          const uint16_t* v, int64_t kv_bs, int64_t kv_rs,
+                                          int Tkv, uint16_t* out, int64_t o_bs, int batch, int H,
+                                          float scale, float* part_o, float* part_ml,
+                                          void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(Tkv <= 512 || (part_o && part_ml), "decode attention: scratch needed past 512 keys");
+    decode_attention_split_launch(reinterpret_cast<const _Float16*>(q), q_bs,
+                                  reinterpret_cast<const _Float16*>(k),
+                                  reinterpret_cast<const _Float16*>(v), kv_bs, kv_rs, Tkv,
+                                  reinterpret_cast<_Float16*>(out), o_bs, batch, H, scale, part_o,
+                                  part_ml, (hipStream_t)stream);
+  });
+}

@@ -225,6 +225,7 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
   }
 }
 
+
 // c[b][h*D + j] = sum_s 2^(m_s - M) C_s[h][j] / sum_s 2^(m_s - M) l_s   (fp16)
 __global__ __launch_bounds__(256) void xattn_combine_kernel(const float* __restrict__ part_c,
                                                             const float* __restrict__ part_ml,
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(128) void xattn_combine_wide_kernel(const float* __
 }
 
 int xattn_split_count(int Te, int requested) {
-  int n = requested > 0 ? requested : 12;  // 768 blocks at batch 64: 3 per CU
+  int n = requested > 0 ? requested : 8;  // 512 blocks at batch 64 (bench sweep: 8 < 6, 10, 12)
   n = std::min(n, 63);
   n = std::min(n, (Te + kXKeys - 1) / kXKeys);
   return std::max(n, 1);

@@ -196,3 +196,33 @@ def test_cross_attention_absorbed(gpu, B, Te, D, nsplit):
     torch.cuda.synchronize()
     err = rel_err(out, ref)
     assert err < 3e-3, err
+
+
+@pytest.mark.parametrize("B,T,H,split", [(3, 1, 8, 0), (2, 37, 6, 0), (64, 448, 8, 0), (2, 512, 8, 0),
+                                         (2, 700, 8, 1), (3, 130, 8, 1)])
+def test_decode_attention(gpu, B, T, H, split, monkeypatch):
+    """One query per (b, h) against a KV cache with row stride > d (the decoder's cache
+    layout [B][n_ctx][d]); per-head kernel (T <= 512) and the key-split + combine path."""
+    d, n_ctx = H * 64, max(T, 448) + 5
+    g = torch.Generator().manual_seed(B * 100 + T + H)
+    q = (torch.randn(B, 3 * d, generator=g)).half()          # q is the first d of a qkv row
+    k = (torch.randn(B, n_ctx, d, generator=g)).half()
+    v = (torch.randn(B, n_ctx, d, generator=g)).half()
+    qh = q[:, :d].double().view(B, H, 1, 64)
+    kh = k[:, :T].double().view(B, T, H, 64).transpose(1, 2)
+    vh = v[:, :T].double().view(B, T, H, 64).transpose(1, 2)
+    ref = (((qh @ kh.transpose(-1, -2)) * 0.125).softmax(-1) @ vh).reshape(B, d)
+    dq, dk, dv = q.to(gpu), k.to(gpu), v.to(gpu)
+    out = torch.empty(B, 2 * d, dtype=torch.float16, device=gpu)
+    ns = (T + 63) // 64
+    po = torch.empty(B * ns * d, dtype=torch.float32, device=gpu) if split or T > 512 else None
+    pm = torch.empty(B * ns * H * 2, dtype=torch.float32, device=gpu) if split or T > 512 else None
+    if split:
+        monkeypatch.setenv("JANUS_DEC_SPLIT", "1")  # read once per process: only affects T <= 512
+    nat.call("janus_decode_attention_f16", dq.data_ptr(), 3 * d, dk.data_ptr(), dv.data_ptr(),
+             n_ctx * d, d, T, out.data_ptr(), 2 * d, B, H, 0.125,
+             po.data_ptr() if po is not None else None, pm.data_ptr() if pm is not None else None,
+             stream())
+    torch.cuda.synchronize()
+    err = rel_err(out[:, :d], ref)
+    assert err < 2e-3, err

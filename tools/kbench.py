@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--units-only", action="store_true")
     ap.add_argument("--xattn", action="store_true")
     ap.add_argument("--wide", action="store_true")
+    ap.add_argument("--dec", action="store_true")
     a = ap.parse_args()
+    if a.dec:
+        dec_bench()
+        return
     if a.xattn:
         xattn_bench()
         return
@@ -168,31 +172,63 @@ def wide_units(B, reps):
               f"two convs {mp:7.3f} ms {flops / mp / 1e9:7.1f} TF/s", flush=True)
 
 
+def _time_cold(fn, reps, flush):
+    """Mean time of fn with the caches flushed (a 512 MB write) before every call."""
+    fn()
+    torch.cuda.synchronize()
+    tot = 0.0
+    for _ in range(reps):
+        flush.fill_(1.0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        tot += e0.elapsed_time(e1)
+    return tot / reps
+
+
 def xattn_bench(reps=20):
-    """Absorbed cross-attention at the bench shape (64 x 1500 x 512, 8 heads) per split count."""
+    """Absorbed cross-attention at the bench shape (64 x 1500 x 512, 8 heads) per split
+    count, caches flushed before every call (the decoder reads enc once per layer)."""
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
     B, Te, D, H = 64, 1500, 512, 8
     enc = torch.randn(B, Te, D, device=dev).half()
     qk = (torch.randn(B, H, D, device=dev) * 0.1).half()
     out = torch.empty(B, H * D, device=dev, dtype=torch.float16)
-    for ns in (4, 8, 12, 16, 24):
+    flush = torch.empty(128 << 20, device=dev)
+    for ns in (8, 12, 16, 24):
         pc = torch.empty(B * ns * H * D, device=dev)
         pml = torch.empty(B * ns * H * 2, device=dev)
 
         def run():
             nat.call("janus_cross_attention_f16", qk.data_ptr(), enc.data_ptr(), B, Te, D, H, ns,
                      pc.data_ptr(), pml.data_ptr(), out.data_ptr(), s)
-        run()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        print(f"xattn nsplit={ns:3d} {ms * 1000:8.1f} us  {B * Te * D * 2 / ms / 1e6:8.1f} GB/s (enc, L2/MALL-warm)",
+        ms = _time_cold(run, reps, flush)
+        print(f"xattn nsplit={ns:3d} {ms * 1000:8.1f} us  {B * Te * D * 2 / ms / 1e6:8.1f} GB/s (enc, cold)",
+              flush=True)
+
+
+def dec_bench(reps=20):
+    """Decoder self-attention (64 utterances, 8 heads, cache [64][448][512]) per cache length."""
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    B, H, NC = 64, 8, 448
+    d = H * 64
+    q = torch.randn(B, 3 * d, device=dev).half()
+    k = torch.randn(B, NC, d, device=dev).half()
+    v = torch.randn(B, NC, d, device=dev).half()
+    out = torch.empty(B, d, device=dev, dtype=torch.float16)
+    po = torch.empty(B * 8 * d, device=dev)
+    pm = torch.empty(B * 8 * H * 2, device=dev)
+    flush = torch.empty(128 << 20, device=dev)
+    for T in (16, 64, 224, 448):
+        def run():
+            nat.call("janus_decode_attention_f16", q.data_ptr(), 3 * d, k.data_ptr(), v.data_ptr(),
+                     NC * d, d, T, out.data_ptr(), d, B, H, 0.125, po.data_ptr(), pm.data_ptr(), s)
+        ms = _time_cold(run, reps, flush)
+        print(f"self-attn T={T:4d} {ms * 1000:8.1f} us  {B * T * d * 4 / ms / 1e6:8.1f} GB/s (K+V, cold)",
               flush=True)
 
 
