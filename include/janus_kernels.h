@@ -31,6 +31,14 @@ int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, i
                    int N, int K, void* stream);
 
 /* LayerNorm rows of an fp32 [rows][d] tensor into fp16 (eps as given). */
+/* C = epilogue(LayerNorm(x) W^T + bias) for M <= 64 rows: the LayerNorm of each block's
+ * rows (fp32 x, row stride ldx; gamma/beta f32 [K]; two-pass fp32 statistics) is computed in
+ * the GEMM's prologue instead of a separate janus_layernorm_f16 launch. K <= 512, K % 4 == 0;
+ * epi one of EPI_F16 / EPI_GELU_F16. The decoder's pre-LN projections (transcriber.py:53-57
+ * -> Whisper decoder layers). */
+int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const float* gamma, const float* beta,
+                      float eps, const uint16_t* W, int64_t ldw, const float* bias, void* C,
+                      int64_t ldc, int M, int N, int K, void* stream);
 int janus_layernorm_f16(const float* x, const float* gamma, const float* beta, uint16_t* out,
                         int rows, int d, float eps, void* stream);
 

@@ -343,10 +343,9 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
   RowRules* sR = reinterpret_cast<RowRules*>(sT + kLgWaves * 64 * 17);  // [64]
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   if (lnx) {  // A = the decoder's final LayerNorm of x, computed here (one wave per row)
-    for (int r = w; r < 64; r += kLgWaves) {
-      if (r < B) ln_row_wave<false>(lnx + (int64_t)r * ldx, ln_g, ln_b, sA + r * AP, K, 1e-5f, lane);
-      else for (int c = lane; c < K; c += 64) sA[r * AP + c] = (_Float16)0.0f;
-    }
+    // wave w: rows w + 8j (j < 8), all loads up front
+    ln_rows_wave<(K + 255) / 256, 64 / kLgWaves>(lnx, ldx, w, kLgWaves, B, ln_g, ln_b, sA, w, AP, K,
+                                                 1e-5f, lane);
   } else {
     for (int i = tid; i < 64 * (K / 8); i += kLgWaves * 64) {
       const int r = i / (K / 8), c8 = (i % (K / 8)) * 8;

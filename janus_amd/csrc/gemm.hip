@@ -177,7 +177,9 @@ constexpr int kSkWaves = 16;
 template <int EPI, int AM, int MTB>
 __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   constexpr bool LNA = AM == AM_LNA, LNX = AM == AM_LNX;
-  constexpr int G = LNA ? 1 : 2;  // k-steps in flight per wave (128-VGPR budget at 1024 threads)
+  // k-steps in flight per wave (128-VGPR budget at 1024 threads; the LayerNorm modes run
+  // K <= 512, one k-step per wave)
+  constexpr int G = (LNA || LNX) ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) _Float16 sk_smem[];  // LNX: [16*MTB][AP]
   __shared__ float red[8][16 * MTB][17];
   __shared__ float s_mean[64], s_rstd[64];
@@ -228,16 +230,9 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   load(kbeg);
 
   if constexpr (LNX) {
-    // this block's rows of LN(x) -> fp16 LDS tile, one wave per row (weights in flight)
-    for (int r = w; r < 16 * MTB; r += kSkWaves) {
-      const int gr = r0 + r;
-      if (gr < M) {
-        ln_row_wave<false>(p.x + (int64_t)gr * p.ldx, p.lnin_g, p.lnin_b, sk_smem + r * AP, K,
-                           p.eps, lane);
-      } else {
-        for (int c = lane; c < K; c += 64) sk_smem[r * AP + c] = (_Float16)0.0f;
-      }
-    }
+    // this block's rows of LN(x) -> fp16 LDS tile: wave w normalises rows w + 16j (j < MTB),
+    // all loads in one round trip behind the weights already in flight
+    ln_rows_wave<2, MTB>(p.x, p.ldx, r0 + w, kSkWaves, M, p.lnin_g, p.lnin_b, sk_smem, w, AP, K, p.eps, lane);
     __syncthreads();
   }
 
@@ -451,7 +446,8 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.ln_part = g.ln_part;
   p.a_group_cols = g.a_group_cols;
   p.ln_g = g.ln_g; p.ln_b = g.ln_b; p.ln_eps = g.ln_eps; p.ln_out = g.ln_out; p.ln_cnt = g.ln_cnt;
-  if (g.lnin_x) {  // A = LayerNorm(x) in the block's prologue
+  if (g.lnin_x) {  // A = LayerNorm(x) in the block's prologue (K <= 512)
+    JANUS_CHECK(g.K <= 512 && g.K % 4 == 0, "skinny LayerNorm prologue: K <= 512, K % 4 == 0");
     p.x = g.lnin_x; p.ldx = g.lnin_ldx; p.lnin_g = g.lnin_g; p.lnin_b = g.lnin_b; p.eps = g.lnin_eps;
     launch_skinny_t<AM_LNX>(epi, p, s);
     return;
@@ -483,9 +479,9 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(!p.lnin_x || (p.M <= 64 && p.K <= 1024 && p.K % 32 == 0 && p.a_group_cols == 0 &&
                             p.lnin_g && p.lnin_b && epi != EPI_RESID_F32 && epi != EPI_F32),
               "gemm: LayerNorm-prologue A needs M <= 64, K <= 1024 (multiple of 32), no groups");
-  JANUS_CHECK(!p.ln_out || (epi == EPI_RESID_F32 && p.M <= 64 && p.N <= 1024 && p.ln_cnt &&
+  JANUS_CHECK(!p.ln_out || (epi == EPI_RESID_F32 && p.M <= 64 && p.N <= 512 && p.N % 4 == 0 && p.ln_cnt &&
                             p.ln_g && p.ln_b && p.ldc == p.N),
-              "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 1024, ldc == N");
+              "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 512, ldc == N");
   if (p.M <= 64) launch_skinny(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }

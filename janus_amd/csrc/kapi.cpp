@@ -48,6 +48,21 @@ extern "C" int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uin
   });
 }
 
+extern "C" int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const float* gamma,
+                                 const float* beta, float eps, const uint16_t* W, int64_t ldw,
+                                 const float* bias, void* C, int64_t ldc, int M, int N, int K,
+                                 void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(M <= 64 && K <= 512 && K % 32 == 0, "gemm_ln: M <= 64, K <= 512 (multiple of 32)");
+    GemmArgs g;
+    g.A = nullptr; g.lda = K; g.R = nullptr; g.ldr = 0;
+    g.W = reinterpret_cast<const _Float16*>(W); g.ldw = ldw;
+    g.bias = bias; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
+    g.lnin_x = x; g.lnin_ldx = ldx; g.lnin_g = gamma; g.lnin_b = beta; g.lnin_eps = eps;
+    gemm_launch(epi, g, (hipStream_t)stream);
+  });
+}
+
 extern "C" int janus_layernorm_f16(const float* x, const float* gamma, const float* beta,
                                    uint16_t* out, int rows, int d, float eps, void* stream) {
   return guarded([&] {

@@ -62,6 +62,81 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// LayerNorm of R fp32 rows by one wave (rows row0 + j*rstep, j < R; d <= 256*MAXV, d % 4
+// == 0): every row, gamma and beta load is issued before the first use (one memory round
+// trip for all R rows); fp16 out rows at out + (lrow0 + j*rstep)*ldo, ALL R of them written
+// (rows >= nrows as zeros: out must hold R rows, e.g. an LDS tile).
+// Two-pass mean / variance in fp32 as layernorm_kernel. MAXV sized to d keeps the register
+// footprint small enough not to cost the caller occupancy; the loads are unconditional
+// (clamped index) — guarded vector loads are split into branchy dword loads by the
+// compiler, which measured 3x slower in the GEMM prologue.
+template <int MAXV, int R>
+__device__ __forceinline__ void ln_rows_wave(const float* x, int64_t ldx, int row0, int rstep,
+                                             int nrows, const float* __restrict__ g,
+                                             const float* __restrict__ b, _Float16* out,
+                                             int lrow0, int ldo, int d, float eps, int lane) {
+  const int nv = d >> 2;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4 v[R][MAXV], gg[MAXV], bb[MAXV];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int r = row0 + j * rstep;
+    const float4* x4 = reinterpret_cast<const float4*>(x + (int64_t)min(r, nrows - 1) * ldx);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int i = lane + 64 * k;
+      // unconditional 16-byte loads (clamped index; values past d are masked below)
+      v[j][k] = x4[min(i, nv - 1)];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int i = min(lane + 64 * k, nv - 1);
+    gg[k] = g4[i];
+    bb[k] = b4[i];
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+      if (lane + 64 * k >= nv) v[j][k] = z;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) s += (v[j][k].x + v[j][k].y) + (v[j][k].z + v[j][k].w);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / d;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      if (lane + 64 * k < nv) {
+        const float a0 = v[j][k].x - mean, a1 = v[j][k].y - mean, a2 = v[j][k].z - mean,
+                    a3 = v[j][k].w - mean;
+        q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = rsqrtf(q / d + eps);
+    const bool rok = row0 + j * rstep < nrows;
+    _Float16* orow = out + (int64_t)(lrow0 + j * rstep) * ldo;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int i = lane + 64 * k;
+      if (i < nv) {
+        half4 h = {(_Float16)((v[j][k].x - mean) * rstd * gg[k].x + bb[k].x),
+                   (_Float16)((v[j][k].y - mean) * rstd * gg[k].y + bb[k].y),
+                   (_Float16)((v[j][k].z - mean) * rstd * gg[k].z + bb[k].z),
+                   (_Float16)((v[j][k].w - mean) * rstd * gg[k].w + bb[k].w)};
+        if (!rok) h = half4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+        *reinterpret_cast<half4*>(orow + 4 * i) = h;
+      }
+    }
+  }
+}
+
 // LayerNorm of one fp32 row of d <= 1024 columns by one wave (two-pass mean / variance
 // in fp32, as layernorm_kernel), fp16 out. SC1: read the row with agent-scope relaxed
 // (sc1) loads — for rows other workgroups of the same launch have just stored sc1.
@@ -69,33 +144,33 @@ template <bool SC1>
 __device__ __forceinline__ void ln_row_wave(const float* xr, const float* __restrict__ g,
                                             const float* __restrict__ b, _Float16* out, int d,
                                             float eps, int lane) {
-  float v[16];
-  float s = 0.f;
+  if constexpr (SC1) {
+    float v[16];
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = lane + 64 * i;
-    float t = 0.f;
-    if (c < d) {
-      if constexpr (SC1) t = __hip_atomic_load(xr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else t = xr[c];
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      const float t = c < d ? __hip_atomic_load(xr + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      v[i] = t;
+      s += t;
     }
-    v[i] = t;
-    s += t;
-  }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float mean = s / d;
-  float q = 0.f;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / d;
+    float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = lane + 64 * i;
-    if (c < d) q += (v[i] - mean) * (v[i] - mean);
-  }
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
-  const float rstd = rsqrtf(q / d + eps);
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      if (c < d) q += (v[i] - mean) * (v[i] - mean);
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = rsqrtf(q / d + eps);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = lane + 64 * i;
-    if (c < d) out[c] = (_Float16)((v[i] - mean) * rstd * g[c] + b[c]);
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      if (c < d) out[c] = (_Float16)((v[i] - mean) * rstd * g[c] + b[c]);
+    }
+  } else {
+    ln_rows_wave<4, 1>(xr, 0, 0, 1, 1, g, b, out, 0, 0, d, eps, lane);
   }
 }
 

@@ -328,10 +328,10 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const ja
   const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && std::getenv("JANUS_LN_FUSE") != nullptr;
   // JANUS_LN_PROLOGUE (opt-in, B <= 64): every pre-LN projection computes LayerNorm(x)
   // for its rows in the block prologue (GemmArgs::lnin_x), the vocabulary projection the
-  // final LayerNorm — no LayerNorm launches. Measured slower than the separate launches
-  // (503.9 vs 483.8 ms per bench step): every block re-reads its x rows in fp32 and runs
-  // the row reductions ahead of its MFMAs.
-  const bool ln_pro = B <= 64 && !fused_ln && !ln_fuse && std::getenv("JANUS_LN_PROLOGUE") != nullptr;
+  // final LayerNorm — no LayerNorm launches. Measured level with the separate launches
+  // (432.7 / 434.7 vs 435.9 / 434.6 ms per bench step, unconditional 16-byte prologue
+  // loads): the prologue's round trip and row reductions cost what the launch saves.
+  const bool ln_pro = B <= 64 && d <= 512 && !fused_ln && !ln_fuse && std::getenv("JANUS_LN_PROLOGUE") != nullptr;
   auto with_ln = [&](GemmArgs g, const float* lg, const float* lb) {
     if (ln_pro) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
     return g;

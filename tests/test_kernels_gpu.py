@@ -226,3 +226,25 @@ def test_decode_attention(gpu, B, T, H, split, monkeypatch):
     torch.cuda.synchronize()
     err = rel_err(out[:, :d], ref)
     assert err < 2e-3, err
+
+
+@pytest.mark.parametrize("M,N,epi", [(64, 1536, 0), (64, 4096, 0), (37, 2048, 1), (5, 512, 0)])
+def test_gemm_layernorm_prologue(gpu, M, N, epi):
+    """epilogue(LayerNorm(x) W^T + b) with the LayerNorm in the GEMM prologue vs float64."""
+    K = 512
+    g = torch.Generator().manual_seed(M + N + epi)
+    x = torch.randn(M, K, generator=g) * 2.0 + 0.5
+    gam = torch.randn(K, generator=g) * 0.2 + 1.0
+    bet = torch.randn(K, generator=g) * 0.1
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).half()
+    bias = torch.randn(N, generator=g) * 0.1
+    xn = F.layer_norm(x.double(), (K,), gam.double(), bet.double(), 1e-5)
+    ref = xn.half().double() @ W.double().T + bias.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    out = torch.empty(M, N, dtype=torch.float16, device=gpu)
+    dx, dg, db, dW, dbias = x.to(gpu), gam.to(gpu), bet.to(gpu), W.to(gpu), bias.to(gpu)
+    nat.call("janus_gemm_ln_f16", epi, dx.data_ptr(), K, dg.data_ptr(), db.data_ptr(), 1e-5,
+             dW.data_ptr(), K, dbias.data_ptr(), out.data_ptr(), N, M, N, K, stream())
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 2e-3

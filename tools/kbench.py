@@ -36,7 +36,11 @@ def main():
     ap.add_argument("--xattn", action="store_true")
     ap.add_argument("--wide", action="store_true")
     ap.add_argument("--dec", action="store_true")
+    ap.add_argument("--lngemm", action="store_true")
     a = ap.parse_args()
+    if a.lngemm:
+        lngemm_bench()
+        return
     if a.dec:
         dec_bench()
         return
@@ -230,6 +234,42 @@ def dec_bench(reps=20):
         ms = _time_cold(run, reps, flush)
         print(f"self-attn T={T:4d} {ms * 1000:8.1f} us  {B * T * d * 4 / ms / 1e6:8.1f} GB/s (K+V, cold)",
               flush=True)
+
+
+def lngemm_bench(reps=50):
+    """Decoder pre-LN projection, M = 64, K = 512: LayerNorm launch + skinny GEMM vs the GEMM
+    with the LayerNorm in its prologue; warm (back to back) and with x rewritten by a kernel
+    just before (as the residual GEMM does in the decoder)."""
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    M, K = 64, 512
+    x = torch.randn(M, K, device=dev)
+    g = torch.ones(K, device=dev)
+    b = torch.zeros(K, device=dev)
+    a = torch.empty(M, K, device=dev, dtype=torch.float16)
+    for N in (1536, 2048, 4096):
+        W = (torch.randn(N, K, device=dev) * 0.04).half()
+        out = torch.empty(M, N, device=dev, dtype=torch.float16)
+
+        def sep():
+            nat.call("janus_layernorm_f16", x.data_ptr(), g.data_ptr(), b.data_ptr(), a.data_ptr(), M, K,
+                     1e-5, s)
+            nat.call("janus_gemm_f16", 0, a.data_ptr(), K, W.data_ptr(), K, None, out.data_ptr(), N, None, 0,
+                     M, N, K, s)
+
+        def fused():
+            nat.call("janus_gemm_ln_f16", 0, x.data_ptr(), K, g.data_ptr(), b.data_ptr(), 1e-5, W.data_ptr(),
+                     K, None, out.data_ptr(), N, M, N, K, s)
+
+        def touch(fn):
+            def run():
+                x.add_(0.0)
+                fn()
+            return run
+        t = [_time(f, reps) * 1000 for f in (sep, fused, touch(sep), touch(fused))]
+        tx = _time(lambda: x.add_(0.0), reps) * 1000
+        print(f"N={N:5d} LN+GEMM {t[0]:6.1f} us  fused {t[1]:6.1f} us | after a write of x: "
+              f"LN+GEMM {t[2] - tx:6.1f} us  fused {t[3] - tx:6.1f} us (write {tx:.1f} us)", flush=True)
 
 
 if __name__ == "__main__":
