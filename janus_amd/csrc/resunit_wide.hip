@@ -171,9 +171,10 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
       const int idx = tid + i * NT;
       const int r = idx / CPR, cc = idx % CPR;
       const int t = xbase + r;
-      pf[i] = (r < R0 && t >= 0 && t < T)
-                  ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * C + cc * 8)
-                  : make_uint4(0, 0, 0, 0);
+      // unconditional load of a clamped row, zeroed below (no branch per load)
+      const int tc = min(max(t, 0), T - 1);
+      pf[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)tc * C + cc * 8);
+      if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < G::NLD; ++i) {
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
         for (int rr = 0; rr < 4; ++rr) {
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
-          const float v = (r < R1 && t >= 0 && t < T) ? silu(acc[j][n][rr] + bias) : 0.0f;
+          // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
+          const float v = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
           sS[r * LI + co] = (_Float16)v;
         }
       }
@@ -395,9 +397,10 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
       const int idx = tid + i * NT;
       const int r = idx / CPR, cc = idx % CPR;
       const int t = xbase + r;
-      pf[i] = (r < R0 && t >= 0 && t < T)
-                  ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * C + cc * 8)
-                  : make_uint4(0, 0, 0, 0);
+      // unconditional load of a clamped row, zeroed below (no branch per load)
+      const int tc = min(max(t, 0), T - 1);
+      pf[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)tc * C + cc * 8);
+      if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
     WIDE_WLOAD(rwA0, rwA1, a.w1, 0);
     WIDE_WLOAD(rwB0, rwB1, a.w1, 1);
@@ -487,7 +490,8 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
         for (int rr = 0; rr < 4; ++rr) {
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
-          const float v = (r < R1 && t >= 0 && t < T) ? silu(acc[j][n][rr] + bias) : 0.0f;
+          // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
+          const float v = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
           sS[r * LI + co] = (_Float16)v;
         }
       }

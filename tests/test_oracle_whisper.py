@@ -96,3 +96,17 @@ def test_segments_and_transcript():
     assert [s[2] for s in segs] == [" hello world", " again"]
     assert tk.transcript(seq) == "hello world again"
     assert tk.transcript([tk.eot]) == ""
+
+
+def test_transcript_fast_path_matches_segments():
+    """The numpy transcript of the table vocabulary equals ' '.join(segment texts)."""
+    from janus_amd.tokenizer import load_tokenizer
+    tk = load_tokenizer()
+    rng = np.random.default_rng(7)
+    tb = tk.timestamp_begin
+    rows = [rng.integers(0, 51864, size=447), rng.integers(tb - 3, 51864, size=300),
+            np.concatenate([rng.integers(0, 1000, size=40), [tk.eot], rng.integers(0, 1000, size=9)]),
+            [], [tb], [tb, tb + 3], [5, tb + 1], [tb, 7, tb + 2, tb + 5, 9, 10], [-1, 5]]
+    for r in rows:
+        ref = " ".join(t.strip() for (_, _, t) in tk.segments(r)).strip()
+        assert tk.transcript(r) == ref
