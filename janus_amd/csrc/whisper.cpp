@@ -44,7 +44,7 @@ struct janus_whisper {
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
       d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt,
-      d_xqk, d_xc, d_xpc, d_xpml;
+      d_xqk, d_xc, d_xpc, d_xpml, d_enc;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t side = nullptr;  // graph capture needs a non-null stream
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -220,11 +220,18 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
                    w->params.get("encoder.layer_norm.bias", d), out, (int)M, d, 1e-5f, s);
 }
 
-static void decode_greedy(janus_whisper* w, const _Float16* enc, int B, const janus_decode_options* opt,
+static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const janus_decode_options* opt,
                           int32_t* tokens_out, int32_t* n_tokens_out, float* sum_lp_out,
                           hipStream_t s) {
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
+  // the captured decode graphs bake in every pointer they read: the encoder output goes
+  // to a context-owned buffer first (one ~0.1 ms device copy) so the graphs are reused
+  // whatever buffer the caller's allocator handed out this time
+  w->d_enc.ensure(sizeof(_Float16) * (int64_t)B * Te * d);
+  JANUS_HIP(hipMemcpyAsync(w->d_enc.p, enc_in, sizeof(_Float16) * (int64_t)B * Te * d,
+                           hipMemcpyDeviceToDevice, s));
+  const _Float16* enc = w->d_enc.as<_Float16>();
   const int maxlen = opt->max_length;
   JANUS_CHECK(opt->prompt_len >= 1 && opt->prompt_len < maxlen && maxlen <= NC,
               "decode: need 1 <= prompt_len < max_length <= n_text_ctx");
