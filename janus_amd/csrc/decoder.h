@@ -51,8 +51,9 @@ void select_launch(const float* logits, int V, const DecodeRules& R, const uint8
                    float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
 void rules_init_launch(RowRules* rules, int B, hipStream_t s);
 // logits = A[B][K] . W[V][K]^T computed block-wise with the filtered statistics reduced
-// in the epilogue (no logits in HBM); nblk = ceil(V/16) partials per row.
-int logits_partial_blocks(int V);
+// in the epilogue (no logits in HBM); nblk = logits_partial_blocks(V) merged partials per row
+// (one per block of the launch).
+int logits_partial_blocks(int V, int K);
 // lnx: A = LayerNorm(lnx) (fp32 [B][K], eps 1e-5) computed in-block instead of read
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,

@@ -144,9 +144,18 @@ void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen
 }
 
 // ------------------------------------------------------------------ select
+// the rules past the suppress mask, for a token whose mask byte is already in a register
+__device__ __forceinline__ bool allowed_unmasked(int t, const DecodeRules& R, const RowRules& rr,
+                                                 bool ban_all_text);
+
 __device__ __forceinline__ bool allowed(int t, const uint8_t* smask, const DecodeRules& R,
                                         const RowRules& rr, bool ban_all_text) {
   if (smask[t]) return false;
+  return allowed_unmasked(t, R, rr, ban_all_text);
+}
+
+__device__ __forceinline__ bool allowed_unmasked(int t, const DecodeRules& R, const RowRules& rr,
+                                                 bool ban_all_text) {
   if (rr.sample_begin && R.suppress_blank && (t == R.blank || t == R.eot)) return false;
   if (R.ts_begin >= 0) {
     if (t == R.no_timestamps) return false;
@@ -314,34 +323,56 @@ void rules_init_launch(RowRules* rules, int B, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
-int logits_partial_blocks(int V) { return (V + 15) / 16; }
+// one merged partial per (row, block): the grid of logits_partial_kernel
+// waves per logits block (16 waves — about one tile per wave — measured 4x slower:
+// 114.7 vs 28.8 us per launch)
+constexpr int lg_waves(int /*K*/) { return 8; }
+int logits_partial_blocks(int V, int K) {
+  return std::min(256, ((V + 15) / 16 + lg_waves(K) - 1) / lg_waves(K));
+}
+
+__device__ __forceinline__ float lse_merge(float m1, float s1, float m2, float s2, float* mo) {
+  const float m = fmaxf(m1, m2);
+  *mo = m;
+  if (m == -INFINITY) return 0.f;
+  return s1 * __expf(m1 - m) + s2 * __expf(m2 - m);
+}
 
 __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
   return v > bv || (v == bv && i < bi);
 }
 
-// Vocabulary projection + rule-filtered statistics, per (row, 16-column tile):
-// logits = A[B<=64][K] . W[V][K]^T (W = the token embedding, tied). The 53 MB weight read
-// once per step is the cost: each block stages A (all rows) in LDS once, then its 8 waves
-// walk 16-column tiles independently — every tile's weight fragments (K/32 x 16 B per
-// lane) are issued before its MFMAs, so each wave keeps 16 KB of weights in flight — and
-// the tile's 64 x 16 logits go through a wave-private LDS patch so lane = row reduces its
-// 16 columns (rule filter, maxima, partition sums, argmaxes) without shuffles.
-constexpr int kLgWaves = 8;
+// Vocabulary projection + rule-filtered statistics: logits = A[B<=64][K] . W[V][K]^T
+// (W = the token embedding, tied). The 53 MB weight read once per step is the cost: each
+// block stages A (all rows) in LDS once, then its 8 waves walk 16-column tiles
+// independently with the next tile's weight fragments (K/32 x 16 B per lane) and its 16
+// suppress-mask bytes in flight during the current tile's epilogue (the first tile's
+// during the A staging). A tile's 64 x 16 logits go through a wave-private LDS patch so
+// lane = row folds its 16 columns (rule filter, maxima, partition sums, argmaxes) into
+// running per-row statistics without shuffles; at the end the 8 waves' statistics are
+// merged per row (wave order) into ONE partial per (row, block) for the selector.
 
 template <int NKS>  // K / 32
-__global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
+__global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
     LogitPart* __restrict__ parts, int ntiles, const float* __restrict__ lnx, int ldx,
     const float* __restrict__ ln_g, const float* __restrict__ ln_b) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   constexpr int K = NKS * 32;
+  constexpr int kLgWaves = lg_waves(K);
   constexpr int AP = K + 16;  // row pitch (halves): 16*AP bytes with AP/8 % 4 == 2 -> conflict-free
   _Float16* sA = lg_smem;                                            // [64][AP]
   float* sT = reinterpret_cast<float*>(sA + 64 * AP);                // [waves][64][17]
   RowRules* sR = reinterpret_cast<RowRules*>(sT + kLgWaves * 64 * 17);  // [64]
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  // the first tile's weights and suppress-mask bytes are issued before A is staged (they
+  // do not depend on it); later tiles' loads are issued before the previous epilogue
+  half8 bw[NKS];
+  uint4 sm16;
+#define LG_LOAD(TILE)                                                                         do {                                                                                          const int bcol_ = min((TILE) * 16 + (lane & 15), V - 1);                                    const _Float16* wrow_ = W + (int64_t)bcol_ * K + 8 * (lane >> 4);                           _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks)                                            bw[ks] = *reinterpret_cast<const half8*>(wrow_ + 32 * ks);                                /* 16 mask bytes per tile (the mask buffer is padded to a multiple of 16) */                 sm16 = *reinterpret_cast<const uint4*>(smask + (TILE) * 16);                              } while (0)
+  const int tile0 = blockIdx.x * kLgWaves + w;
+  if (tile0 < ntiles) LG_LOAD(tile0);
   if (lnx) {  // A = the decoder's final LayerNorm of x, computed here (one wave per row)
     // wave w: rows w + 8j (j < 8), all loads up front
     ln_rows_wave<(K + 255) / 256, 64 / kLgWaves>(lnx, ldx, w, kLgWaves, B, ln_g, ln_b, sA, w, AP, K,
@@ -366,14 +397,13 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
   RowRules rr;  // lane = row in the statistics pass (fields copied: no scratch for pad[])
   rr.sample_begin = sR[lane].sample_begin; rr.suppress_all_ts = sR[lane].suppress_all_ts;
   rr.suppress_text = sR[lane].suppress_text; rr.ts_floor = sR[lane].ts_floor;
-  for (int tile = blockIdx.x * kLgWaves + w; tile < ntiles; tile += gridDim.x * kLgWaves) {
+  // running statistics of this wave's tiles for row = lane
+  float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
+  float ba_v = -INFINITY, bt_v = -INFINITY;
+  int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+  const int stride = gridDim.x * kLgWaves;
+  for (int tile = tile0; tile < ntiles; tile += stride) {
     const int col0 = tile * 16;
-    const int bcol = min(col0 + lr, V - 1);
-    const _Float16* wrow = W + (int64_t)bcol * K + kc8;
-    half8 bw[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) bw[ks] = *reinterpret_cast<const half8*>(wrow + 32 * ks);
-    __builtin_amdgcn_sched_barrier(0);  // keep every weight load of the tile ahead of the MFMAs
     f32x4 acc[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
@@ -389,10 +419,12 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) patch[(16 * m + 4 * (lane >> 4) + r) * 17 + lr] = acc[m][r];
+    const uint4 smc = sm16;
+    if (tile + stride < ntiles) LG_LOAD(tile + stride);  // next tile's weights during the epilogue
     // wave-private patch: the wave's own stores are visible to its loads in order
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     const int row = lane;
-    float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
+    float t_all = -INFINITY, t_text = -INFINITY, t_ts = -INFINITY;
     float vals[16];
     unsigned okm = 0;
 #pragma unroll
@@ -400,44 +432,68 @@ __global__ __launch_bounds__(kLgWaves * 64) void logits_partial_kernel(
       const int t = col0 + c;
       const float v = patch[row * 17 + c];
       vals[c] = v;
-      const bool ok = row < B && t < V && allowed(t, smask, R, rr, false);
+      const unsigned smw = c < 4 ? smc.x : c < 8 ? smc.y : c < 12 ? smc.z : smc.w;
+      const bool masked = (smw >> (8 * (c & 3))) & 0xffu;
+      const bool ok = row < B && t < V && !masked && allowed_unmasked(t, R, rr, false);
       okm |= (unsigned)ok << c;
       if (ok) {
-        m_all = fmaxf(m_all, v);
-        if (R.ts_begin >= 0 && t >= R.ts_begin) m_ts = fmaxf(m_ts, v);
-        else m_text = fmaxf(m_text, v);
+        t_all = fmaxf(t_all, v);
+        if (R.ts_begin >= 0 && t >= R.ts_begin) t_ts = fmaxf(t_ts, v);
+        else t_text = fmaxf(t_text, v);
       }
     }
-    float s_all = 0.f, s_ts = 0.f, ba_v = -INFINITY, bt_v = -INFINITY;
-    int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+    float u_all = 0.f, u_ts = 0.f;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       if (!((okm >> c) & 1u)) continue;
       const int t = col0 + c;
       const float v = vals[c];
-      s_all += __expf(v - m_all);
+      u_all += __expf(v - t_all);
       if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
       if (R.ts_begin >= 0 && t >= R.ts_begin) {
-        s_ts += __expf(v - m_ts);
+        u_ts += __expf(v - t_ts);
         if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
       }
     }
-    if (row < B) {
-      LogitPart p;
-      p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
-      p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
-      parts[(int64_t)row * ntiles + tile] = p;
+    float mo;
+    s_all = lse_merge(m_all, s_all, t_all, u_all, &mo); m_all = mo;
+    s_ts = lse_merge(m_ts, s_ts, t_ts, u_ts, &mo); m_ts = mo;
+    m_text = fmaxf(m_text, t_text);
+  }
+  // merge the 8 waves' statistics per row (wave order), one partial per (row, block)
+  __syncthreads();  // every wave is done with its patch: reuse sT for the wave partials
+  LogitPart* wp = reinterpret_cast<LogitPart*>(sT);  // [kLgWaves][64]
+  {
+    LogitPart p;
+    p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
+    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
+    wp[w * 64 + lane] = p;
+  }
+  __syncthreads();
+  if (w == 0 && lane < B) {
+    LogitPart q = wp[lane];
+    for (int k = 1; k < kLgWaves; ++k) {
+      const LogitPart p = wp[k * 64 + lane];
+      float mo;
+      q.s_all = lse_merge(q.m_all, q.s_all, p.m_all, p.s_all, &mo); q.m_all = mo;
+      q.s_ts = lse_merge(q.m_ts, q.s_ts, p.m_ts, p.s_ts, &mo); q.m_ts = mo;
+      q.m_text = fmaxf(q.m_text, p.m_text);
+      if (better(p.b_all_v, p.b_all_i, q.b_all_v, q.b_all_i)) { q.b_all_v = p.b_all_v; q.b_all_i = p.b_all_i; }
+      if (better(p.b_ts_v, p.b_ts_i, q.b_ts_v, q.b_ts_i)) { q.b_ts_v = p.b_ts_v; q.b_ts_i = p.b_ts_i; }
     }
+    parts[(int64_t)lane * gridDim.x + blockIdx.x] = q;
   }
 }
+#undef LG_LOAD
 
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s, const float* lnx, int ldx,
                            const float* ln_g, const float* ln_b) {
   JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
-  const int ntiles = logits_partial_blocks(V);
-  const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)kLgWaves * 64 * 17 * 4 + 64 * sizeof(RowRules);
+  const int ntiles = (V + 15) / 16;
+  const int nw = lg_waves(K);
+  const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)nw * 64 * 17 * 4 + 64 * sizeof(RowRules);
   auto kern = K == 384 ? logits_partial_kernel<12> : K == 512 ? logits_partial_kernel<16>
                                                               : logits_partial_kernel<24>;
   static bool attr[3] = {false, false, false};
@@ -447,20 +503,14 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                                   160 * 1024));
     attr[ai] = true;
   }
-  const int grid = std::min(256, (ntiles + kLgWaves - 1) / kLgWaves);
+  const int grid = logits_partial_blocks(V, K);
   for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
-    kern<<<grid, kLgWaves * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
-                                          smask, rules + r0, parts + (int64_t)r0 * ntiles, ntiles,
+    kern<<<grid, nw * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
+                                          smask, rules + r0, parts + (int64_t)r0 * grid, ntiles,
                                           lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b);
   JANUS_LAUNCH_CHECK();
 }
 
-__device__ __forceinline__ float lse_merge(float m1, float s1, float m2, float s2, float* mo) {
-  const float m = fmaxf(m1, m2);
-  *mo = m;
-  if (m == -INFINITY) return 0.f;
-  return s1 * __expf(m1 - m) + s2 * __expf(m2 - m);
-}
 
 // One block per row: reduce the partials, apply the timestamp-probability rule, pick
 // the token, accumulate its log-probability and derive the next step's row rules.

@@ -246,11 +246,11 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
   w->d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
   w->d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
 
-  w->d_smask.ensure(V);
+  w->d_smask.ensure((V + 15) / 16 * 16);  // logits_partial_kernel reads 16 mask bytes per tile
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   w->d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
   w->d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
-  const int nblk = logits_partial_blocks(V);
+  const int nblk = logits_partial_blocks(V, d);
   w->d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
   w->d_rules.ensure(sizeof(RowRules) * B);
   float* part_o = w->d_part_o.as<float>();
