@@ -34,20 +34,22 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   const int wm = wid / WN, wn = wid % WN;
 
   uint4 ra[A_CH], rb[B_CH];
+  // unconditional loads of clamped addresses, zeroed after (a guarded load compiles to a
+  // branch per 16-byte chunk)
   auto gload = [&](int k0) {
 #pragma unroll
     for (int c = 0; c < A_CH; ++c) {
       const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
       const int gr = row0 + r, gk = k0 + kc * 8;
-      ra[c] = (gr < M && gk < K) ? *reinterpret_cast<const uint4*>(p.A + (int64_t)gr * p.lda + gk)
-                                 : make_uint4(0, 0, 0, 0);
+      ra[c] = *reinterpret_cast<const uint4*>(p.A + (int64_t)min(gr, M - 1) * p.lda + min(gk, K - 8));
+      if (!(gr < M && gk < K)) ra[c] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int c = 0; c < B_CH; ++c) {
       const int idx = tid + c * 256, r = idx / KC, kc = idx % KC;
       const int gr = col0 + r, gk = k0 + kc * 8;
-      rb[c] = (gr < N && gk < K) ? *reinterpret_cast<const uint4*>(p.W + (int64_t)gr * p.ldw + gk)
-                                 : make_uint4(0, 0, 0, 0);
+      rb[c] = *reinterpret_cast<const uint4*>(p.W + (int64_t)min(gr, N - 1) * p.ldw + min(gk, K - 8));
+      if (!(gr < N && gk < K)) rb[c] = make_uint4(0, 0, 0, 0);
     }
   };
   auto sstore = [&](int buf) {
@@ -99,27 +101,64 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
     __syncthreads();
   }
 
+  // epilogue through LDS (the loop's last barrier freed it): the fp32 tile, then 8
+  // consecutive columns per thread -> bias / activation / residual -> 16-byte stores
+  constexpr int EP = BN + 4;  // fp32 pitch: the 4 row groups of a fragment store hit distinct banks
+  static_assert((size_t)BM * EP * 4 <= sizeof(smem), "epilogue tile must fit the staging LDS");
+  float* sC = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int n = 0; n < WNT; ++n) {
-    const int col = col0 + wn * WNT * 16 + n * 16 + (lane & 15);
-    if (col >= N) continue;
-    const float bv = p.bias ? p.bias[col] : 0.0f;
+  for (int m = 0; m < WMT; ++m)
 #pragma unroll
-    for (int m = 0; m < WMT; ++m) {
+    for (int n = 0; n < WNT; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = row0 + wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + r;
-        if (row >= M) continue;
-        float v = acc[m][n][r] + bv;
+      for (int r = 0; r < 4; ++r)
+        sC[(wm * WMT * 16 + m * 16 + (lane >> 4) * 4 + r) * EP + wn * WNT * 16 + n * 16 + (lane & 15)] =
+            acc[m][n][r];
+  __syncthreads();
+  constexpr int CPR8 = BN / 8;  // 8-column chunks per tile row
+  const bool vec = (N % 8) == 0 && (p.ldc % 8) == 0 && (EPI != EPI_RESID_F32 || (p.ldr % 4) == 0);
+#pragma unroll 2
+  for (int idx = tid; idx < BM * CPR8; idx += 256) {
+    const int r = idx / CPR8, c8 = (idx % CPR8) * 8;
+    const int row = row0 + r, col = col0 + c8;
+    if (row >= M || col >= N) continue;
+    const float4 lo = *reinterpret_cast<const float4*>(sC + r * EP + c8);
+    const float4 hi = *reinterpret_cast<const float4*>(sC + r * EP + c8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += p.bias[min(col + j, N - 1)];
+    }
+    if (vec) {
+      if constexpr (EPI == EPI_F16 || EPI == EPI_GELU_F16) {
+        half8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (_Float16)(EPI == EPI_GELU_F16 ? gelu_erf(v[j]) : v[j]);
+        *reinterpret_cast<half8*>(static_cast<_Float16*>(p.C) + (int64_t)row * p.ldc + col) = h;
+      } else {
+        float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col;
+        if constexpr (EPI == EPI_RESID_F32) {
+          const float4 r0 = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + col);
+          const float4 r1 = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + col + 4);
+          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+          v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        }
+        *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (col + j >= N) break;
         if constexpr (EPI == EPI_F16) {
-          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)v;
+          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col + j] = (_Float16)v[j];
         } else if constexpr (EPI == EPI_GELU_F16) {
-          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col] = (_Float16)gelu_erf(v);
+          static_cast<_Float16*>(p.C)[(int64_t)row * p.ldc + col + j] = (_Float16)gelu_erf(v[j]);
         } else if constexpr (EPI == EPI_RESID_F32) {
-          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col;
-          *c = p.R[(int64_t)row * p.ldr + col] + v;
+          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col + j;
+          *c = p.R[(int64_t)row * p.ldr + col + j] + v[j];
         } else {
-          static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
+          static_cast<float*>(p.C)[(int64_t)row * p.ldc + col + j] = v[j];
         }
       }
     }

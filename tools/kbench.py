@@ -145,8 +145,13 @@ def wide_units(B, reps):
     """Fused ResBlock1 unit (resunit_wide.hip) vs the same unit as two conv launches."""
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream().cuda_stream
-    for (C, k, d, T) in [(256, 3, 1, 20672), (256, 11, 5, 20672), (128, 3, 1, 165376), (128, 7, 3, 165376),
-                         (128, 11, 5, 165376), (64, 3, 1, 330752), (64, 7, 3, 330752), (64, 11, 5, 330752)]:
+    shapes = [(256, 3, 1, 20672), (256, 11, 5, 20672), (128, 3, 1, 165376), (128, 7, 3, 165376),
+              (128, 11, 5, 165376), (64, 3, 1, 330752), (64, 7, 3, 330752), (64, 11, 5, 330752)]
+    if os.environ.get("WIDE_C"):  # every (k, d) of one channel count
+        C = int(os.environ["WIDE_C"])
+        T = {256: 20672, 128: 165376, 64: 330752}[C]
+        shapes = [(C, k, d, T) for k in (3, 7, 11) for d in (1, 3, 5)]
+    for (C, k, d, T) in shapes:
         x = torch.randn(B, T, C, device=dev).half()
         out = torch.empty_like(x)
         mid = torch.empty_like(x)
