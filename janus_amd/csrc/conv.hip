@@ -292,6 +292,10 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
       // y = scale * (conv + res) (+ out): res/pv are zero when absent
       hv[j] = (_Float16)((v[j] + (float)rv[j]) * a.out_scale + (float)pv[j]);
     }
+    if (a.post_acc_silu) {  // block-uniform
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)rv[j]) * a.out_scale + (float)pv[j]);
+    }
     *reinterpret_cast<half8*>(outb + oo[i]) = hv;
   }
 }
@@ -325,6 +329,7 @@ static void conv_act(const ConvArgs& a, hipStream_t s) {
   // the (pre, post) pairs the Whisper stem and the Firefly-GAN generator use
   if (a.pre_act == ACT_NONE && a.post_act == ACT_NONE) conv_cfg<BM, BN, WMT, WNT, CK, ACT_NONE, ACT_NONE>(a, s);
   else if (a.pre_act == ACT_SILU && a.post_act == ACT_NONE) conv_cfg<BM, BN, WMT, WNT, CK, ACT_SILU, ACT_NONE>(a, s);
+  else if (a.pre_act == ACT_NONE && a.post_act == ACT_SILU) conv_cfg<BM, BN, WMT, WNT, CK, ACT_NONE, ACT_SILU>(a, s);
   else if (a.pre_act == ACT_SILU && a.post_act == ACT_SILU) conv_cfg<BM, BN, WMT, WNT, CK, ACT_SILU, ACT_SILU>(a, s);
   else if (a.pre_act == ACT_NONE && a.post_act == ACT_GELU) conv_cfg<BM, BN, WMT, WNT, CK, ACT_NONE, ACT_GELU>(a, s);
   else throw Error("conv: unsupported (pre_act, post_act) = (" + std::to_string(a.pre_act) + ", " +

@@ -113,6 +113,7 @@ struct ConvArgs {
   int pre_act, post_act;
   float out_scale; int accumulate;      // out = (accumulate ? out : 0) + out_scale * y
   int B;
+  int post_acc_silu = 0;                // out = silu(out) after the accumulation
 };
 struct ConvPack { int ck, kb, chunks, groups; int64_t phase_elems; };
 ConvPack conv_pack_geometry(int Cin, int Cout, int taps);
@@ -131,6 +132,9 @@ struct ResUnitArgs {
   const _Float16* w2; const float* b2;
   int B, T, C, k, d;
   float scale; int accumulate;
+  // out = silu(out) after the accumulation: the last unit of a ParallelBlock stores the
+  // SiLU its consumer (the next upsampler, or conv_post) would apply on every read
+  int post_silu = 0;
 };
 int resunit_kp(int C, int k);
 bool resunit_supported(int C, int k);

@@ -279,6 +279,10 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
         half8 hv;
 #pragma unroll
         for (int j = 0; j < 8; ++j) hv[j] = (_Float16)((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+      if (a.post_silu) {  // block-uniform
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
+      }
         *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
       }
     }

@@ -144,10 +144,11 @@ static hipEvent_t take_event(janus_vocoder* v) {
 
 static void run_conv(janus_vocoder* v, const VConv& cv, const _Float16* in, int B, int T_in,
                      _Float16* out, int T_out, int pre, int post, const _Float16* res, float scale,
-                     int acc, hipStream_t s) {
+                     int acc, hipStream_t s, int post_acc_silu = 0) {
   ConvArgs a = conv_args_torch(in, B, T_in, cv.cin, cv.packed.as<_Float16>(), cv.bias, out, T_out,
                                cv.cout, cv.taps, cv.stride, cv.pad, cv.dil, cv.transposed, pre,
                                post, res, (int64_t)T_out * cv.cout, scale, acc);
+  a.post_acc_silu = post_acc_silu;
   if (v->timing) {
     TimedLaunch t;
     t.a = take_event(v);
@@ -164,11 +165,11 @@ static void run_conv(janus_vocoder* v, const VConv& cv, const _Float16* in, int 
 }
 
 static void run_unit(janus_vocoder* v, const VUnit& U, const _Float16* x, _Float16* out, int B,
-                     int T, float scale, int acc, hipStream_t s) {
+                     int T, float scale, int acc, hipStream_t s, int post_silu = 0) {
   ResUnitArgs a;
   a.x = x; a.out = out; a.w1 = U.w1.as<_Float16>(); a.b1 = U.b1; a.w2 = U.w2.as<_Float16>();
   a.b2 = U.b2; a.B = B; a.T = T; a.C = U.c; a.k = U.k; a.d = U.d; a.scale = scale;
-  a.accumulate = acc;
+  a.accumulate = acc; a.post_silu = post_silu;
   if (v->timing) {
     TimedLaunch t;
     t.a = take_event(v);
@@ -202,11 +203,14 @@ static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* 
   _Float16* S = v->buf[2].as<_Float16>();
   _Float16* X[2] = {v->buf[3].as<_Float16>(), v->buf[4].as<_Float16>()};
   int T = F;
-  run_conv(v, v->pre, lat, B, F, H, F, ACT_NONE, ACT_NONE, nullptr, 1.0f, 0, s);
+  // H only feeds the next upsampler or conv_post, which both take silu(H): every producer
+  // of H's final value (conv_pre, the last unit of each ParallelBlock) stores silu(H)
+  // instead, so the SiLU runs once per element rather than once per upsampler phase
+  run_conv(v, v->pre, lat, B, F, H, F, ACT_NONE, ACT_SILU, nullptr, 1.0f, 0, s);
   const float inv_k = 1.0f / c.n_kernels;
   for (int i = 0; i < c.n_ups; ++i) {
     const int Tn = T * c.up_rates[i];
-    run_conv(v, v->ups[i], H, B, T, U, Tn, ACT_SILU, ACT_NONE, nullptr, 1.0f, 0, s);
+    run_conv(v, v->ups[i], H, B, T, U, Tn, ACT_NONE, ACT_NONE, nullptr, 1.0f, 0, s);
     T = Tn;
     for (int kj = 0; kj < c.n_kernels; ++kj) {
       const _Float16* x = U;
@@ -218,7 +222,7 @@ static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* 
             run_unit(v, U, x, xn, B, T, 1.0f, 0, s);
             x = xn;
           } else {
-            run_unit(v, U, x, H, B, T, inv_k, kj > 0 ? 1 : 0, s);
+            run_unit(v, U, x, H, B, T, inv_k, kj > 0 ? 1 : 0, s, kj + 1 == c.n_kernels);
           }
           continue;
         }
@@ -230,12 +234,13 @@ static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* 
           run_conv(v, c2, S, B, T, xn, T, ACT_NONE, ACT_NONE, x, 1.0f, 0, s);
           x = xn;
         } else {
-          run_conv(v, c2, S, B, T, H, T, ACT_NONE, ACT_NONE, x, inv_k, kj > 0 ? 1 : 0, s);
+          run_conv(v, c2, S, B, T, H, T, ACT_NONE, ACT_NONE, x, inv_k, kj > 0 ? 1 : 0, s,
+                   kj + 1 == c.n_kernels);
         }
       }
     }
   }
-  conv_post_launch(H, B, T, v->post_w, v->post_b, wav, pcm, s);
+  conv_post_launch(H, B, T, v->post_w, v->post_b, wav, pcm, s, /*pre_silu=*/0);
 }
 
 static void collect_timing(janus_vocoder* v) {

@@ -36,12 +36,13 @@ void frontend_launch(const uint8_t* bytes, const int64_t* boff, const int32_t* e
 }
 
 // conv_post: y[t] = tanh(b + sum_{c,j} w[c][j] * silu(x[t + j - 6][c])), x fp16 [B][T][16]
+// (pre_silu = 0: x already holds silu(x), stored by the last ResBlock unit)
 constexpr int kPostC = 16, kPostK = 13, kPostT = 256;
 
 __global__ __launch_bounds__(kPostT) void conv_post_kernel(const _Float16* __restrict__ x, int T,
                                                            const float* __restrict__ w, float bias,
                                                            float* __restrict__ wav,
-                                                           int16_t* __restrict__ pcm) {
+                                                           int16_t* __restrict__ pcm, int pre_silu) {
   __shared__ float xs[(kPostT + kPostK - 1) * (kPostC + 1)];
   __shared__ float ws[kPostC * kPostK];
   const int b = blockIdx.y, t0 = blockIdx.x * kPostT;
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(kPostT) void conv_post_kernel(const _Float16* __res
     if (t >= 0 && t < T) v = *reinterpret_cast<const uint4*>(xb + (int64_t)t * kPostC + half * 8);
     const _Float16* h = reinterpret_cast<const _Float16*>(&v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xs[r * (kPostC + 1) + half * 8 + j] = silu((float)h[j]);
+    for (int j = 0; j < 8; ++j) xs[r * (kPostC + 1) + half * 8 + j] = pre_silu ? silu((float)h[j]) : (float)h[j];
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
@@ -75,9 +76,10 @@ __global__ __launch_bounds__(kPostT) void conv_post_kernel(const _Float16* __res
 }
 
 void conv_post_launch(const _Float16* x, int B, int T, const float* w, float bias, float* wav,
-                      int16_t* pcm, hipStream_t s) {
+                      int16_t* pcm, hipStream_t s, int pre_silu) {
   if (B <= 0 || T <= 0) return;
-  conv_post_kernel<<<dim3((T + kPostT - 1) / kPostT, B), kPostT, 0, s>>>(x, T, w, bias, wav, pcm);
+  conv_post_kernel<<<dim3((T + kPostT - 1) / kPostT, B), kPostT, 0, s>>>(x, T, w, bias, wav, pcm,
+                                                                         pre_silu);
   JANUS_LAUNCH_CHECK();
 }
 
