@@ -36,50 +36,100 @@ void frontend_launch(const uint8_t* bytes, const int64_t* boff, const int32_t* e
 }
 
 // conv_post: y[t] = tanh(b + sum_{c,j} w[c][j] * silu(x[t + j - 6][c])), x fp16 [B][T][16]
-// (pre_silu = 0: x already holds silu(x), stored by the last ResBlock unit)
-constexpr int kPostC = 16, kPostK = 13, kPostT = 256;
+// (pre_silu = 0: x already holds silu(x), stored by the last ResBlock unit).
+// A block covers kPostT = 1024 samples of one utterance; the input rows are staged
+// channel-major (xs[c][row]) so a thread's 16-row window of one channel is four 16-byte
+// LDS reads, shared by its kPostR = 4 consecutive outputs (52 FMAs per channel window);
+// the waveform goes out as one float4 and the PCM as one 8-byte store per thread.
+constexpr int kPostC = 16, kPostK = 13, kPostR = 4, kPostThreads = 256;
+constexpr int kPostT = kPostThreads * kPostR;                   // samples per block
+constexpr int kPostRows = kPostT + 16;                          // staged rows (>= T + K - 1), 16-B rows
+constexpr size_t kPostLds = (size_t)(kPostC * kPostRows + kPostC * 16) * sizeof(float);
 
-__global__ __launch_bounds__(kPostT) void conv_post_kernel(const _Float16* __restrict__ x, int T,
-                                                           const float* __restrict__ w, float bias,
-                                                           float* __restrict__ wav,
-                                                           int16_t* __restrict__ pcm, int pre_silu) {
-  __shared__ float xs[(kPostT + kPostK - 1) * (kPostC + 1)];
-  __shared__ float ws[kPostC * kPostK];
-  const int b = blockIdx.y, t0 = blockIdx.x * kPostT;
+__global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16* __restrict__ x, int T,
+                                                                 const float* __restrict__ w, float bias,
+                                                                 float* __restrict__ wav,
+                                                                 int16_t* __restrict__ pcm, int pre_silu) {
+  extern __shared__ __attribute__((aligned(16))) float post_smem[];
+  float* xs = post_smem;                        // [kPostC][kPostRows]
+  float* ws = post_smem + kPostC * kPostRows;   // [kPostC][16] (taps padded to 16)
+  const int b = blockIdx.y, t0 = blockIdx.x * kPostT, tid = threadIdx.x;
   const _Float16* xb = x + (int64_t)b * T * kPostC;
-  for (int i = threadIdx.x; i < kPostC * kPostK; i += kPostT) ws[i] = w[i];
-  // stage rows t0-6 .. t0+255+6, 16 channels each (one 32-byte row = 2 x 16 B)
-  for (int i = threadIdx.x; i < (kPostT + kPostK - 1) * 2; i += kPostT) {
+  for (int i = tid; i < kPostC * 16; i += kPostThreads) {
+    const int c = i >> 4, j = i & 15;
+    ws[i] = j < kPostK ? w[c * kPostK + j] : 0.0f;
+  }
+  // stage rows t0-6 .. t0+kPostT+9 (16 channels = two 16-byte halves per row)
+  for (int i = tid; i < kPostRows * 2; i += kPostThreads) {
     const int r = i >> 1, half = i & 1;
     const int t = t0 - kPostK / 2 + r;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t >= 0 && t < T) v = *reinterpret_cast<const uint4*>(xb + (int64_t)t * kPostC + half * 8);
     const _Float16* h = reinterpret_cast<const _Float16*>(&v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xs[r * (kPostC + 1) + half * 8 + j] = pre_silu ? silu((float)h[j]) : (float)h[j];
+    for (int j = 0; j < 8; ++j)
+      xs[(half * 8 + j) * kPostRows + r] = pre_silu ? silu((float)h[j]) : (float)h[j];
   }
   __syncthreads();
-  const int t = t0 + threadIdx.x;
-  if (t >= T) return;
-  float acc = bias;
+  float acc[kPostR];
 #pragma unroll
-  for (int j = 0; j < kPostK; ++j)
+  for (int o = 0; o < kPostR; ++o) acc[o] = bias;
+#pragma unroll 4
+  for (int c = 0; c < kPostC; ++c) {
+    float xv[16], wv[16];
+    const float4* xr = reinterpret_cast<const float4*>(xs + c * kPostRows + kPostR * tid);
+    const float4* wr = reinterpret_cast<const float4*>(ws + c * 16);
 #pragma unroll
-    for (int c = 0; c < kPostC; ++c) acc += ws[c * kPostK + j] * xs[(threadIdx.x + j) * (kPostC + 1) + c];
-  const float y = tanhf(acc);
-  wav[(int64_t)b * T + t] = y;
-  if (pcm) {
-    float q = rintf(y * 32767.0f);
-    q = fminf(fmaxf(q, -32768.0f), 32767.0f);
-    pcm[(int64_t)b * T + t] = (int16_t)q;
+    for (int q = 0; q < 4; ++q) {
+      const float4 a4 = xr[q], w4 = wr[q];
+      xv[4 * q] = a4.x; xv[4 * q + 1] = a4.y; xv[4 * q + 2] = a4.z; xv[4 * q + 3] = a4.w;
+      wv[4 * q] = w4.x; wv[4 * q + 1] = w4.y; wv[4 * q + 2] = w4.z; wv[4 * q + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < kPostK; ++j)
+#pragma unroll
+      for (int o = 0; o < kPostR; ++o) acc[o] += wv[j] * xv[o + j];
+  }
+  const int t = t0 + kPostR * tid;
+  float y[kPostR];
+  int16_t q16[kPostR];
+#pragma unroll
+  for (int o = 0; o < kPostR; ++o) {
+    y[o] = tanhf(acc[o]);
+    const float q = fminf(fmaxf(rintf(y[o] * 32767.0f), -32768.0f), 32767.0f);
+    q16[o] = (int16_t)q;
+  }
+  float* wo = wav + (int64_t)b * T + t;
+  int16_t* po = pcm ? pcm + (int64_t)b * T + t : nullptr;
+  if (t + kPostR <= T && (T & 3) == 0) {  // aligned full group: vector stores
+    *reinterpret_cast<float4*>(wo) = make_float4(y[0], y[1], y[2], y[3]);
+    if (po) {
+      short4 v4;
+      v4.x = q16[0]; v4.y = q16[1]; v4.z = q16[2]; v4.w = q16[3];
+      *reinterpret_cast<short4*>(po) = v4;
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < kPostR; ++o) {
+      if (t + o < T) {
+        wo[o] = y[o];
+        if (po) po[o] = q16[o];
+      }
+    }
   }
 }
 
 void conv_post_launch(const _Float16* x, int B, int T, const float* w, float bias, float* wav,
                       int16_t* pcm, hipStream_t s, int pre_silu) {
   if (B <= 0 || T <= 0) return;
-  conv_post_kernel<<<dim3((T + kPostT - 1) / kPostT, B), kPostT, 0, s>>>(x, T, w, bias, wav, pcm,
-                                                                         pre_silu);
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)conv_post_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPostLds));
+    attr = true;
+  }
+  conv_post_kernel<<<dim3((T + kPostT - 1) / kPostT, B), kPostThreads, kPostLds, s>>>(
+      x, T, w, bias, wav, pcm, pre_silu);
   JANUS_LAUNCH_CHECK();
 }
 
