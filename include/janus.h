@@ -26,6 +26,15 @@ const char* janus_last_error(void);
 /* ABI version: major*10000 + minor*100 + patch. */
 int janus_version(void);
 
+/*
+ * A HIP stream whose kernels run only on the CUs set in cu_mask (words x 32 bits, bit i =
+ * CU i; hipExtStreamCreateWithCUMask). The pipeline runs the vocoder of one batch and
+ * the latency-bound greedy decoder of the next on disjoint CU sets. Destroy with
+ * janus_stream_destroy.
+ */
+int janus_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream_out);
+int janus_stream_destroy(void* stream);
+
 /* ------------------------------------------------------------- prosody --- */
 /*
  * Batched ProsodyExtractor core: aubio YIN per hop + RMS per utterance.

@@ -46,6 +46,8 @@ _F32 = ctypes.c_float
 # name -> (argtypes). Every entry point returns int status.
 SIGNATURES = {
     "janus_version": [],
+    "janus_stream_create_cu_mask": [_P, _I32, _P],
+    "janus_stream_destroy": [_P],
     "janus_duck_pcm16": [_P, _I64, _F32, _P],
     "janus_vad_energy": [_P, _I64, _I32, _I32, _F32, _F32, _P, _P],
     "janus_prosody_analyze": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
@@ -128,3 +130,43 @@ def require_gpu() -> torch.device:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+class MaskedStream:
+    """A HIP stream restricted to a CU subset (janus_stream_create_cu_mask), usable as a
+    torch stream (``torch.cuda.ExternalStream``). ``words``: 32-bit CU mask words."""
+
+    def __init__(self, words, device=None):
+        arr = (ctypes.c_uint32 * len(words))(*[int(w) & 0xFFFFFFFF for w in words])
+        h = ctypes.c_void_p()
+        call("janus_stream_create_cu_mask", ctypes.addressof(arr), len(words), ctypes.addressof(h))
+        self._h = h
+        self.n_cus = sum(bin(int(w) & 0xFFFFFFFF).count("1") for w in words)
+        self.stream = torch.cuda.ExternalStream(h.value, device=device)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().janus_stream_destroy(h)
+            except Exception:
+                pass
+
+
+def split_cu_masks(n_cus: int, dec_per_xcd: int, n_xcd: int = 8):
+    """Two disjoint CU masks, balanced per XCD. Workgroups of a launch are dealt round-robin
+    to the 8 XCDs whatever the mask, so a launch runs at the pace of the XCD with the
+    fewest enabled CUs: each mask must hold the same number of CUs on every XCD. gfx950
+    numbers CUs interleaved across XCDs (CU i sits on XCD i % 8; measured: masks that are
+    unbalanced under this mapping ran at the speed of their smallest per-XCD share), so
+    the first mask takes CU i when (i // 8) < dec_per_xcd, the second the rest."""
+    per_xcd = n_cus // n_xcd
+    assert 0 < dec_per_xcd < per_xcd, "each side needs at least one CU per XCD"
+    words = (n_cus + 31) // 32
+    a, b = [0] * words, [0] * words
+    for i in range(n_cus):
+        if (i // n_xcd) < dec_per_xcd:
+            a[i // 32] |= 1 << (i % 32)
+        else:
+            b[i // 32] |= 1 << (i % 32)
+    return a, b

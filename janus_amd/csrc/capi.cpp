@@ -25,6 +25,21 @@ extern "C" const char* janus_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int janus_version(void) { return 100; }
 
+extern "C" int janus_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** out) {
+  return guarded([&] {
+    JANUS_CHECK(cu_mask && out && words > 0, "bad argument");
+    hipStream_t st = nullptr;
+    JANUS_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)words, cu_mask));
+    *out = st;
+  });
+}
+
+extern "C" int janus_stream_destroy(void* stream) {
+  return guarded([&] {
+    if (stream) JANUS_HIP(hipStreamDestroy((hipStream_t)stream));
+  });
+}
+
 extern "C" int janus_prosody_analyze(const float* pcm, const int64_t* sample_offsets,
                                      const int64_t* hop_offsets, int batch, int64_t total_hops,
                                      int sample_rate, int hop_size, float tolerance,

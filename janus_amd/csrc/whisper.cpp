@@ -9,7 +9,10 @@
 #include <algorithm>
 #include <cstdlib>
 #include <map>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <cstring>
 #include "devmem.h"
 #include "kernels.h"
@@ -29,6 +32,52 @@ struct DecLayer {
   const float *ln1g, *ln1b, *ln2g, *ln2b, *ln3g, *ln3b;
 };
 
+// Lanes allocate their workspaces (hipMalloc / hipFree) before any of them starts a graph
+// capture: every lane arrives here after its allocations, and captures once all have.
+struct LaneLatch {
+  std::mutex m;
+  std::condition_variable cv;
+  int left = 0;
+  void arrive(bool wait) {
+    std::unique_lock<std::mutex> lk(m);
+    if (--left == 0) cv.notify_all();
+    if (wait) cv.wait(lk, [&] { return left <= 0; });
+  }
+};
+struct LaneArrival {
+  LaneLatch* l;
+  bool done = false;
+  explicit LaneArrival(LaneLatch* latch) : l(latch) {}
+  void now() {
+    if (l && !done) l->arrive(true);
+    done = true;
+  }
+  ~LaneArrival() {
+    if (l && !done) l->arrive(false);  // a lane that failed early must not stall the others
+  }
+};
+
+// One decoder lane: the per-step workspaces, KV caches and captured decode graphs for one
+// slice of the batch, plus the stream it runs on. Independent lanes run concurrently
+// (one host thread and one HIP stream each): every decoder launch is latency-bound at
+// B <= 64, so two half-batch chains overlap their launch and memory round trips.
+struct DecLane {
+  DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt,
+      d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
+      d_xc, d_xpc, d_xpml, d_enc;
+  std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
+  hipStream_t stream = nullptr;  // graph capture needs a non-null stream
+  hipEvent_t ev_done = nullptr;
+  DecLane() = default;
+  DecLane(const DecLane&) = delete;
+  DecLane& operator=(const DecLane&) = delete;
+  ~DecLane() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+  }
+};
+
 }  // namespace janus
 
 struct janus_whisper {
@@ -42,17 +91,11 @@ struct janus_whisper {
   std::vector<janus::DecLayer> dec;
   // workspaces
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
-  janus::DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_logits, d_kc, d_vc, d_ck, d_cv, d_smask,
-      d_done, d_prompt, d_supp, d_ntok_scratch, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt,
-      d_xqk, d_xc, d_xpc, d_xpml, d_enc;
-  std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
-  hipStream_t side = nullptr;  // graph capture needs a non-null stream
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  // decoder lanes: each owns the workspaces, captured graphs and stream of one batch slice
+  std::vector<std::unique_ptr<janus::DecLane>> lanes;
+  hipEvent_t ev_in = nullptr;
   ~janus_whisper() {
-    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
-    if (side) (void)hipStreamDestroy(side);
     if (ev_in) (void)hipEventDestroy(ev_in);
-    if (ev_out) (void)hipEventDestroy(ev_out);
   }
 };
 
@@ -220,83 +263,84 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
                    w->params.get("encoder.layer_norm.bias", d), out, (int)M, d, 1e-5f, s);
 }
 
-static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const janus_decode_options* opt,
+static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, int B, const janus_decode_options* opt,
                           int32_t* tokens_out, int32_t* n_tokens_out, float* sum_lp_out,
-                          hipStream_t s) {
+                          hipStream_t s, LaneLatch* latch) {
+  LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
   // the captured decode graphs bake in every pointer they read: the encoder output goes
   // to a context-owned buffer first (one ~0.1 ms device copy) so the graphs are reused
   // whatever buffer the caller's allocator handed out this time
-  w->d_enc.ensure(sizeof(_Float16) * (int64_t)B * Te * d);
-  JANUS_HIP(hipMemcpyAsync(w->d_enc.p, enc_in, sizeof(_Float16) * (int64_t)B * Te * d,
+  Z.d_enc.ensure(sizeof(_Float16) * (int64_t)B * Te * d);
+  JANUS_HIP(hipMemcpyAsync(Z.d_enc.p, enc_in, sizeof(_Float16) * (int64_t)B * Te * d,
                            hipMemcpyDeviceToDevice, s));
-  const _Float16* enc = w->d_enc.as<_Float16>();
+  const _Float16* enc = Z.d_enc.as<_Float16>();
   const int maxlen = opt->max_length;
   JANUS_CHECK(opt->prompt_len >= 1 && opt->prompt_len < maxlen && maxlen <= NC,
               "decode: need 1 <= prompt_len < max_length <= n_text_ctx");
   const int64_t Me = (int64_t)B * Te;
   const int nl = c.dec_layers;
-  w->d_x.ensure(sizeof(float) * B * d);
-  w->d_a.ensure(sizeof(_Float16) * B * d);
-  w->d_qkv.ensure(sizeof(_Float16) * B * 3 * d);
-  w->d_o.ensure(sizeof(_Float16) * B * d);
-  w->d_q2.ensure(sizeof(_Float16) * B * d);
-  w->d_f.ensure(sizeof(_Float16) * B * 4 * d);
-  w->d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
-  w->d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
+  Z.d_x.ensure(sizeof(float) * B * d);
+  Z.d_a.ensure(sizeof(_Float16) * B * d);
+  Z.d_qkv.ensure(sizeof(_Float16) * B * 3 * d);
+  Z.d_o.ensure(sizeof(_Float16) * B * d);
+  Z.d_q2.ensure(sizeof(_Float16) * B * d);
+  Z.d_f.ensure(sizeof(_Float16) * B * 4 * d);
+  Z.d_kc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
+  Z.d_vc.ensure(sizeof(_Float16) * (int64_t)nl * B * NC * d);
 
-  w->d_smask.ensure((V + 15) / 16 * 16);  // logits_partial_kernel reads 16 mask bytes per tile
+  Z.d_smask.ensure((V + 15) / 16 * 16);  // logits_partial_kernel reads 16 mask bytes per tile
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
-  w->d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
-  w->d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
+  Z.d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
+  Z.d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
   const int nblk = logits_partial_blocks(V, d);
-  w->d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
-  w->d_rules.ensure(sizeof(RowRules) * B);
-  float* part_o = w->d_part_o.as<float>();
-  float* part_ml = w->d_part_ml.as<float>();
-  w->d_done.ensure(sizeof(int32_t) * B);
-  w->d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
-  w->d_tok.ensure(sizeof(int32_t) * (int64_t)B * maxlen);
-  w->d_ntok.ensure(sizeof(int32_t) * B);
-  w->d_slp.ensure(sizeof(float) * B);
-  int32_t* tokens = w->d_tok.as<int32_t>();
-  int32_t* n_tokens = w->d_ntok.as<int32_t>();
-  float* sum_lp = w->d_slp.as<float>();
-  w->d_supp.ensure(sizeof(int32_t) * (opt->n_suppress > 0 ? opt->n_suppress : 1));
-  float* x = w->d_x.as<float>();
-  _Float16 *a = w->d_a.as<_Float16>(), *qkv = w->d_qkv.as<_Float16>(), *o = w->d_o.as<_Float16>(),
-           *q2 = w->d_q2.as<_Float16>(), *f = w->d_f.as<_Float16>();
-  int32_t* done = w->d_done.as<int32_t>();
+  Z.d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
+  Z.d_rules.ensure(sizeof(RowRules) * B);
+  float* part_o = Z.d_part_o.as<float>();
+  float* part_ml = Z.d_part_ml.as<float>();
+  Z.d_done.ensure(sizeof(int32_t) * B);
+  Z.d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
+  Z.d_tok.ensure(sizeof(int32_t) * (int64_t)B * maxlen);
+  Z.d_ntok.ensure(sizeof(int32_t) * B);
+  Z.d_slp.ensure(sizeof(float) * B);
+  int32_t* tokens = Z.d_tok.as<int32_t>();
+  int32_t* n_tokens = Z.d_ntok.as<int32_t>();
+  float* sum_lp = Z.d_slp.as<float>();
+  Z.d_supp.ensure(sizeof(int32_t) * (opt->n_suppress > 0 ? opt->n_suppress : 1));
+  float* x = Z.d_x.as<float>();
+  _Float16 *a = Z.d_a.as<_Float16>(), *qkv = Z.d_qkv.as<_Float16>(), *o = Z.d_o.as<_Float16>(),
+           *q2 = Z.d_q2.as<_Float16>(), *f = Z.d_f.as<_Float16>();
+  int32_t* done = Z.d_done.as<int32_t>();
 
-  JANUS_HIP(hipMemcpyAsync(w->d_prompt.p, opt->prompt, sizeof(int32_t) * opt->prompt_len,
+  JANUS_HIP(hipMemcpyAsync(Z.d_prompt.p, opt->prompt, sizeof(int32_t) * opt->prompt_len,
                            hipMemcpyHostToDevice, s));
   if (opt->n_suppress > 0)
-    JANUS_HIP(hipMemcpyAsync(w->d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
+    JANUS_HIP(hipMemcpyAsync(Z.d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
                              hipMemcpyHostToDevice, s));
-  build_mask_launch(w->d_supp.as<int32_t>(), opt->n_suppress, w->d_smask.as<uint8_t>(), V, s);
-  init_tokens_launch(tokens, maxlen, w->d_prompt.as<int32_t>(), opt->prompt_len, done, sum_lp,
+  build_mask_launch(Z.d_supp.as<int32_t>(), opt->n_suppress, Z.d_smask.as<uint8_t>(), V, s);
+  init_tokens_launch(tokens, maxlen, Z.d_prompt.as<int32_t>(), opt->prompt_len, done, sum_lp,
                      n_tokens, B, s);
-  rules_init_launch(w->d_rules.as<RowRules>(), B, s);
+  rules_init_launch(Z.d_rules.as<RowRules>(), B, s);
 
   // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
   const bool xabs = xattn_supported(d, H) && B <= 64 && std::getenv("JANUS_NO_XABSORB") == nullptr;
   const int xsplit = xattn_split_count(Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : 0);
   if (xabs) {
-    w->d_xqk.ensure(sizeof(_Float16) * B * H * d);
-    w->d_xc.ensure(sizeof(_Float16) * B * H * d);
-    w->d_xpc.ensure(sizeof(float) * (int64_t)B * xsplit * H * d);
-    w->d_xpml.ensure(sizeof(float) * (int64_t)B * xsplit * H * 2);
+    Z.d_xqk.ensure(sizeof(_Float16) * B * H * d);
+    Z.d_xc.ensure(sizeof(_Float16) * B * H * d);
+    Z.d_xpc.ensure(sizeof(float) * (int64_t)B * xsplit * H * d);
+    Z.d_xpml.ensure(sizeof(float) * (int64_t)B * xsplit * H * 2);
   }
   // cross-attention keys/values, once per window
   if (!xabs) {
-    w->d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
-    w->d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+    Z.d_ck.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
+    Z.d_cv.ensure(sizeof(_Float16) * (int64_t)nl * Me * d);
   }
   for (int l = 0; l < nl && !xabs; ++l) {
     DecLayer& L = w->dec[l];
-    _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
-    _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
+    _Float16* ck = Z.d_ck.as<_Float16>() + (int64_t)l * Me * d;
+    _Float16* cv = Z.d_cv.as<_Float16>() + (int64_t)l * Me * d;
     gemm_launch(EPI_F16, gargs(enc, d, L.wk_c.as<_Float16>(), d, nullptr, ck, d, (int)Me, d, d), s);
     gemm_launch(EPI_F16, gargs(enc, d, L.wv_c.as<_Float16>(), d, L.bv_c, cv, d, (int)Me, d, d), s);
   }
@@ -317,8 +361,8 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
   // Opt-in: with the 16-wave skinny GEMM the separate LayerNorm launch measured faster
   // (637.7 vs 660.8 ms per bench step) — the consumer ingests A as fp32.
   const bool fused_ln = B <= 64 && std::getenv("JANUS_FUSED_LN") != nullptr;
-  w->d_lnp.ensure(sizeof(float2) * B * (d / 16));
-  float2* lnp = w->d_lnp.as<float2>();
+  Z.d_lnp.ensure(sizeof(float2) * B * (d / 16));
+  float2* lnp = Z.d_lnp.as<float2>();
   auto lnargs = [&](const float* g, const float* bta, const _Float16* W, const float* bias,
                     void* C, int64_t ldc, int N, _Float16* kcp, _Float16* vcp, int pos) {
     SkinnyLnArgs p;
@@ -343,15 +387,15 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
     if (ln_pro) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
     return g;
   };
-  w->d_lncnt.ensure(sizeof(int));
-  JANUS_HIP(hipMemsetAsync(w->d_lncnt.p, 0, sizeof(int), s));
+  Z.d_lncnt.ensure(sizeof(int));
+  JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int), s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
   const float* fin_b = w->params.get("decoder.layer_norm.bias", d);
   auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias, const float* ng,
                    const float* nb) {
     GemmArgs g = gargs(A, K, W.as<_Float16>(), K, bias, x, d, B, d, K, x, d);
     if (fused_ln) g.ln_part = lnp;
-    if (ln_fuse) { g.ln_g = ng; g.ln_b = nb; g.ln_out = a; g.ln_cnt = w->d_lncnt.as<int>(); }
+    if (ln_fuse) { g.ln_g = ng; g.ln_b = nb; g.ln_out = a; g.ln_cnt = Z.d_lncnt.as<int>(); }
     gemm_launch(EPI_RESID_F32, g, s);
   };
   auto step = [&](int pos) {
@@ -360,10 +404,10 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
                  ln_fuse ? a : nullptr);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
-      _Float16* kc = w->d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
-      _Float16* vc = w->d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
-      _Float16* ck = w->d_ck.as<_Float16>() + (int64_t)l * Me * d;
-      _Float16* cv = w->d_cv.as<_Float16>() + (int64_t)l * Me * d;
+      _Float16* kc = Z.d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
+      _Float16* vc = Z.d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
+      _Float16* ck = Z.d_ck.as<_Float16>() + (int64_t)l * Me * d;
+      _Float16* cv = Z.d_cv.as<_Float16>() + (int64_t)l * Me * d;
       if (fused_ln) {
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
@@ -384,8 +428,8 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
       resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
       if (xabs) {
         const int hd = H * d;
-        _Float16* xqk = w->d_xqk.as<_Float16>();
-        _Float16* xc = w->d_xc.as<_Float16>();
+        _Float16* xqk = Z.d_xqk.as<_Float16>();
+        _Float16* xc = Z.d_xc.as<_Float16>();
         if (fused_ln) {
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
@@ -394,7 +438,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
           gemm_launch(EPI_F16, with_ln(gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
                                        L.ln2g, L.ln2b), s);
         }
-        xattn_launch(xqk, enc, B, Te, d, H, xsplit, w->d_xpc.as<float>(), w->d_xpml.as<float>(), xc, s);
+        xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s);
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
         GemmArgs gv = gargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
         gv.a_group_cols = 64;
@@ -427,10 +471,10 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
     if (!ln_fuse && !ln_pro) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
-    logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, w->d_smask.as<uint8_t>(),
-                          w->d_rules.as<RowRules>(), w->d_parts.as<LogitPart>(), s,
+    logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
+                          Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
                           ln_pro ? x : nullptr, d, fin_g, fin_b);
-    select_partials_launch(w->d_parts.as<LogitPart>(), nblk, R, w->d_rules.as<RowRules>(), tokens,
+    select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                            maxlen, pos, done, sum_lp, n_tokens, B, s);
   };
   const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
@@ -438,15 +482,16 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
   // every device pointer a captured kernel touches, plus the shape: the graph cache key
   const std::vector<int64_t> base_key = {
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
-      (int64_t)q2, (int64_t)f, (int64_t)w->d_kc.p, (int64_t)w->d_vc.p, (int64_t)w->d_ck.p,
-      (int64_t)w->d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)w->d_parts.p,
-      (int64_t)w->d_rules.p, (int64_t)w->d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)w->d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)w->d_xqk.p,
-      (int64_t)w->d_xc.p, (int64_t)w->d_xpc.p, (int64_t)w->d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
-      (int64_t)n_tokens, (int64_t)w->d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
+      (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
+      (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
+      (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
-  if (w->graphs.size() > 512) {
-    for (auto& kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
-    w->graphs.clear();
+  arrival.now();  // all lanes' allocations done: captures may start
+  if (Z.graphs.size() > 512) {
+    for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
+    Z.graphs.clear();
   }
   for (int p0 = 0; p0 + 1 < maxlen; p0 += chunk) {
     const int n = std::min(chunk, maxlen - 1 - p0);
@@ -454,8 +499,8 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
       std::vector<int64_t> key = base_key;
       key.push_back(p0);
       key.push_back(n);
-      auto it = w->graphs.find(key);
-      if (it == w->graphs.end()) {
+      auto it = Z.graphs.find(key);
+      if (it == Z.graphs.end()) {
         hipGraph_t g;
         JANUS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         try {
@@ -470,7 +515,7 @@ static void decode_greedy(janus_whisper* w, const _Float16* enc_in, int B, const
         hipGraphExec_t ge;
         JANUS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         JANUS_HIP(hipGraphDestroy(g));
-        it = w->graphs.emplace(key, ge).first;
+        it = Z.graphs.emplace(key, ge).first;
       }
       JANUS_HIP(hipGraphLaunch(it->second, s));
     } else {
@@ -563,25 +608,67 @@ extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc
                                            int32_t* n_tokens, float* sum_logprob, void* stream) {
   return guarded([&] {
     JANUS_CHECK(w && enc && opt && tokens && n_tokens && sum_logprob, "null argument");
+    JANUS_CHECK(batch >= 1, "decode: batch must be >= 1");
     std::lock_guard<std::mutex> lk(w->mu);
     hipStream_t s = (hipStream_t)stream;
     prepare(w, s);
-    if (s != nullptr) {
-      decode_greedy(w, reinterpret_cast<const _Float16*>(enc), batch, opt, tokens, n_tokens,
-                    sum_logprob, s);
+    const _Float16* e = reinterpret_cast<const _Float16*>(enc);
+    // lanes: JANUS_DEC_LANES (default 1). Two half-batch lanes measured slower at B = 64
+    // (428.7 vs 419.6 ms per bench step): the skinny projections are weight-stream
+    // launches, so each lane re-streams every weight matrix, and the cross-attention
+    // already saturates HBM.
+    int nlanes = 1;
+    if (const char* v = std::getenv("JANUS_DEC_LANES")) nlanes = std::atoi(v);
+    nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
+    while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
+    if (nlanes == 1 && s != nullptr) {
+      decode_greedy(w, *w->lanes[0], e, batch, opt, tokens, n_tokens, sum_logprob, s, nullptr);
       return;
     }
-    // the null stream cannot be captured: run on a side stream ordered by events
-    if (!w->side) {
-      JANUS_HIP(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
-      JANUS_HIP(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
-      JANUS_HIP(hipEventCreateWithFlags(&w->ev_out, hipEventDisableTiming));
-    }
+    // the null stream cannot be captured, and lanes run concurrently: each lane gets its
+    // own stream (the caller's priority), forked from and joined back into the caller's
+    int prio = 0;
+    JANUS_HIP(hipStreamGetPriority(s, &prio));
+    if (!w->ev_in) JANUS_HIP(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
     JANUS_HIP(hipEventRecord(w->ev_in, s));
-    JANUS_HIP(hipStreamWaitEvent(w->side, w->ev_in, 0));
-    decode_greedy(w, reinterpret_cast<const _Float16*>(enc), batch, opt, tokens, n_tokens,
-                  sum_logprob, w->side);
-    JANUS_HIP(hipEventRecord(w->ev_out, w->side));
-    JANUS_HIP(hipStreamWaitEvent(s, w->ev_out, 0));
+    for (int i = 0; i < nlanes; ++i) {
+      DecLane& Z = *w->lanes[i];
+      if (!Z.stream) {
+        JANUS_HIP(hipStreamCreateWithPriority(&Z.stream, hipStreamNonBlocking, prio));
+        JANUS_HIP(hipEventCreateWithFlags(&Z.ev_done, hipEventDisableTiming));
+      }
+      JANUS_HIP(hipStreamWaitEvent(Z.stream, w->ev_in, 0));
+    }
+    const int maxlen = opt->max_length;
+    LaneLatch latch;
+    latch.left = nlanes;
+    std::vector<std::string> errs(nlanes);
+    int dev = 0;
+    JANUS_HIP(hipGetDevice(&dev));
+    auto run = [&](int i) {
+      const int b0 = (int)((int64_t)batch * i / nlanes), b1 = (int)((int64_t)batch * (i + 1) / nlanes);
+      DecLane& Z = *w->lanes[i];
+      try {
+        JANUS_HIP(hipSetDevice(dev));  // a fresh host thread starts on device 0
+        decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, opt,
+                      tokens + (int64_t)b0 * maxlen, n_tokens + b0, sum_logprob + b0, Z.stream,
+                      nlanes > 1 ? &latch : nullptr);
+      } catch (const std::exception& ex) {
+        errs[i] = ex.what();
+      } catch (...) {
+        errs[i] = "unknown error";
+      }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < nlanes; ++i) th.emplace_back(run, i);
+    run(0);
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nlanes; ++i) {
+      DecLane& Z = *w->lanes[i];
+      JANUS_HIP(hipEventRecord(Z.ev_done, Z.stream));
+      JANUS_HIP(hipStreamWaitEvent(s, Z.ev_done, 0));
+    }
+    for (int i = 0; i < nlanes; ++i)
+      JANUS_CHECK(errs[i].empty(), "decode lane " + std::to_string(i) + ": " + errs[i]);
   });
 }

@@ -12,6 +12,8 @@ build the "(emotion) text" prompt (synthesizer.py:149-177), then the GPU front e
 Firefly-GAN vocoder produce f32 audio and int16 PCM for all packets in one batch.
 Morse packets stay on the host (synthesizer.py:257-326).
 """
+import os
+import sys
 import time
 
 import numpy as np
@@ -111,3 +113,95 @@ class JanusPipeline:
         enc = self.encode(pcm, offsets, lengths)
         wav, pcm16, _ = self.decode(enc.packets, frames)
         return enc, wav, pcm16
+
+    # ------------------------------------------------------- overlapped (serving) step
+    def _split_streams(self, device, dec_per_xcd: int):
+        key = (str(device), dec_per_xcd)
+        if getattr(self, "_split_key", None) != key:
+            n = torch.cuda.get_device_properties(device).multi_processor_count
+            dmask, vmask = nat.split_cu_masks(n, dec_per_xcd)
+            self._dec_s = nat.MaskedStream(dmask, device)
+            self._voc_s = nat.MaskedStream(vmask, device)
+            self._split_key = key
+        return self._dec_s.stream, self._voc_s.stream
+
+    def step_overlapped(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
+                        mode=JanusMode.SEMANTIC_VOICE, override="auto", timestamp=None):
+        """One serving step of a two-stage pipeline: encode batch i while the vocoder
+        renders the packets of batch i-1 (kept from the previous call).
+
+        Mel + encoder (compute-bound) get the whole GPU; then the greedy decoder of batch
+        i (latency-bound) runs on a CU-masked stream holding `dec_per_xcd` CUs of each XCD,
+        and the vocoder of batch i-1 followed by this batch's YIN on the disjoint rest, so
+        neither holds the CUs the other needs (an unmasked overlap measured slower: the
+        vocoder's long-running blocks delay every decoder launch). Returns
+        (EncodeResult of batch i, wav / pcm16 of batch i-1 or None)."""
+        B = len(lengths)
+        w = self.whisper
+        main = torch.cuda.current_stream(pcm.device)
+        hi = self._hi_stream(pcm.device)
+        ds, vs = self._split_streams(pcm.device, dec_per_xcd)
+        hi.wait_stream(main)
+        with torch.cuda.stream(hi):
+            mel = w.logmel(pcm, offsets, B, 3)
+            enc = w.encode(mel)
+        vs.wait_stream(hi)
+        ds.wait_stream(hi)
+        prev = getattr(self, "_pending", None)
+        wav = pcm16 = None
+        timing = os.environ.get("JANUS_OVERLAP_TIMING") is not None
+        yin_dec = os.environ.get("JANUS_YIN_SIDE", "voc") == "dec"
+        if timing:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(vs)
+            ev[2].record(ds)
+        pres = None
+
+        # YIN follows the vocoder on its own CUs: an uncapped grid lets the hardware balance
+        # the uneven per-hop cost (early exit, silent hops) over them
+        yin_blocks = int(os.environ.get("JANUS_YIN_BLOCKS", "0"))
+
+        def yin():
+            try:
+                return prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=yin_blocks)
+            except Exception:  # engine.py:520-525
+                return None
+        with torch.cuda.stream(vs):
+            if prev is not None:
+                wav, pcm16, _ = self.decode(prev, frames)
+            if not yin_dec:
+                pres = yin()
+            if timing:
+                ev[1].record(vs)  # before the decoder call, which blocks the host
+        with torch.cuda.stream(ds):
+            if yin_dec:
+                pres = yin()
+            tokens, ntok, _ = w.decode(enc, self.max_length)
+        if timing:
+            ev[3].record(ds)
+        main.wait_stream(ds)
+        main.wait_stream(vs)
+        if timing:
+            torch.cuda.synchronize()
+            print(f"[overlap] vocoder side {ev[0].elapsed_time(ev[1]):.1f} ms, decoder side "
+                  f"{ev[2].elapsed_time(ev[3]):.1f} ms", file=sys.stderr, flush=True)
+        try:
+            tags = pres.tags() if pres is not None else None
+        except Exception:
+            tags = None
+        if tags is None:
+            tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
+        texts = w.texts(tokens)
+        ts = time.time() if timestamp is None else timestamp
+        packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
+                   for t, g in zip(texts, tags)]
+        self._pending = packets
+        return EncodeResult(texts, tags, packets, tokens, ntok), wav, pcm16
+
+    def flush(self, frames):
+        """Render the packets the last overlapped step left pending."""
+        prev, self._pending = getattr(self, "_pending", None), None
+        if prev is None:
+            return None, None
+        wav, pcm16, _ = self.decode(prev, frames)
+        return wav, pcm16

@@ -39,3 +39,17 @@ def test_version_and_error_slot(native_lib):
 def test_gfx950_code_object():
     data = open(_native.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_split_cu_masks_balanced_per_xcd():
+    """Both masks of the overlapped step hold the same CU count on every XCD (CU i on XCD
+    i % 8) and, at multiples of 4, on every shader engine; they are disjoint and cover
+    all CUs."""
+    for dec in (4, 8, 16, 20, 28):
+        a, b = _native.split_cu_masks(256, dec)
+        bits_a = [i for i in range(256) if a[i // 32] >> (i % 32) & 1]
+        bits_b = [i for i in range(256) if b[i // 32] >> (i % 32) & 1]
+        assert len(bits_a) == 8 * dec and len(bits_a) + len(bits_b) == 256
+        assert not set(bits_a) & set(bits_b)
+        for x in range(8):
+            assert sum(1 for i in bits_a if i % 8 == x) == dec

@@ -47,3 +47,38 @@ def test_transcriber_wav(gpu, tmp_path):
     t1 = tr.transcribe_file(str(path))
     t2 = tr.transcribe_buffer(np.repeat(x, 3))  # 48 kHz buffer whose [::3] is x
     assert isinstance(t1, str) and t1 == t2
+
+
+def test_overlapped_step_matches_sequential(gpu):
+    """The serving pipeline (encode batch i on the whole GPU, then the greedy decoder of
+    batch i and the vocoder of batch i-1 + YIN on disjoint CU-masked streams) produces the
+    same packets and the same waveforms as the back-to-back step."""
+    pipe = JanusPipeline("tiny.en", max_length=12)
+    batches = []
+    for i in range(2):
+        utts = [synth_speech(300 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]
+        lengths = [len(u) for u in utts]
+        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+        pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+        batches.append((pcm, offs, lengths))
+    frames = 16
+    seq = []
+    for pcm, offs, lengths in batches:
+        enc = pipe.encode(pcm, offs, lengths, timestamp=5.0)
+        wav, pcm16, _ = pipe.decode(enc.packets, frames)
+        seq.append((enc.packets, wav, pcm16))
+    ov_packets, ov_wavs = [], []
+    for pcm, offs, lengths in batches:
+        enc, wav, pcm16 = pipe.step_overlapped(pcm, offs, lengths, frames, 16, timestamp=5.0)
+        ov_packets.append(enc.packets)
+        ov_wavs.append((wav, pcm16))
+    ov_wavs.append(pipe.flush(frames))
+    assert ov_wavs[0] == (None, None)  # nothing pending before the first step
+    for i in range(2):
+        assert ov_packets[i] == seq[i][0]
+        wav, pcm16 = ov_wavs[i + 1]
+        if seq[i][1] is None:
+            assert wav is None
+            continue
+        torch.testing.assert_close(wav, seq[i][1], rtol=0, atol=0)
+        assert torch.equal(pcm16, seq[i][2])
