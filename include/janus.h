@@ -202,6 +202,8 @@ typedef struct {
   int no_timestamps;       /* <|notimestamps|> id */
   int max_initial_timestamp_index; /* 50 (= 1.0 s), -1 = unbounded */
   int check_every;         /* poll for all-rows-finished every N steps (0 = never) */
+  int xattn_splits;        /* cross-attention key splits per utterance (0 = auto: 8; the
+                              overlapped step on half the CUs runs best at 4) */
 } janus_decode_options;
 
 /*

@@ -325,7 +325,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
 
   // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
   const bool xabs = xattn_supported(d, H) && B <= 64 && std::getenv("JANUS_NO_XABSORB") == nullptr;
-  const int xsplit = xattn_split_count(Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : 0);
+  const int xsplit = xattn_split_count(
+      Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : opt->xattn_splits);
   if (xabs) {
     Z.d_xqk.ensure(sizeof(_Float16) * B * H * d);
     Z.d_xc.ensure(sizeof(_Float16) * B * H * d);

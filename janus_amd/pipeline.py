@@ -176,7 +176,8 @@ class JanusPipeline:
         with torch.cuda.stream(ds):
             if yin_dec:
                 pres = yin()
-            tokens, ntok, _ = w.decode(enc, self.max_length)
+            # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339 ms)
+            tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4)
         if timing:
             ev[3].record(ds)
         main.wait_stream(ds)
