@@ -28,9 +28,10 @@ namespace janus {
 
 constexpr int kYinBuf = 4096;          // aubio pitch buffer (prosody.py:32)
 constexpr int kYinLen = kYinBuf / 2;   // yin fvec length
-constexpr int kYinThreads = 256;       // 4 waves; each lane owns 2 consecutive taus
-constexpr int kTauChunk = kYinThreads * 2;  // 512 taus per pass: voiced hops (F0 >= 95 Hz at
-                                            // 48 kHz: period <= 505) exit after one pass
+// Block = NT threads, each lane owns 2 consecutive taus, so one pass covers 2·NT taus.
+// NT = 128 (256-tau passes, the default): voiced hops with F0 >= 190 Hz at 48 kHz exit
+// after one pass and F0 >= 95 Hz after two, so a 160 / 260 Hz voice computes half the
+// taus of a 512-tau pass. NT = 256 (512-tau passes) kept for A/B (JANUS_YIN_THREADS).
 
 __device__ __forceinline__ int find_utt(const int64_t* offs, int B, int64_t g) {
   // largest b with offs[b] <= g (offs is non-decreasing, offs[0]=0, offs[B]=total)
@@ -51,6 +52,7 @@ __device__ __forceinline__ float window_sample(const float* pcm, int64_t base, i
   return p < n ? pcm[base + p] : 0.0f;
 }
 
+template <int kYinThreads>
 __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
     const int64_t* __restrict__ hop_off, int B, int hop, const float* __restrict__ state_in,
@@ -58,6 +60,8 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     int64_t total_hops) {
   __shared__ __attribute__((aligned(16))) float w[kYinBuf];
   __shared__ __attribute__((aligned(16))) float dd[kYinLen];   // d(tau), then yin(tau)
+  constexpr int kTauChunk = kYinThreads * 2;
+  constexpr int kWaves = kYinThreads / 64;
   __shared__ float cum[kTauChunk];                             // running sum (tmp2) of a chunk
   __shared__ int s_found;
   __shared__ float s_level;
@@ -86,9 +90,12 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
       for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off);
       if ((tid & 63) == 0) cum[tid >> 6] = e;
       __syncthreads();
-      const float pe = (cum[0] + cum[1] + cum[2] + cum[3]) / (float)hop;
+      float ps = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kWaves; ++k) ps += cum[k];
+      const float pe = ps / (float)hop;
       const bool silent = 10.0f * log10f(pe) < silence_db - 1.0f;
-      __syncthreads();  // cum[0..3] read by all before the tau passes reuse it
+      __syncthreads();  // cum[0..kWaves) read by all before the tau passes reuse it
       if (silent) {
         if (tid == 0) f0_out[g] = 0.0f;
         continue;
@@ -285,9 +292,15 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
     const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
     const int64_t grid = std::min<int64_t>(total_hops, cap);
-    yin_hops_kernel<<<dim3((unsigned)grid), dim3(kYinThreads), 0, stream>>>(
-        pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate, f0_out,
-        total_hops);
+    static const int nt = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 128;
+    if (nt == 256)
+      yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(
+          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate,
+          f0_out, total_hops);
+    else
+      yin_hops_kernel<128><<<dim3((unsigned)grid), dim3(128), 0, stream>>>(
+          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate,
+          f0_out, total_hops);
     JANUS_LAUNCH_CHECK();
   }
   prosody_reduce_kernel<<<dim3(B), dim3(256), 0, stream>>>(pcm, sample_off, hop_off, f0_out, rms_out,
