@@ -6,6 +6,7 @@
 // stay in registers; 64-key K and V tiles are staged in LDS (V transposed on the way
 // in so P·V reads 16-byte B fragments); P goes through a per-wave LDS tile to become
 // the A operand. The S = QK^T score matrix is never materialised in HBM.
+#include <cstdlib>
 #include "mfma.h"
 #include "kernels.h"
 
@@ -149,11 +150,190 @@ __global__ __launch_bounds__(256) void attention_kernel(const _Float16* __restri
   }
 }
 
+// Encoder attention, transposed-score form. Each wave owns 32 queries (two 16-query
+// groups) and computes S^T = K Q^T, so the MFMA output puts one query per lane (column
+// l & 15) and 16 keys per lane (rows 4(l>>4) + r of the 4 key tiles): the online softmax
+// needs two cross-lane shuffles per tile instead of four per row, and the exponentials
+// feed O^T += V^T P^T straight from registers — lane l's own 8 probabilities of a 32-key
+// chunk ARE its B fragment, under the key order k = 8g + j <-> key 16(2c + j/4) + 4g + j%4
+// (g = l >> 4); the V^T A fragments are read from LDS in that same order (two 8-byte
+// reads). No P round trip through LDS. K / V^T tiles are double-buffered in LDS with the
+// next tile's global loads in flight during this tile's MFMAs (one barrier per tile);
+// each thread stages key pairs so the transposed V writes are 4-byte and conflict-free.
+constexpr int kSQW = 32;            // queries per wave
+constexpr int kSQB = 4 * kSQW;      // queries per block
+constexpr int kSKT = 64;            // keys per tile
+constexpr int kSLK = kHd + 8;       // sK pitch (halves): 36 dwords, conflict-free 16-B reads
+constexpr int kSLV = kSKT + 8;      // sVt pitch (halves): 36 dwords
+
+__global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __restrict__ qkv,
+                                                           _Float16* __restrict__ out, int T,
+                                                           int H, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) _Float16 sK[2][kSKT * kSLK];
+  __shared__ __attribute__((aligned(16))) _Float16 sVt[2][kHd * kSLV];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int g = lane >> 4, lr = lane & 15;
+  const int d = H * kHd;
+  const int64_t ld = 3 * (int64_t)d;
+  const _Float16* base = qkv + (int64_t)b * T * ld + h * kHd;
+  const int q0 = blockIdx.x * kSQB + w * kSQW;
+
+  // Q^T B fragments: query q0 + 16 qg + lr, dims 32 ks + 8 g .. +7
+  half8 qb[2][2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int qr = q0 + 16 * qg + lr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qb[qg][ks] = qr < T ? *reinterpret_cast<const half8*>(base + (int64_t)qr * ld + ks * 32 + 8 * g)
+                          : zero_half8();
+  }
+
+  // staging: thread -> (16-byte dim chunk sc, key pair kp); keys 2kp, 2kp + 1
+  const int sc = tid >> 5, kp = tid & 31;
+  uint4 pk[2], pv[2];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int kr = k0 + 2 * kp + e;
+      const bool ok = kr < T;
+      const _Float16* rowp = base + (int64_t)(ok ? kr : 0) * ld + sc * 8;
+      pk[e] = ok ? *reinterpret_cast<const uint4*>(rowp + d) : make_uint4(0, 0, 0, 0);
+      pv[e] = ok ? *reinterpret_cast<const uint4*>(rowp + 2 * d) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      *reinterpret_cast<uint4*>(&sK[buf][(2 * kp + e) * kSLK + sc * 8]) = pk[e];
+    const _Float16* v0 = reinterpret_cast<const _Float16*>(&pv[0]);
+    const _Float16* v1 = reinterpret_cast<const _Float16*>(&pv[1]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __attribute__((ext_vector_type(2))) _Float16 pr = {v0[j], v1[j]};
+      *reinterpret_cast<decltype(pr)*>(&sVt[buf][(sc * 8 + j) * kSLV + 2 * kp]) = pr;
+    }
+  };
+
+  f32x4 o[2][4];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[qg][m] = zero_f32x4();
+  float mq[2] = {-INFINITY, -INFINITY}, lq[2] = {0.f, 0.f};
+
+  const int ntiles = (T + kSKT - 1) / kSKT;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1, k0 = t * kSKT;
+    if (t + 1 < ntiles) load_tile(k0 + kSKT);  // in flight during this tile
+    const _Float16* K = sK[buf];
+    const _Float16* Vt = sVt[buf];
+
+    // S^T tiles: rows = keys 16n + 4g + r, column = query lr
+    f32x4 st[2][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const half8 ka0 = *reinterpret_cast<const half8*>(K + (16 * n + lr) * kSLK + 8 * g);
+      const half8 ka1 = *reinterpret_cast<const half8*>(K + (16 * n + lr) * kSLK + 32 + 8 * g);
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        st[qg][n] = mfma16(ka0, qb[qg][0], zero_f32x4());
+        st[qg][n] = mfma16(ka1, qb[qg][1], st[qg][n]);
+      }
+    }
+    // V^T A fragments for dim tile m, chunk c (keys in the B-fragment order)
+    half8 va[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const _Float16* vr = Vt + (16 * m + lr) * kSLV + 32 * c + 4 * g;
+        const half4 lo = *reinterpret_cast<const half4*>(vr);
+        const half4 hi = *reinterpret_cast<const half4*>(vr + 16);
+        va[m][c] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+
+    const bool tail = k0 + kSKT > T;  // block-uniform: only the last tile masks keys
+    if (tail) {
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + 16 * n + 4 * g + r >= T) st[qg][n][r] = -INFINITY;
+    }
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      // max on raw scores (the scale is positive); p = exp2(s * scale - m) as one fma
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, st[qg][n][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mn = fmaxf(mq[qg], tmax * scale_log2);
+      const float alpha = __builtin_amdgcn_exp2f(mq[qg] - mn);  // mq = -inf on the first tile -> 0
+      mq[qg] = mn;
+      float ls = 0.f;
+      half8 pb[2];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv_ = __builtin_amdgcn_exp2f(fmaf(st[qg][n][r], scale_log2, -mn));
+          ls += pv_;
+          pb[n >> 1][4 * (n & 1) + r] = (_Float16)pv_;
+        }
+      lq[qg] = lq[qg] * alpha + ls;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[qg][m][r] *= alpha;
+        o[qg][m] = mfma16(va[m][0], pb[0], o[qg][m]);
+        o[qg][m] = mfma16(va[m][1], pb[1], o[qg][m]);
+      }
+    }
+    if (t + 1 < ntiles) store_tile(buf ^ 1);  // its readers finished before the last barrier
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    float l = lq[qg];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const int qr = q0 + 16 * qg + lr;
+    if (qr >= T) continue;
+    const float inv = 1.0f / l;
+    _Float16* orow = out + ((int64_t)b * T + qr) * d + h * kHd;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const half4 hv = {(_Float16)(o[qg][m][0] * inv), (_Float16)(o[qg][m][1] * inv),
+                        (_Float16)(o[qg][m][2] * inv), (_Float16)(o[qg][m][3] * inv)};
+      *reinterpret_cast<half4*>(orow + 16 * m + 4 * g) = hv;
+    }
+  }
+}
+
 void attention_launch(const _Float16* qkv, _Float16* out, int B, int T, int H, float scale,
                       hipStream_t s) {
   if (B <= 0 || T <= 0) return;
-  dim3 grid((T + kQT - 1) / kQT, H, B);
-  attention_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
+  // JANUS_ATTN_V1: the first form (P through LDS, one query row per 4 lanes' registers)
+  static const bool v1 = std::getenv("JANUS_ATTN_V1") != nullptr;
+  if (v1) {
+    dim3 grid((T + kQT - 1) / kQT, H, B);
+    attention_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
+  } else {
+    dim3 grid((T + kSQB - 1) / kSQB, H, B);
+    attention_st_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
+  }
   JANUS_LAUNCH_CHECK();
 }
 

@@ -141,22 +141,9 @@ class JanusPipeline:
         main = torch.cuda.current_stream(pcm.device)
         hi = self._hi_stream(pcm.device)
         ds, vs = self._split_streams(pcm.device, dec_per_xcd)
-        hi.wait_stream(main)
-        with torch.cuda.stream(hi):
-            mel = w.logmel(pcm, offsets, B, 3)
-            enc = w.encode(mel)
-        vs.wait_stream(hi)
-        ds.wait_stream(hi)
-        prev = getattr(self, "_pending", None)
-        wav = pcm16 = None
         timing = os.environ.get("JANUS_OVERLAP_TIMING") is not None
-        yin_dec = os.environ.get("JANUS_YIN_SIDE", "voc") == "dec"
-        if timing:
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            ev[0].record(vs)
-            ev[2].record(ds)
-        pres = None
-
+        yin_side = os.environ.get("JANUS_YIN_SIDE", "voc")
+        yin_dec = yin_side == "dec"
         # YIN follows the vocoder on its own CUs: an uncapped grid lets the hardware balance
         # the uneven per-hop cost (early exit, silent hops) over them
         yin_blocks = int(os.environ.get("JANUS_YIN_BLOCKS", "0"))
@@ -166,10 +153,27 @@ class JanusPipeline:
                 return prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
+        pres = None
+        hi.wait_stream(main)
+        if yin_side == "early":  # on the vocoder's CUs, beside the (high-priority) encoder
+            vs.wait_stream(main)
+            with torch.cuda.stream(vs):
+                pres = yin()
+        with torch.cuda.stream(hi):
+            mel = w.logmel(pcm, offsets, B, 3)
+            enc = w.encode(mel)
+        vs.wait_stream(hi)
+        ds.wait_stream(hi)
+        prev = getattr(self, "_pending", None)
+        wav = pcm16 = None
+        if timing:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(vs)
+            ev[2].record(ds)
         with torch.cuda.stream(vs):
             if prev is not None:
                 wav, pcm16, _ = self.decode(prev, frames)
-            if not yin_dec:
+            if yin_side == "voc":
                 pres = yin()
             if timing:
                 ev[1].record(vs)  # before the decoder call, which blocks the host
