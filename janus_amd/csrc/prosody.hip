@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
   __shared__ __attribute__((aligned(16))) float dd[kYinLen];   // d(tau), then yin(tau)
   constexpr int kTauChunk = kYinThreads * 2;
   constexpr int kWaves = kYinThreads / 64;
-  __shared__ float cum[kTauChunk];                             // running sum (tmp2) of a chunk
+  __shared__ __attribute__((aligned(16))) float cum[kTauChunk];                           // running sum (tmp2) of a chunk
   __shared__ int s_found;
   __shared__ float s_level;
   __shared__ unsigned long long s_best;  // argmin key
@@ -133,12 +133,37 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
       dd[tau0 + 0] = acc0;
       dd[tau0 + 1] = acc1;
       __syncthreads();
-      // tmp2 += yin[tau] in tau order (pitchyin.c), one lane.
+      // tmp2 += yin[tau] in tau order (pitchyin.c), one lane. 16 taus per batch through
+      // 16-byte LDS reads / writes: the add chain stays sequential (bit-exact), but one LDS
+      // round trip now serves 16 adds instead of one (the per-tau read->add->write loop
+      // was latency-bound at ~100 cycles a tau). tau = 0 adds nothing (cum[0] unread).
       if (tid == 0) {
-        const int t_begin = chunk == 0 ? 1 : chunk * kTauChunk;
-        for (int t = t_begin; t < (chunk + 1) * kTauChunk; ++t) {
-          running = __fadd_rn(running, dd[t]);
-          cum[t - chunk * kTauChunk] = running;
+        const float4* d4 = reinterpret_cast<const float4*>(dd + chunk * kTauChunk);
+        float4* c4 = reinterpret_cast<float4*>(cum);
+        float4 nxt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nxt[q] = d4[q];
+        for (int bt = 0; bt < kTauChunk / 16; ++bt) {
+          float4 cur[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+          if (bt + 1 < kTauChunk / 16) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nxt[q] = d4[4 * (bt + 1) + q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 o;
+            running = (chunk == 0 && bt == 0 && q == 0) ? running : __fadd_rn(running, cur[q].x);
+            o.x = running;
+            running = __fadd_rn(running, cur[q].y);
+            o.y = running;
+            running = __fadd_rn(running, cur[q].z);
+            o.z = running;
+            running = __fadd_rn(running, cur[q].w);
+            o.w = running;
+            c4[4 * bt + q] = o;
+          }
         }
       }
       __syncthreads();
