@@ -75,8 +75,25 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     const int64_t n = sample_off[b + 1] - base;
     const float* st = state_in ? state_in + (int64_t)b * kYinBuf : nullptr;
 
-    for (int k = tid; k < kYinBuf; k += kYinThreads)
-      w[k] = window_sample(pcm, base, n, st, i, hop, k);
+    {
+      // all of this thread's window loads in flight at once (a load -> wait -> LDS store
+      // per sample serialised 32 global round trips per hop): clamped addresses, no
+      // branches, out-of-range samples zeroed after the load
+      constexpr int kPer = kYinBuf / kYinThreads;
+      const int64_t p0 = (i + 1) * (int64_t)hop - kYinBuf;
+      float v[kPer];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int64_t p = p0 + tid + u * kYinThreads;
+        const bool in_pcm = p >= 0 && p < n;
+        const bool in_st = p < 0 && st != nullptr;
+        const float* src = in_pcm ? pcm + base + p : (in_st ? st + kYinBuf + p : pcm);
+        v[u] = *src;
+        v[u] = (in_pcm || in_st) ? v[u] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) w[tid + u * kYinThreads] = v[u];
+    }
     if (tid == 0) s_found = 0x7fffffff;
     __syncthreads();
 
