@@ -145,8 +145,9 @@ def main():
 
     def step():
         if args.overlap > 0:
-            # steady-state serving pipeline: encode batch i, vocode batch i-1 (the warm-up
-            # step primes it, so every timed step carries a full encode and a full decode)
+            # steady-state serving pipeline: batch i through mel / encoder / decoder / YIN,
+            # batch i-1 through packets and the vocoder (the warm-up step primes it, so
+            # every timed step carries a full encode and a full decode)
             enc, wav, pcm16 = pipe.step_overlapped(pcm, offs, lengths, frames, args.overlap)
         else:
             enc, wav, pcm16 = pipe.step(pcm, offs, lengths, frames)

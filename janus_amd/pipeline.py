@@ -127,15 +127,18 @@ class JanusPipeline:
 
     def step_overlapped(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
                         mode=JanusMode.SEMANTIC_VOICE, override="auto", timestamp=None):
-        """One serving step of a two-stage pipeline: encode batch i while the vocoder
-        renders the packets of batch i-1 (kept from the previous call).
+        """One serving step of a two-stage pipeline: batch i goes through mel, encoder,
+        greedy decoder and YIN; batch i-1 (kept from the previous call) through
+        detokenisation, packets and the vocoder. Returns (EncodeResult, wav, pcm16) of
+        batch i-1 — (None, None, None) on the first call; `flush` returns the last batch.
 
-        Mel + encoder (compute-bound) get the whole GPU; then the greedy decoder of batch
-        i (latency-bound) runs on a CU-masked stream holding `dec_per_xcd` CUs of each XCD,
-        and the vocoder of batch i-1 followed by this batch's YIN on the disjoint rest, so
-        neither holds the CUs the other needs (an unmasked overlap measured slower: the
-        vocoder's long-running blocks delay every decoder launch). Returns
-        (EncodeResult of batch i, wav / pcm16 of batch i-1 or None)."""
+        Mel + encoder (compute-bound) get the whole GPU, and the host finishes batch i-1
+        (transcripts, tags, MessagePack packets: a few ms) while they run. Then the greedy
+        decoder of batch i (latency-bound) runs on a CU-masked stream holding
+        `dec_per_xcd` CUs of each XCD, and the vocoder of batch i-1 followed by batch i's
+        YIN on the disjoint rest, so neither holds the CUs the other needs (an unmasked
+        overlap measured slower: the vocoder's long-running blocks delay every decoder
+        launch)."""
         B = len(lengths)
         w = self.whisper
         main = torch.cuda.current_stream(pcm.device)
@@ -143,7 +146,6 @@ class JanusPipeline:
         ds, vs = self._split_streams(pcm.device, dec_per_xcd)
         timing = os.environ.get("JANUS_OVERLAP_TIMING") is not None
         yin_side = os.environ.get("JANUS_YIN_SIDE", "voc")
-        yin_dec = yin_side == "dec"
         # YIN follows the vocoder on its own CUs: an uncapped grid lets the hardware balance
         # the uneven per-hop cost (early exit, silent hops) over them
         yin_blocks = int(os.environ.get("JANUS_YIN_BLOCKS", "0"))
@@ -162,23 +164,27 @@ class JanusPipeline:
         with torch.cuda.stream(hi):
             mel = w.logmel(pcm, offsets, B, 3)
             enc = w.encode(mel)
+        # batch i-1 on the host while the encoder runs (its tensors were joined into the
+        # caller's stream at the end of the previous call)
+        prev = getattr(self, "_pending", None)
+        self._pending = None
+        res_prev = self._finish(*prev) if prev is not None else None
         vs.wait_stream(hi)
         ds.wait_stream(hi)
-        prev = getattr(self, "_pending", None)
         wav = pcm16 = None
         if timing:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             ev[0].record(vs)
             ev[2].record(ds)
         with torch.cuda.stream(vs):
-            if prev is not None:
-                wav, pcm16, _ = self.decode(prev, frames)
+            if res_prev is not None:
+                wav, pcm16, _ = self.decode(res_prev.packets, frames)
             if yin_side == "voc":
                 pres = yin()
             if timing:
                 ev[1].record(vs)  # before the decoder call, which blocks the host
         with torch.cuda.stream(ds):
-            if yin_dec:
+            if yin_side == "dec":
                 pres = yin()
             # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339 ms)
             tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4)
@@ -190,23 +196,30 @@ class JanusPipeline:
             torch.cuda.synchronize()
             print(f"[overlap] vocoder side {ev[0].elapsed_time(ev[1]):.1f} ms, decoder side "
                   f"{ev[2].elapsed_time(ev[3]):.1f} ms", file=sys.stderr, flush=True)
+        self._pending = (tokens, ntok, pres, B, mode, override, timestamp)
+        return res_prev, wav, pcm16
+
+    def _finish(self, tokens, ntok, pres, B, mode, override, timestamp) -> EncodeResult:
+        """Host tail of an encode: transcripts, prosody tags (fallback Normal/Normal,
+        engine.py:520-525), packets (engine.py:527-548)."""
         try:
             tags = pres.tags() if pres is not None else None
         except Exception:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts = w.texts(tokens)
+        texts = self.whisper.texts(tokens)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
-        self._pending = packets
-        return EncodeResult(texts, tags, packets, tokens, ntok), wav, pcm16
+        return EncodeResult(texts, tags, packets, tokens, ntok)
 
     def flush(self, frames):
-        """Render the packets the last overlapped step left pending."""
+        """Finish and render the batch the last overlapped step left pending:
+        (EncodeResult, wav, pcm16), or (None, None, None)."""
         prev, self._pending = getattr(self, "_pending", None), None
         if prev is None:
-            return None, None
-        wav, pcm16, _ = self.decode(prev, frames)
-        return wav, pcm16
+            return None, None, None
+        res = self._finish(*prev)
+        wav, pcm16, _ = self.decode(res.packets, frames)
+        return res, wav, pcm16

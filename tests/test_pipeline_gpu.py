@@ -67,16 +67,13 @@ def test_overlapped_step_matches_sequential(gpu):
         enc = pipe.encode(pcm, offs, lengths, timestamp=5.0)
         wav, pcm16, _ = pipe.decode(enc.packets, frames)
         seq.append((enc.packets, wav, pcm16))
-    ov_packets, ov_wavs = [], []
-    for pcm, offs, lengths in batches:
-        enc, wav, pcm16 = pipe.step_overlapped(pcm, offs, lengths, frames, 16, timestamp=5.0)
-        ov_packets.append(enc.packets)
-        ov_wavs.append((wav, pcm16))
-    ov_wavs.append(pipe.flush(frames))
-    assert ov_wavs[0] == (None, None)  # nothing pending before the first step
+    outs = [pipe.step_overlapped(pcm, offs, lengths, frames, 16, timestamp=5.0)
+            for pcm, offs, lengths in batches]
+    outs.append(pipe.flush(frames))
+    assert outs[0] == (None, None, None)  # nothing pending before the first step
     for i in range(2):
-        assert ov_packets[i] == seq[i][0]
-        wav, pcm16 = ov_wavs[i + 1]
+        res, wav, pcm16 = outs[i + 1]  # batch i finishes one step later
+        assert res.packets == seq[i][0]
         if seq[i][1] is None:
             assert wav is None
             continue
