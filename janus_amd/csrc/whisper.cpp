@@ -384,6 +384,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // (432.7 / 434.7 vs 435.9 / 434.6 ms per bench step, unconditional 16-byte prologue
   // loads): the prologue's round trip and row reductions cost what the launch saves.
   const bool ln_pro = B <= 64 && d <= 512 && !fused_ln && !ln_fuse && std::getenv("JANUS_LN_PROLOGUE") != nullptr;
+  // the embedding kernel owns whole rows (one block per utterance): it also writes the
+  // first layer's LayerNorm of its row, one launch fewer per position
+  // (JANUS_NO_EMBED_LN restores the separate launch)
+  const bool embed_ln = !fused_ln && !ln_fuse && !ln_pro && d <= 512 &&
+                        std::getenv("JANUS_NO_EMBED_LN") == nullptr;
   auto with_ln = [&](GemmArgs g, const float* lg, const float* lb) {
     if (ln_pro) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
     return g;
@@ -402,7 +407,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   auto step = [&](int pos) {
     embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
                  fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
-                 ln_fuse ? a : nullptr);
+                 (ln_fuse || embed_ln) ? a : nullptr);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = Z.d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
@@ -413,7 +418,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
-        if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
+        if (!ln_fuse && !ln_pro && !(embed_ln && l == 0))
+          layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
         if (B <= 64) {
           GemmArgs g = with_ln(gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
                                L.ln1g, L.ln1b);
@@ -485,7 +491,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};
