@@ -68,7 +68,8 @@ class JanusPipeline:
             tokens, ntok, _ = w.decode(enc, self.max_length)
         main.wait_stream(hi)
         try:
-            tags = pres.tags() if pres is not None else None
+            parts = pres if isinstance(pres, tuple) else (pres,)
+            tags = None if any(p is None for p in parts) else [t for p in parts for t in p.tags()]
         except Exception:
             tags = None
         if tags is None:
@@ -150,11 +151,15 @@ class JanusPipeline:
         # the uneven per-hop cost (early exit, silent hops) over them
         yin_blocks = int(os.environ.get("JANUS_YIN_BLOCKS", "0"))
 
-        def yin():
+        def yin(u0=0, u1=B):
             try:
-                return prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=yin_blocks)
+                return prosody_launch(pcm, offsets[u0:u1 + 1], lengths[u0:u1], CAPTURE_RATE, 512,
+                                      max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
+        # the decoder side ends ~3 ms before the vocoder side: the YIN of the first few
+        # utterances runs there, after the decoder (JANUS_YIN_DEC_UTTS, default 4 of 64)
+        n_dec = min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "4"))) if yin_side == "voc" else 0
         pres = None
         hi.wait_stream(main)
         if yin_side == "early":  # on the vocoder's CUs, beside the (high-priority) encoder
@@ -180,7 +185,7 @@ class JanusPipeline:
             if res_prev is not None:
                 wav, pcm16, _ = self.decode(res_prev.packets, frames)
             if yin_side == "voc":
-                pres = yin()
+                pres = yin(n_dec, B)
             if timing:
                 ev[1].record(vs)  # before the decoder call, which blocks the host
         with torch.cuda.stream(ds):
@@ -188,6 +193,8 @@ class JanusPipeline:
                 pres = yin()
             # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339 ms)
             tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4)
+            if n_dec > 0:
+                pres = (yin(0, n_dec), pres)
         if timing:
             ev[3].record(ds)
         main.wait_stream(ds)
@@ -203,7 +210,8 @@ class JanusPipeline:
         """Host tail of an encode: transcripts, prosody tags (fallback Normal/Normal,
         engine.py:520-525), packets (engine.py:527-548)."""
         try:
-            tags = pres.tags() if pres is not None else None
+            parts = pres if isinstance(pres, tuple) else (pres,)
+            tags = None if any(p is None for p in parts) else [t for p in parts for t in p.tags()]
         except Exception:
             tags = None
         if tags is None:
