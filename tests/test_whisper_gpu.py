@@ -87,3 +87,20 @@ def test_greedy_teacher_forced(engine, gpu):
     assert agree >= 0.9 * total, (agree, total)
     texts = eng.texts(tokens)
     assert all(isinstance(s, str) for s in texts)
+
+
+def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
+    """Opt-in decoder lanes (JANUS_DEC_LANES: the batch split over concurrent streams and
+    host threads) decode every utterance exactly as the single-lane decoder does: rows
+    are independent through every decoder kernel."""
+    eng, _ = engine
+    utts = [synth_speech(60 + k, 3.0 + k) for k in range(5)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    monkeypatch.setenv("JANUS_DEC_LANES", "1")
+    t1, n1, _ = eng.decode(enc, 24)
+    t1, n1 = t1.cpu(), n1.cpu()
+    monkeypatch.setenv("JANUS_DEC_LANES", "2")
+    t2, n2, _ = eng.decode(enc, 24)
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
