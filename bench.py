@@ -153,7 +153,9 @@ def main():
             enc, wav, pcm16 = pipe.step(pcm, offs, lengths, frames)
         return enc
 
-    for _ in range(max(args.warmup, 1 if args.overlap > 0 else 0)):
+    # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
+    # pass), then the W warm-up steps, each a full encode + decode like the timed ones
+    for _ in range(args.warmup + (1 if args.overlap > 0 else 0)):
         enc = step()
     torch.cuda.synchronize()
     if world > 1:
