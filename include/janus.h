@@ -204,6 +204,8 @@ typedef struct {
   int check_every;         /* poll for all-rows-finished every N steps (0 = never) */
   int xattn_splits;        /* cross-attention key splits per utterance (0 = auto: 8; the
                               overlapped step on half the CUs runs best at 4) */
+  int logits_blocks;       /* vocabulary-projection blocks (0 = 256, one per CU): the CUs the
+                              decoder's stream may use, e.g. 128 on a half-GPU CU mask */
 } janus_decode_options;
 
 /*

@@ -53,13 +53,13 @@ void rules_init_launch(RowRules* rules, int B, hipStream_t s);
 // logits = A[B][K] . W[V][K]^T computed block-wise with the filtered statistics reduced
 // in the epilogue (no logits in HBM); nblk = logits_partial_blocks(V) merged partials per row
 // (one per block of the launch).
-int logits_partial_blocks(int V, int K);
+int logits_partial_blocks(int V, int K, int max_blocks = 256);
 // lnx: A = LayerNorm(lnx) (fp32 [B][K], eps 1e-5) computed in-block instead of read
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s,
                            const float* lnx = nullptr, int ldx = 0, const float* ln_g = nullptr,
-                           const float* ln_b = nullptr);
+                           const float* ln_b = nullptr, int max_blocks = 256);
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
                             float* sum_lp, int32_t* n_tok, int B, hipStream_t s);

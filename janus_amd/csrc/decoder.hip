@@ -327,8 +327,9 @@ void rules_init_launch(RowRules* rules, int B, hipStream_t s) {
 // waves per logits block (16 waves — about one tile per wave — measured 4x slower:
 // 114.7 vs 28.8 us per launch)
 constexpr int lg_waves(int /*K*/) { return 8; }
-int logits_partial_blocks(int V, int K) {
-  return std::min(256, ((V + 15) / 16 + lg_waves(K) - 1) / lg_waves(K));
+int logits_partial_blocks(int V, int K, int max_blocks) {
+  const int cap = max_blocks > 0 ? max_blocks : 256;  // one per CU of a whole MI355X
+  return std::max(1, std::min(cap, ((V + 15) / 16 + lg_waves(K) - 1) / lg_waves(K)));
 }
 
 __device__ __forceinline__ float lse_merge(float m1, float s1, float m2, float s2, float* mo) {
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s, const float* lnx, int ldx,
-                           const float* ln_g, const float* ln_b) {
+                           const float* ln_g, const float* ln_b, int max_blocks) {
   JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
   const int ntiles = (V + 15) / 16;
   const int nw = lg_waves(K);
@@ -503,7 +504,7 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                                   160 * 1024));
     attr[ai] = true;
   }
-  const int grid = logits_partial_blocks(V, K);
+  const int grid = logits_partial_blocks(V, K, max_blocks);
   for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
     kern<<<grid, nw * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
                                           smask, rules + r0, parts + (int64_t)r0 * grid, ntiles,

@@ -294,7 +294,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   Z.d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
   Z.d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
-  const int nblk = logits_partial_blocks(V, d);
+  const int lg_cap = std::getenv("JANUS_LOGITS_BLOCKS") ? std::atoi(std::getenv("JANUS_LOGITS_BLOCKS"))
+                                                        : opt->logits_blocks;
+  const int nblk = logits_partial_blocks(V, d, lg_cap);
   Z.d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
   Z.d_rules.ensure(sizeof(RowRules) * B);
   float* part_o = Z.d_part_o.as<float>();
@@ -480,7 +482,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     if (!ln_fuse && !ln_pro) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
-                          ln_pro ? x : nullptr, d, fin_g, fin_b);
+                          ln_pro ? x : nullptr, d, fin_g, fin_b, lg_cap);
     select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                            maxlen, pos, done, sum_lp, n_tokens, B, s);
   };
@@ -491,7 +493,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)nblk, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};

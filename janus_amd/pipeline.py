@@ -157,9 +157,11 @@ class JanusPipeline:
                                       max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
-        # the decoder side ends ~3 ms before the vocoder side: the YIN of the first few
-        # utterances runs there, after the decoder (JANUS_YIN_DEC_UTTS, default 4 of 64)
-        n_dec = min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "4"))) if yin_side == "voc" else 0
+        # the decoder side would end a few ms before the vocoder side: the YIN of the first
+        # B/8 utterances runs there, after the decoder (JANUS_YIN_DEC_UTTS; 64 utterances:
+        # 0 / 4 / 8 / 11 -> 328.9 / 327.8 / 326.7 / 327.9 ms per step)
+        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(max(1, B // 8)))))
+                 if yin_side == "voc" else 0)
         pres = None
         hi.wait_stream(main)
         if yin_side == "early":  # on the vocoder's CUs, beside the (high-priority) encoder
@@ -191,8 +193,11 @@ class JanusPipeline:
         with torch.cuda.stream(ds):
             if yin_side == "dec":
                 pres = yin()
-            # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339 ms)
-            tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4)
+            # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339
+            # ms); the vocabulary projection at one block per CU of the decoder's partition
+            # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms)
+            tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4,
+                                       logits_blocks=self._dec_s.n_cus)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
         if timing:
