@@ -200,6 +200,7 @@ struct SkinnyArgs {
   _Float16* kc; _Float16* vc; int pos, n_ctx, qkv_d;
   float2* ln_part;
   int a_group_cols;
+  int msplit_n;
   const float* ln_g; const float* ln_b; float ln_eps; _Float16* ln_out; int* ln_cnt;
   const float* lnin_g; const float* lnin_b;  // AM_LNX: A = LayerNorm(x) computed in-block
 };
@@ -473,7 +474,7 @@ static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
     const char* e = std::getenv("JANUS_SKINNY_MSPLIT_N");
     return e ? std::atoi(e) : 2048;
   }();
-  if (p.N <= msplit_n) { launch_skinny_m<AM, 1>(epi, p, s); return; }
+  if (p.N <= (p.msplit_n > 0 ? p.msplit_n : msplit_n)) { launch_skinny_m<AM, 1>(epi, p, s); return; }
   launch_skinny_m<AM, 4>(epi, p, s);
 }
 
@@ -484,6 +485,7 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
   p.ln_part = g.ln_part;
   p.a_group_cols = g.a_group_cols;
+  p.msplit_n = g.msplit_n;
   p.ln_g = g.ln_g; p.ln_b = g.ln_b; p.ln_eps = g.ln_eps; p.ln_out = g.ln_out; p.ln_cnt = g.ln_cnt;
   if (g.lnin_x) {  // A = LayerNorm(x) in the block's prologue (K <= 512)
     JANUS_CHECK(g.K <= 512 && g.K % 4 == 0, "skinny LayerNorm prologue: K <= 512, K % 4 == 0");

@@ -22,6 +22,9 @@ struct GemmArgs {
   // grouped (block-diagonal) product, M <= 64 only: output columns [g*a_group_cols,
   // (g+1)*a_group_cols) read A columns [g*K, (g+1)*K) — per-head projections
   int a_group_cols = 0;
+  // M <= 64 only: outputs up to this many columns also split their rows over blocks
+  // (0 = JANUS_SKINNY_MSPLIT_N or 2048, tuned on a whole GPU; 1024 on a half-GPU CU mask)
+  int msplit_n = 0;
   // EPI_RESID_F32 (M <= 64 only): the LayerNorm of the NEW residual rows, fused: the
   // output rows are stored write-through (sc1), every block adds to ln_cnt once its
   // stores have drained, and the last block to arrive normalises all M rows (sc1 loads)

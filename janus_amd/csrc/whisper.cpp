@@ -294,8 +294,15 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   Z.d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
   Z.d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
+  // cu_count: the CUs the caller's stream may use (a CU-masked partition); 0 = all
   const int lg_cap = std::getenv("JANUS_LOGITS_BLOCKS") ? std::atoi(std::getenv("JANUS_LOGITS_BLOCKS"))
-                                                        : opt->logits_blocks;
+                                                        : opt->cu_count;
+  const int msplit_n = opt->cu_count > 0 && opt->cu_count <= 128 ? 1024 : 0;
+  auto dgargs = [&](auto&&... args) {
+    GemmArgs g = gargs(args...);
+    g.msplit_n = msplit_n;
+    return g;
+  };
   const int nblk = logits_partial_blocks(V, d, lg_cap);
   Z.d_parts.ensure(sizeof(LogitPart) * (int64_t)B * nblk);
   Z.d_rules.ensure(sizeof(RowRules) * B);
@@ -344,8 +351,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     DecLayer& L = w->dec[l];
     _Float16* ck = Z.d_ck.as<_Float16>() + (int64_t)l * Me * d;
     _Float16* cv = Z.d_cv.as<_Float16>() + (int64_t)l * Me * d;
-    gemm_launch(EPI_F16, gargs(enc, d, L.wk_c.as<_Float16>(), d, nullptr, ck, d, (int)Me, d, d), s);
-    gemm_launch(EPI_F16, gargs(enc, d, L.wv_c.as<_Float16>(), d, L.bv_c, cv, d, (int)Me, d, d), s);
+    gemm_launch(EPI_F16, dgargs(enc, d, L.wk_c.as<_Float16>(), d, nullptr, ck, d, (int)Me, d, d), s);
+    gemm_launch(EPI_F16, dgargs(enc, d, L.wv_c.as<_Float16>(), d, L.bv_c, cv, d, (int)Me, d, d), s);
   }
 
   DecodeRules R;
@@ -401,7 +408,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const float* fin_b = w->params.get("decoder.layer_norm.bias", d);
   auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias, const float* ng,
                    const float* nb) {
-    GemmArgs g = gargs(A, K, W.as<_Float16>(), K, bias, x, d, B, d, K, x, d);
+    GemmArgs g = dgargs(A, K, W.as<_Float16>(), K, bias, x, d, B, d, K, x, d);
     if (fused_ln) g.ln_part = lnp;
     if (ln_fuse) { g.ln_g = ng; g.ln_b = nb; g.ln_out = a; g.ln_cnt = Z.d_lncnt.as<int>(); }
     gemm_launch(EPI_RESID_F32, g, s);
@@ -423,12 +430,12 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         if (!ln_fuse && !ln_pro && !(embed_ln && l == 0))
           layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
         if (B <= 64) {
-          GemmArgs g = with_ln(gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
+          GemmArgs g = with_ln(dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
                                L.ln1g, L.ln1b);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
           gemm_launch(EPI_QKV, g, s);
         } else {
-          gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
+          gemm_launch(EPI_F16, dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
           kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
         }
       }
@@ -444,12 +451,12 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
         } else {
           if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-          gemm_launch(EPI_F16, with_ln(gargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
+          gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
                                        L.ln2g, L.ln2b), s);
         }
         xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s);
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
-        GemmArgs gv = gargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
+        GemmArgs gv = dgargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
         gv.a_group_cols = 64;
         gemm_launch(EPI_F16, gv, s);
         resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
@@ -459,7 +466,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                                                 nullptr, nullptr, pos), s);
         } else {
           if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
-          gemm_launch(EPI_F16, with_ln(gargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d),
+          gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d),
                                        L.ln2g, L.ln2b), s);
         }
         decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
@@ -471,7 +478,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
         if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
-        gemm_launch(EPI_GELU_F16, with_ln(gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d),
+        gemm_launch(EPI_GELU_F16, with_ln(dgargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d),
                                           L.ln3g, L.ln3b), s);
       }
       // next LayerNorm: the following layer's LN1, or the decoder's final LN
@@ -493,7 +500,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)nblk, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts};

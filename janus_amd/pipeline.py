@@ -194,10 +194,11 @@ class JanusPipeline:
             if yin_side == "dec":
                 pres = yin()
             # 4 key splits per utterance on half the CUs (sweep 4/6/8/12/16: 313/315/327/330/339
-            # ms); the vocabulary projection at one block per CU of the decoder's partition
-            # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms)
+            # ms); cu_count: the vocabulary projection at one block per CU of the partition
+            # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms) and row-split skinny
+            # projections from N <= 1024 (vs 2048: 310.5 -> 306.3 ms)
             tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4,
-                                       logits_blocks=self._dec_s.n_cus)
+                                       cu_count=self._dec_s.n_cus)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
         if timing:

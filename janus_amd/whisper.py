@@ -56,7 +56,7 @@ class janus_decode_options(ctypes.Structure):
                 ("suppress_blank", ctypes.c_int), ("blank_token", ctypes.c_int),
                 ("timestamp_begin", ctypes.c_int), ("no_timestamps", ctypes.c_int),
                 ("max_initial_timestamp_index", ctypes.c_int), ("check_every", ctypes.c_int),
-                ("xattn_splits", ctypes.c_int), ("logits_blocks", ctypes.c_int)]
+                ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int)]
 
 
 # ----------------------------------------------------------------- front end
@@ -225,7 +225,7 @@ class WhisperEngine:
         return enc
 
     def decode_options(self, max_length: int = 448, check_every: int = 16,
-                       timestamps: bool = True, xattn_splits: int = 0, logits_blocks: int = 0):
+                       timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0):
         t = self.tokenizer
         prompt = np.array(t.sot_sequence, np.int32)
         supp = np.array(t.suppress_tokens(), np.int32)
@@ -243,14 +243,14 @@ class WhisperEngine:
         opt.max_initial_timestamp_index = 50
         opt.check_every = check_every
         opt.xattn_splits = xattn_splits
-        opt.logits_blocks = logits_blocks
+        opt.cu_count = cu_count
         return opt, (prompt, supp)
 
     def decode(self, enc: torch.Tensor, max_length: int = 448, check_every: int = 16,
-               timestamps: bool = True, xattn_splits: int = 0, logits_blocks: int = 0):
+               timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0):
         B = enc.shape[0]
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits,
-                                        logits_blocks)
+                                        cu_count)
         tokens = torch.empty(B, max_length, dtype=torch.int32, device=self.device)
         ntok = torch.empty(B, dtype=torch.int32, device=self.device)
         slp = torch.empty(B, dtype=torch.float32, device=self.device)
