@@ -204,9 +204,10 @@ typedef struct {
   int check_every;         /* poll for all-rows-finished every N steps (0 = never) */
   int xattn_splits;        /* cross-attention key splits per utterance (0 = auto: 8; the
                               overlapped step on half the CUs runs best at 4) */
-  int cu_count;            /* CUs the decoder's stream may use (0 = all 256), e.g. 128 on a
-                              half-GPU CU mask: one vocabulary-projection block per CU, and
-                              at <= 128 the skinny projections split rows from N <= 1024 */
+  int cu_count;            /* CUs the decoder's stream may use (0 = the popcount of the
+                              stream's CU mask), e.g. 128 on a half-GPU partition: one
+                              vocabulary-projection block per CU, and at <= 128 the skinny
+                              projections split rows from N <= 1024 */
 } janus_decode_options;
 
 /*

@@ -1,4 +1,6 @@
 // C-ABI glue: error slot, version, thin extern "C" wrappers over the launchers.
+#include <map>
+#include <mutex>
 #include "common.h"
 #include "../../include/janus.h"
 
@@ -6,6 +8,26 @@ namespace janus {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+int stream_cu_count(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<hipStream_t, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(s);
+  if (it != cache.end()) return it->second;
+  uint32_t mask[32] = {};
+  int n = 0;
+  if (hipExtStreamGetCUMask(s, 32, mask) == hipSuccess)
+    for (uint32_t m : mask) n += __builtin_popcount(m);
+  if (n <= 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            ? prop.multiProcessorCount : 256;
+  }
+  cache[s] = n;
+  return n;
+}
 
 void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
                     int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,

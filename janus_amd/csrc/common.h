@@ -16,6 +16,11 @@ namespace janus {
 
 void set_error(const std::string& msg);
 
+// CUs a stream may dispatch to: the popcount of its CU mask (hipExtStreamGetCUMask; all
+// CUs for an unmasked stream). Cached per stream handle. Persistent / per-CU grids size
+// themselves with it, so a kernel on a half-GPU partition runs one round, not two.
+int stream_cu_count(hipStream_t s);
+
 struct Error : std::runtime_error {
   using std::runtime_error::runtime_error;
 };

@@ -294,10 +294,12 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const int max_split = std::max(decode_split_count(Te), decode_split_count(NC));
   Z.d_part_o.ensure(sizeof(float) * (int64_t)B * max_split * d);
   Z.d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
-  // cu_count: the CUs the caller's stream may use (a CU-masked partition); 0 = all
+  // cu_count: the CUs the caller's stream may use (a CU-masked partition); 0 = read it
+  // from the stream's CU mask
+  const int cus = opt->cu_count > 0 ? opt->cu_count : stream_cu_count(s);
   const int lg_cap = std::getenv("JANUS_LOGITS_BLOCKS") ? std::atoi(std::getenv("JANUS_LOGITS_BLOCKS"))
-                                                        : opt->cu_count;
-  const int msplit_n = opt->cu_count > 0 && opt->cu_count <= 128 ? 1024 : 0;
+                                                        : cus;
+  const int msplit_n = cus <= 128 ? 1024 : 0;
   auto dgargs = [&](auto&&... args) {
     GemmArgs g = gargs(args...);
     g.msplit_n = msplit_n;
