@@ -304,7 +304,13 @@ static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
   const int tiles_per_utt = (a.T + BM - 1) / BM;
   const int n_tiles = tiles_per_utt * a.B;
   const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / G::LDS)));
-  const int grid = std::min(n_tiles, 256 * per_cu);
+  // persistent grid: 1024 x blocks-per-CU — on the vocoder's 128-CU partition that is
+  // eight rounds of short tile stripes, which balances the uneven tile costs (edge tiles,
+  // HBM contention with the decoder) better than fewer, longer stripes. Sweep (vocoder
+  // side per step): 128 -> +3 ms, 256 -> 315.6, 512 -> 313.5, 1024 -> 312.2, 2048 -> 313,
+  // one block per tile -> 327.7 ms. JANUS_NARROW_GRID_CUS overrides the 1024.
+  static const int gcu = std::getenv("JANUS_NARROW_GRID_CUS") ? std::atoi(std::getenv("JANUS_NARROW_GRID_CUS")) : 1024;
+  const int grid = std::min(n_tiles, std::max(1, gcu) * per_cu);
   kern<<<grid, 256, G::LDS, s>>>(a, tiles_per_utt, n_tiles);
   JANUS_LAUNCH_CHECK();
 }
