@@ -347,7 +347,11 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
     const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
     const int64_t grid = std::min<int64_t>(total_hops, cap);
-    static const int nt = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 128;
+    // 128-thread blocks (256-tau passes) for an uncapped grid on its own CUs (overlapped
+    // step: 33.5 vs 36 ms); a capped grid beside the greedy decoder keeps the 256-thread
+    // blocks (back-to-back step: 422 vs 449 ms per step with 128)
+    static const int nt_env = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 0;
+    const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 128);
     if (nt == 256)
       yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(
           pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate,
