@@ -265,12 +265,35 @@ int janus_vocoder_frontend(janus_vocoder* v, const uint8_t* bytes, const int64_t
                            const int32_t* emotion_ids, int batch, int frames, uint16_t* latents,
                            void* stream);
 /*
+ * Same, plus a per-row voice term: latent += speaker[b] ([device] f32 [B][latent], or NULL
+ * for none). The voice stands in for the reference's voice cloning, which sends the
+ * hot-reloaded recording as references=[ReferenceAudio(audio, text="")] or, without one,
+ * reference_id="5196af35..." (synthesizer.py:179-200, :243-249).
+ */
+int janus_vocoder_frontend_ex(janus_vocoder* v, const uint8_t* bytes, const int64_t* byte_offsets,
+                              const int32_t* emotion_ids, const float* speaker, int batch,
+                              int frames, uint16_t* latents, void* stream);
+/*
+ * Voice embedding of reference recordings (the ReferenceAudio bytes of
+ * synthesizer.py:183-187, decoded to 16 kHz f32 by the caller): pcm16k [device] f32
+ * clips back to back, offsets [device] int64[B+1] (<= 30 s used per clip) ->
+ * speaker_out [device] f32 [B][latent] = speaker_bias + speaker_proj . mean over the
+ * clip's frames of its normalised Whisper log-mel. Needs the parameters
+ * "frontend.speaker_proj" [latent][80], "frontend.speaker_bias" [latent], "mel.basis"
+ * and "mel.filters" (as for janus_whisper_set_tensor).
+ */
+int janus_vocoder_speaker(janus_vocoder* v, const float* pcm16k, const int64_t* offsets, int batch,
+                          float* speaker_out, void* stream);
+/*
  * Generator forward: latents [device] fp16 [B][frames][latent] -> wav [device] f32
  * [B][frames*prod(up_rates)] in [-1, 1] and, if pcm != NULL, int16 [B][...]
  * (clip(round(32767*y))).
  */
 int janus_vocoder_forward(janus_vocoder* v, const uint16_t* latents, int batch, int frames,
                           float* wav, int16_t* pcm, void* stream);
+/* Same, plus pre_tanh [device] f32 [B][samples] (conv_post output before tanh; may be NULL). */
+int janus_vocoder_forward_ex(janus_vocoder* v, const uint16_t* latents, int batch, int frames,
+                             float* wav, int16_t* pcm, float* pre_tanh, void* stream);
 /* HIP-event timing of every conv launch (for roofline accounting). */
 int janus_vocoder_set_timing(janus_vocoder* v, int on);
 /* Accumulated conv FLOPs (2*Cin*Cout*taps*rows), kernel milliseconds and launches. */

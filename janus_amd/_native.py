@@ -68,7 +68,10 @@ SIGNATURES = {
     "janus_vocoder_destroy": [_P],
     "janus_vocoder_set_tensor": [_P, ctypes.c_char_p, _P, _I64],
     "janus_vocoder_frontend": [_P, _P, _P, _P, _I32, _I32, _P, _P],
+    "janus_vocoder_frontend_ex": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P],
+    "janus_vocoder_speaker": [_P, _P, _P, _I32, _P, _P],
     "janus_vocoder_forward": [_P, _P, _I32, _I32, _P, _P, _P],
+    "janus_vocoder_forward_ex": [_P, _P, _I32, _I32, _P, _P, _P, _P],
     "janus_vocoder_set_timing": [_P, _I32],
     "janus_vocoder_conv_stats": [_P, _P, _P, _P, _I32],
     # include/janus_kernels.h

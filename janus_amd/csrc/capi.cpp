@@ -9,12 +9,9 @@ namespace janus {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+// Not cached: a destroyed CU-masked stream's handle can be reused by a new stream with a
+// different mask, and the query is cheap next to a decode.
 int stream_cu_count(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<hipStream_t, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(s);
-  if (it != cache.end()) return it->second;
   uint32_t mask[32] = {};
   int n = 0;
   if (hipExtStreamGetCUMask(s, 32, mask) == hipSuccess)
@@ -25,7 +22,6 @@ int stream_cu_count(hipStream_t s) {
     n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
             ? prop.multiProcessorCount : 256;
   }
-  cache[s] = n;
   return n;
 }
 

@@ -55,6 +55,7 @@ struct janus_vocoder {
   const float* post_w = nullptr;
   float post_b = 0.f;
   janus::DevMem buf[5];
+  janus::DevMem spk_logmel, spk_maxkey;  // speaker-conditioning workspace
   // timing
   bool timing = false;
   std::vector<janus::TimedLaunch> pending;
@@ -185,7 +186,7 @@ static void run_unit(janus_vocoder* v, const VUnit& U, const _Float16* x, _Float
 }
 
 static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* wav, int16_t* pcm,
-                    hipStream_t s) {
+                    float* pre_tanh, hipStream_t s) {
   const auto& c = v->cfg;
   int64_t maxel = (int64_t)F * c.channels;
   {
@@ -240,7 +241,7 @@ static void forward(janus_vocoder* v, const _Float16* lat, int B, int F, float* 
       }
     }
   }
-  conv_post_launch(H, B, T, v->post_w, v->post_b, wav, pcm, s, /*pre_silu=*/0);
+  conv_post_launch(H, B, T, v->post_w, v->post_b, wav, pcm, s, /*pre_silu=*/0, pre_tanh);
 }
 
 static void collect_timing(janus_vocoder* v) {
@@ -294,9 +295,10 @@ extern "C" int janus_vocoder_set_tensor(janus_vocoder* v, const char* name, cons
   });
 }
 
-extern "C" int janus_vocoder_frontend(janus_vocoder* v, const uint8_t* bytes,
-                                      const int64_t* byte_offsets, const int32_t* emotion_ids,
-                                      int batch, int frames, uint16_t* latents, void* stream) {
+extern "C" int janus_vocoder_frontend_ex(janus_vocoder* v, const uint8_t* bytes,
+                                         const int64_t* byte_offsets, const int32_t* emotion_ids,
+                                         const float* speaker, int batch, int frames,
+                                         uint16_t* latents, void* stream) {
   return guarded([&] {
     JANUS_CHECK(v && byte_offsets && emotion_ids && latents, "null argument");
     std::lock_guard<std::mutex> lk(v->mu);
@@ -304,21 +306,55 @@ extern "C" int janus_vocoder_frontend(janus_vocoder* v, const uint8_t* bytes,
     frontend_launch(bytes, byte_offsets, emotion_ids,
                     v->params.get("frontend.text_embed", 256 * (int64_t)c.latent_dim),
                     v->params.get("frontend.emotion_embed", (int64_t)c.n_emotions * c.latent_dim),
-                    batch, frames, c.latent_dim, reinterpret_cast<_Float16*>(latents),
+                    speaker, batch, frames, c.latent_dim, reinterpret_cast<_Float16*>(latents),
                     (hipStream_t)stream);
   });
 }
 
-extern "C" int janus_vocoder_forward(janus_vocoder* v, const uint16_t* latents, int batch,
-                                     int frames, float* wav, int16_t* pcm, void* stream) {
+extern "C" int janus_vocoder_frontend(janus_vocoder* v, const uint8_t* bytes,
+                                      const int64_t* byte_offsets, const int32_t* emotion_ids,
+                                      int batch, int frames, uint16_t* latents, void* stream) {
+  return janus_vocoder_frontend_ex(v, bytes, byte_offsets, emotion_ids, nullptr, batch, frames,
+                                   latents, stream);
+}
+
+extern "C" int janus_vocoder_speaker(janus_vocoder* v, const float* pcm16k, const int64_t* offsets,
+                                     int batch, float* speaker_out, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(v && pcm16k && offsets && speaker_out, "null argument");
+    JANUS_CHECK(batch >= 1, "speaker: batch must be >= 1");
+    std::lock_guard<std::mutex> lk(v->mu);
+    const auto& c = v->cfg;
+    hipStream_t s = (hipStream_t)stream;
+    constexpr int kFrames = 3000;  // one 30 s Whisper window at 16 kHz
+    v->spk_logmel.ensure(sizeof(float) * (int64_t)batch * kFrames * 80);
+    v->spk_maxkey.ensure(sizeof(uint32_t) * batch);
+    mel_launch(pcm16k, offsets, batch, v->params.get("mel.basis", 400 * 416),
+               v->params.get("mel.filters", 208 * 80), v->spk_logmel.as<float>(),
+               v->spk_maxkey.as<uint32_t>(), kFrames, 1, s);
+    speaker_launch(v->spk_logmel.as<float>(), v->spk_maxkey.as<uint32_t>(), offsets, batch, kFrames,
+                   v->params.get("frontend.speaker_proj", (int64_t)c.latent_dim * 80),
+                   v->params.get("frontend.speaker_bias", c.latent_dim), c.latent_dim, speaker_out,
+                   s);
+  });
+}
+
+extern "C" int janus_vocoder_forward_ex(janus_vocoder* v, const uint16_t* latents, int batch,
+                                        int frames, float* wav, int16_t* pcm, float* pre_tanh,
+                                        void* stream) {
   return guarded([&] {
     JANUS_CHECK(v && latents && wav, "null argument");
     std::lock_guard<std::mutex> lk(v->mu);
     hipStream_t s = (hipStream_t)stream;
     prepare(v, s);
     if (batch <= 0 || frames <= 0) return;
-    forward(v, reinterpret_cast<const _Float16*>(latents), batch, frames, wav, pcm, s);
+    forward(v, reinterpret_cast<const _Float16*>(latents), batch, frames, wav, pcm, pre_tanh, s);
   });
+}
+
+extern "C" int janus_vocoder_forward(janus_vocoder* v, const uint16_t* latents, int batch,
+                                     int frames, float* wav, int16_t* pcm, void* stream) {
+  return janus_vocoder_forward_ex(v, latents, batch, frames, wav, pcm, nullptr, stream);
 }
 
 extern "C" int janus_vocoder_set_timing(janus_vocoder* v, int on) {

@@ -13,8 +13,8 @@ namespace janus {
 
 __global__ void frontend_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ boff,
                                 const int32_t* __restrict__ emo, const float* __restrict__ e_text,
-                                const float* __restrict__ e_emo, int F, int C,
-                                _Float16* __restrict__ lat) {
+                                const float* __restrict__ e_emo, const float* __restrict__ spk,
+                                int F, int C, _Float16* __restrict__ lat) {
   const int f = blockIdx.x, b = blockIdx.y;
   const int64_t n = boff[b + 1] - boff[b];
   const float* et = nullptr;
@@ -23,15 +23,65 @@ __global__ void frontend_kernel(const uint8_t* __restrict__ bytes, const int64_t
     et = e_text + (int64_t)bytes[boff[b] + j] * C;
   }
   const float* ee = e_emo + (int64_t)emo[b] * C;
+  const float* sp = spk ? spk + (int64_t)b * C : nullptr;
   _Float16* o = lat + ((int64_t)b * F + f) * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) o[c] = (_Float16)((et ? et[c] : 0.0f) + ee[c]);
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    o[c] = (_Float16)(((et ? et[c] : 0.0f) + ee[c]) + (sp ? sp[c] : 0.0f));
 }
 
 void frontend_launch(const uint8_t* bytes, const int64_t* boff, const int32_t* emo,
-                     const float* e_text, const float* e_emo, int B, int F, int C, _Float16* lat,
-                     hipStream_t s) {
+                     const float* e_text, const float* e_emo, const float* spk, int B, int F, int C,
+                     _Float16* lat, hipStream_t s) {
   if (B <= 0 || F <= 0) return;
-  frontend_kernel<<<dim3(F, B), 256, 0, s>>>(bytes, boff, emo, e_text, e_emo, F, C, lat);
+  frontend_kernel<<<dim3(F, B), 256, 0, s>>>(bytes, boff, emo, e_text, e_emo, spk, F, C, lat);
+  JANUS_LAUNCH_CHECK();
+}
+
+// Speaker (voice-cloning) conditioning, build-defined: the reference hands its reference
+// recording to the cloud TTS as references=[ReferenceAudio(audio, text="")]
+// (synthesizer.py:183-200). Locally the recording's Whisper log-mel (mel_kernel, 16 kHz)
+// is averaged over the frames that hold audio and projected to the latent width:
+//   spk[b][c] = bias[c] + sum_m P[c][m] * mean_f norm(logmel[b][f][m]),
+//   norm(v) = (max(v, gmax_b - 8) + 4) / 4  (the encoder's own normalisation).
+// One block per clip; HBM/latency-bound (<= 3000 x 80 floats read).
+__global__ __launch_bounds__(256) void speaker_kernel(const float* __restrict__ logmel,
+                                                      const uint32_t* __restrict__ maxkey,
+                                                      const int64_t* __restrict__ offsets,
+                                                      int frames, const float* __restrict__ P,
+                                                      const float* __restrict__ bias, int C,
+                                                      float* __restrict__ spk) {
+  constexpr int kM = 80, kPh = 3;  // 240 threads: (frame phase, mel bin)
+  __shared__ float part[kPh][kM];
+  __shared__ float mean[kM];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int64_t len = offsets[b + 1] - offsets[b];
+  const int nf = (int)max((int64_t)1, min((int64_t)frames, (len + 159) / 160));
+  const uint32_t k = maxkey[b];
+  const float gmax = __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+  if (tid < kPh * kM) {
+    const int ph = tid / kM, m = tid % kM;
+    float s = 0.f;
+    for (int f = ph; f < nf; f += kPh)
+      s += (fmaxf(logmel[((int64_t)b * frames + f) * kM + m], gmax - 8.0f) + 4.0f) * 0.25f;
+    part[ph][m] = s;
+  }
+  __syncthreads();
+  if (tid < kM) mean[tid] = (part[0][tid] + part[1][tid] + part[2][tid]) / (float)nf;
+  __syncthreads();
+  for (int c = tid; c < C; c += blockDim.x) {
+    float acc = bias ? bias[c] : 0.f;
+    const float* pr = P + (int64_t)c * kM;
+#pragma unroll 8
+    for (int m = 0; m < kM; ++m) acc = fmaf(pr[m], mean[m], acc);
+    spk[(int64_t)b * C + c] = acc;
+  }
+}
+
+void speaker_launch(const float* logmel, const uint32_t* maxkey, const int64_t* offsets, int B,
+                    int frames, const float* P, const float* bias, int C, float* spk,
+                    hipStream_t s) {
+  if (B <= 0) return;
+  speaker_kernel<<<B, 256, 0, s>>>(logmel, maxkey, offsets, frames, P, bias, C, spk);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -49,7 +99,8 @@ constexpr size_t kPostLds = (size_t)(kPostC * kPostRows + kPostC * 16) * sizeof(
 __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16* __restrict__ x, int T,
                                                                  const float* __restrict__ w, float bias,
                                                                  float* __restrict__ wav,
-                                                                 int16_t* __restrict__ pcm, int pre_silu) {
+                                                                 int16_t* __restrict__ pcm, int pre_silu,
+                                                                 float* __restrict__ pre_tanh) {
   extern __shared__ __attribute__((aligned(16))) float post_smem[];
   float* xs = post_smem;                        // [kPostC][kPostRows]
   float* ws = post_smem + kPostC * kPostRows;   // [kPostC][16] (taps padded to 16)
@@ -101,6 +152,11 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
   }
   float* wo = wav + (int64_t)b * T + t;
   int16_t* po = pcm ? pcm + (int64_t)b * T + t : nullptr;
+  if (pre_tanh) {  // conv_post output before tanh (parity checks upstream of saturation)
+#pragma unroll
+    for (int o = 0; o < kPostR; ++o)
+      if (t + o < T) pre_tanh[(int64_t)b * T + t + o] = acc[o];
+  }
   if (t + kPostR <= T && (T & 3) == 0) {  // aligned full group: vector stores
     *reinterpret_cast<float4*>(wo) = make_float4(y[0], y[1], y[2], y[3]);
     if (po) {
@@ -120,7 +176,7 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
 }
 
 void conv_post_launch(const _Float16* x, int B, int T, const float* w, float bias, float* wav,
-                      int16_t* pcm, hipStream_t s, int pre_silu) {
+                      int16_t* pcm, hipStream_t s, int pre_silu, float* pre_tanh) {
   if (B <= 0 || T <= 0) return;
   static bool attr = false;
   if (!attr) {
@@ -129,7 +185,7 @@ void conv_post_launch(const _Float16* x, int B, int T, const float* w, float bia
     attr = true;
   }
   conv_post_kernel<<<dim3((T + kPostT - 1) / kPostT, B), kPostThreads, kPostLds, s>>>(
-      x, T, w, bias, wav, pcm, pre_silu);
+      x, T, w, bias, wav, pcm, pre_silu, pre_tanh);
   JANUS_LAUNCH_CHECK();
 }
 

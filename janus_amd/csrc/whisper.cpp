@@ -132,6 +132,13 @@ static void fuse_f32(const ParamStore& P, const std::vector<std::string>& names,
 
 static void prepare(janus_whisper* w, hipStream_t s) {
   if (w->prepared) return;
+  // the captured decode graphs bake in the device weight pointers that are re-allocated
+  // below: drop them (a set_tensor after a decode must not replay freed weights)
+  JANUS_HIP(hipDeviceSynchronize());
+  for (auto& lane : w->lanes) {
+    for (auto& kv : lane->graphs) (void)hipGraphExecDestroy(kv.second);
+    lane->graphs.clear();
+  }
   const auto& c = w->cfg;
   const int d = c.d_model, ff = 4 * d;
   const ParamStore& P = w->params;

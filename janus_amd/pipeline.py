@@ -23,7 +23,7 @@ from . import _native as nat
 from .common.protocol import JanusMode, JanusPacket
 from .services.prosody import prosody_launch
 from .services.synthesizer import emotion_prompt
-from .vocoder import FireflyConfig, VocoderEngine, emotion_id
+from .vocoder import DEFAULT_REFERENCE_ID, FireflyConfig, VocoderEngine, emotion_id
 from .whisper import CONFIGS, WhisperEngine
 
 CAPTURE_RATE = 48000
@@ -86,10 +86,30 @@ class JanusPipeline:
         return self._hi
 
     # ------------------------------------------------------------------ decode
+    def set_reference_audio(self, wav: bytes = None):
+        """The receiver's voice-cloning recording (synthesizer.py:67-104), or None. With a
+        recording every packet is rendered in its voice (references=[...], :183-187,
+        :243-247); without one SEMANTIC packets use the stock voice id (:189) and
+        TEXT_ONLY packets none (references=None, :249)."""
+        from .common.wavio import read_wav_16k
+        self._ref_voice = (self.vocoder.speaker_embedding([read_wav_16k(wav)])[0]
+                           if wav else None)
+
+    def _voices(self, modes):
+        v = self.vocoder
+        if getattr(self, "_ref_voice", None) is not None:
+            return self._ref_voice.expand(len(modes), -1)
+        if getattr(self, "_stock_voice", None) is None:
+            self._stock_voice = v.voice(DEFAULT_REFERENCE_ID)
+        zero = torch.zeros_like(self._stock_voice)
+        return torch.stack([self._stock_voice if m == JanusMode.SEMANTIC_VOICE else zero
+                            for m in modes])
+
     def decode(self, packets, frames: int):
         """packets: MessagePack bytes (None entries skipped). Returns (wav, pcm, prompts)
-        for the SEMANTIC / TEXT_ONLY packets, all rendered to `frames` latent frames."""
-        prompts, emos = [], []
+        for the SEMANTIC / TEXT_ONLY packets, all rendered to `frames` latent frames, in
+        the voice the Synthesizer would request (set_reference_audio)."""
+        prompts, emos, modes = [], [], []
         for p in packets:
             if p is None:
                 continue
@@ -98,15 +118,16 @@ class JanusPipeline:
                 continue
             if pkt.mode == JanusMode.TEXT_ONLY:
                 emo = pkt.override_emotion
-                prompt, tag = ((f"({emo}) {pkt.text}", str(emo)) if emo and emo != "Auto"
+                prompt, tag = ((f"({emo}) {pkt.text}", f"{emo}") if emo and emo != "Auto"
                                else (pkt.text, "relaxed"))
             else:
                 prompt, tag = emotion_prompt(pkt)
             prompts.append(prompt.encode("utf-8"))
             emos.append(emotion_id(tag, self.vocoder.cfg.n_emotions))
+            modes.append(pkt.mode)
         if not prompts:
             return None, None, []
-        lat = self.vocoder.frontend(prompts, emos, frames)
+        lat = self.vocoder.frontend(prompts, emos, frames, self._voices(modes))
         wav, pcm = self.vocoder.forward(lat)
         return wav, pcm, prompts
 

@@ -4,20 +4,30 @@ Same constructor, routing and private methods as the reference (synthesizer.py:2
 ``synthesize`` routes MORSE -> ``_generate_morse_audio``, TEXT_ONLY ->
 ``_generate_fast_tts``, SEMANTIC -> ``_generate_semantic_audio`` with the identical
 prosody -> emotion-tag prompt mapping (:149-177) and fallbacks (:205-207, :253-255).
-Where the reference calls the Fish Audio cloud (``client.tts.convert``, :202, :251),
-this calls the local Firefly-GAN vocoder on the GPU and returns WAV bytes (44-byte
-RIFF header + int16 PCM @ 44.1 kHz), the format the reference requests
-(``format="wav"``). Voice-cloning reference audio is loaded and hot-reloaded exactly
-as in the reference (:67-104) but does not condition the local vocoder.
-Morse generation is host numpy, as in the reference.
+
+The reference's cloud client is replaced by a module-level ``FishAudio`` with the SDK's
+call shape — ``FishAudio(api_key=...)`` (:46) and ``client.tts.convert(text=prompt,
+format="wav", latency="balanced", references=[ReferenceAudio(audio=..., text="")] |
+reference_id=...)`` (:191-202, :237-251) — backed by the local Firefly-GAN vocoder on the
+GPU. It returns WAV bytes (44-byte RIFF header + int16 PCM @ 44.1 kHz, the format the
+reference requests). The prompt's leading "(tag)" selects the emotion row, the rest of
+the prompt drives the text front end, and the voice follows the SDK arguments: a
+``ReferenceAudio`` recording (the hot-reloaded voice-cloning file, :67-104, :183-187) is
+embedded on the GPU (janus_vocoder_speaker), a ``reference_id`` selects a stock voice
+row, neither means no voice term. Tests patch ``FishAudio`` exactly as the reference
+suite does (backend/tests/test_synthesis.py:28-312). Morse generation is host numpy, as
+in the reference.
 """
+import dataclasses
 import logging
 import os
 
 import numpy as np
 
+from ..common import wavio
 from ..common.protocol import JanusMode, JanusPacket
-from ..vocoder import FRAMES_PER_BYTE, VocoderEngine, emotion_id, wav_bytes
+from ..vocoder import (DEFAULT_REFERENCE_ID, FRAMES_PER_BYTE, VocoderEngine, emotion_id,
+                       split_prompt, wav_bytes)
 
 logger = logging.getLogger(__name__)
 
@@ -41,7 +51,7 @@ def emotion_prompt(packet: JanusPacket) -> tuple:
     voices reach the energy-only rules, as in the reference.)"""
     override = packet.override_emotion
     if override and override != "Auto":
-        tag = str(override)
+        tag = f"{override}"  # f-string, as :152 formats it (a str-enum gives its value)
     else:
         p = packet.prosody or {}
         key = (p.get('pitch', 'Normal'), p.get('energy', 'Normal'))
@@ -61,6 +71,56 @@ MORSE_CODE = {  # synthesizer.py:57-65
 }
 
 
+@dataclasses.dataclass
+class ReferenceAudio:
+    """fishaudio.types.ReferenceAudio's fields as the reference fills them (:184-187)."""
+    audio: bytes
+    text: str = ""
+
+
+class _TTS:
+    """``client.tts``: ``convert(text=..., format="wav", latency=..., references=...,
+    reference_id=...)`` -> WAV bytes rendered by the local GPU vocoder."""
+
+    def __init__(self, engine: VocoderEngine):
+        self.engine = engine
+
+    def voice(self, references=None, reference_id=None):
+        """[latent] f32 voice vector (device) for the SDK's voice arguments, or None."""
+        eng = self.engine
+        if references:
+            ref = references[0]
+            audio = ref.audio if isinstance(ref, ReferenceAudio) else ref["audio"]
+            return eng.speaker_embedding([wavio.read_wav_16k(bytes(audio))])[0]
+        if reference_id:
+            return eng.voice(reference_id)
+        return None
+
+    def convert(self, *, text: str, format: str = "wav", latency: str = "balanced",
+                references=None, reference_id=None, **_kw) -> bytes:
+        if format != "wav":
+            raise ValueError(f"local TTS renders WAV only, not {format!r}")
+        tag, _ = split_prompt(text)
+        eng = self.engine
+        pb = text.encode("utf-8")
+        frames = max(1, len(pb)) * FRAMES_PER_BYTE
+        v = self.voice(references, reference_id)
+        spk = v.reshape(1, -1) if v is not None else None
+        lat = eng.frontend([pb], [emotion_id(tag or "relaxed", eng.cfg.n_emotions)], frames, spk)
+        _, pcm = eng.forward(lat)
+        return wav_bytes(pcm[0].cpu().numpy())
+
+
+class FishAudio:
+    """Module-level stand-in for ``fishaudio.FishAudio`` (synthesizer.py:16, :46): the same
+    constructor and ``.tts.convert`` surface over the GPU vocoder. ``api_key`` is kept and
+    unused (nothing leaves the machine). Raises if no GPU / HIP library is present."""
+
+    def __init__(self, api_key: str = None, engine: VocoderEngine = None):
+        self.api_key = api_key
+        self.tts = _TTS(engine if engine is not None else VocoderEngine())
+
+
 def morse_audio(text: str) -> bytes:
     """Synthesizer._generate_morse_audio without building a Synthesizer (no vocoder)."""
     class _Codes:
@@ -70,8 +130,7 @@ def morse_audio(text: str) -> bytes:
 
 class Synthesizer:
     def __init__(self, api_key: str, reference_audio_path: str | None = None):
-        self.api_key = api_key
-        self.client = VocoderEngine()
+        self.client = FishAudio(api_key=api_key)
         self.reference_audio_bytes = None
         self._reference_audio_mtime = None
         self._reference_audio_path = reference_audio_path
@@ -110,30 +169,41 @@ class Synthesizer:
         else:
             raise ValueError(f"Unknown packet mode: {packet.mode}")
 
-    def _vocode(self, prompt: str, tag: str) -> bytes:
-        pb = prompt.encode("utf-8")
-        frames = max(1, len(pb)) * FRAMES_PER_BYTE
-        lat = self.client.frontend([pb], [emotion_id(tag, self.client.cfg.n_emotions)], frames)
-        _, pcm = self.client.forward(lat)
-        return wav_bytes(pcm[0].cpu().numpy())
-
     def _generate_semantic_audio(self, packet: JanusPacket) -> bytes:
+        """synthesizer.py:133-207."""
         self._check_and_reload_reference_audio()
-        prompt, tag = emotion_prompt(packet)
+        prompt, _ = emotion_prompt(packet)
         try:
-            return self._vocode(prompt, tag)
+            references = None
+            reference_id = None
+            if self.reference_audio_bytes:
+                references = [ReferenceAudio(audio=self.reference_audio_bytes, text="")]
+            else:
+                reference_id = DEFAULT_REFERENCE_ID
+            api_params = {"text": prompt, "format": "wav", "latency": "balanced"}
+            if references:
+                api_params["references"] = references
+            else:
+                api_params["reference_id"] = reference_id
+            return self.client.tts.convert(**api_params)
         except Exception as e:
             logger.error(f"Synthesis error: {e}")
             return self._generate_fast_tts(packet.text, packet.override_emotion)
 
     def _generate_fast_tts(self, text: str, emotion: str | None = None) -> bytes:
+        """synthesizer.py:209-255."""
         self._check_and_reload_reference_audio()
         if emotion and emotion != "Auto":
-            prompt, tag = f"({emotion}) {text}", str(emotion)
+            prompt = f"({emotion}) {text}"
         else:
-            prompt, tag = text, "relaxed"
+            prompt = text
         try:
-            return self._vocode(prompt, tag)
+            api_params = {"text": prompt, "format": "wav", "latency": "balanced"}
+            if self.reference_audio_bytes:
+                api_params["references"] = [ReferenceAudio(audio=self.reference_audio_bytes, text="")]
+            else:
+                api_params["references"] = None
+            return self.client.tts.convert(**api_params)
         except Exception as e:
             logger.error(f"Fast TTS error: {e}")
             return b''

@@ -15,12 +15,12 @@ at T > 0), no-speech skipping and timestamp-seek re-decoding are not reproduced;
 longer than 30 s is cut into consecutive 30 s windows.
 """
 import dataclasses
-import wave
 
 import numpy as np
 import torch
 
 from .. import _native as nat
+from ..common import wavio
 from ..whisper import CONFIGS, WhisperEngine
 
 WINDOW_16K = 480000
@@ -43,33 +43,36 @@ class TranscriptionInfo:
     duration: float
 
 
-def read_wav_16k(path: str) -> np.ndarray:
-    """16-bit PCM WAV -> float32 mono at 16 kHz (48 kHz by [::3] like transcriber.py:51,
-    other rates by linear interpolation)."""
-    with wave.open(path, "rb") as w:
-        sr, ch, sw, n = w.getframerate(), w.getnchannels(), w.getsampwidth(), w.getnframes()
-        raw = w.readframes(n)
-    if sw != 2:
-        raise ValueError("only 16-bit PCM WAV is supported")
-    x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
-    if ch > 1:
-        x = x.reshape(-1, ch).mean(axis=1)
-    if sr == 16000:
-        return x.astype(np.float32)
-    if sr == 48000:
-        return np.ascontiguousarray(x[::3])
-    t = np.arange(int(round(len(x) * 16000 / sr))) * (sr / 16000.0)
-    return np.interp(t, np.arange(len(x)), x).astype(np.float32)
+read_wav_16k = wavio.read_wav_16k  # 16-bit PCM WAV -> f32 @ 16 kHz
+
+# faster-whisper's device / compute_type vocabulary (WhisperModel(model_size, device=...,
+# compute_type=...)); every value names the SAME GPU engine here (see WhisperModel)
+DEVICES = ("cpu", "cuda", "auto")
+COMPUTE_TYPES = ("default", "auto", "int8", "int8_float32", "int8_float16", "int8_bfloat16",
+                 "int16", "float16", "bfloat16", "float32")
 
 
 class WhisperModel:
-    """faster-whisper-shaped front of the GPU Whisper engine."""
+    """faster-whisper-shaped front of the GPU Whisper engine.
 
-    def __init__(self, model_size: str, device: str = "cuda", compute_type: str = "float16",
+    Accepts faster-whisper's constructor arguments, including the reference's
+    ``device='cpu', compute_type='int8'`` (transcriber.py:23-27), and maps every
+    combination onto the one engine this build has: the gfx950 HIP kernels on the
+    current device, with fp16 weights on MFMA and fp32 accumulation (the decoder's
+    activations carried at fp32 precision as split-fp16 operands). ``device`` and
+    ``compute_type`` are recorded (``requested_device`` / ``requested_compute_type``)
+    but select nothing: there is no CPU path (the product fails loudly without a GPU)."""
+
+    def __init__(self, model_size: str, device: str = "auto", compute_type: str = "default",
                  **_ignored):
         if model_size not in CONFIGS:
             raise ValueError(f"unknown model size {model_size!r}; one of {sorted(CONFIGS)}")
+        if device not in DEVICES:
+            raise ValueError(f"unsupported device {device!r}; one of {DEVICES}")
+        if compute_type not in COMPUTE_TYPES:
+            raise ValueError(f"unsupported compute_type {compute_type!r}")
         self.model_size = model_size
+        self.requested_device, self.requested_compute_type = device, compute_type
         self.engine = WhisperEngine(CONFIGS[model_size])
 
     def transcribe(self, audio, beam_size: int = 1, language: str = "en", **_ignored):
@@ -105,8 +108,12 @@ class WhisperModel:
 
 class Transcriber:
     def __init__(self, model_size: str = 'base.en') -> None:
-        """transcriber.py:11-27 (device/compute type are the GPU's: fp16 MFMA)."""
-        self.model = WhisperModel(model_size, device='cuda', compute_type='float16')
+        """transcriber.py:11-27, the same call (WhisperModel maps it onto the GPU engine)."""
+        self.model = WhisperModel(
+            model_size,
+            device='cpu',
+            compute_type='int8'
+        )
 
     def transcribe_buffer(self, audio_buffer: np.ndarray) -> str:
         """transcriber.py:29-64."""

@@ -154,9 +154,12 @@ class StreamingEncoder:
                 torch.from_numpy(np.ascontiguousarray(host)).to(self.device)
             speech = self.vad.is_speech_batch(dev.reshape(S * n, CHUNK).contiguous()).reshape(S, n)
         done = []
+        # MORSE / TEXT_ONLY bypass the speech gate (engine.py:473-474, is_non_vad_mode)
+        non_vad = self.mode in (JanusMode.TEXT_ONLY, JanusMode.MORSE_CODE)
         for s in range(S):
             for j in range(n):
-                ph = self.segmenters[s].push(host[s, j * CHUNK:(j + 1) * CHUNK], bool(speech[s, j]))
+                ph = self.segmenters[s].push(host[s, j * CHUNK:(j + 1) * CHUNK], bool(speech[s, j]),
+                                             non_vad_mode=non_vad)
                 if ph is not None:
                     done.append((s, ph))
         out = self._encode(done, timestamp) if done else []
@@ -169,18 +172,41 @@ class StreamingEncoder:
         lengths = [len(p) for _, p in done]
         pcm_np = np.concatenate([p for _, p in done] + [np.zeros(1, np.float32)]).astype(np.float32)
         pcm = torch.from_numpy(pcm_np).to(self.device)
-        offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(self.device)
+        offs_np = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+        offs = torch.from_numpy(offs_np).to(self.device)
         B = len(done)
         w = self.whisper
         mel = w.logmel(pcm, offs, B, 3)                 # transcriber.py:51 [::3]
         tokens, _, _ = w.decode(w.encode(mel), self.max_length)
-        idx = torch.tensor(streams, dtype=torch.int64, device=self.device)
-        st_in = self.yin_state.index_select(0, idx).contiguous()
-        st_out = torch.empty_like(st_in)
+        # prosody in rounds: round r takes every channel's r-th phrase of this tick, so a
+        # channel that completed two phrases runs them in order, the second from the first's
+        # end state (one aubio object per channel, prosody.py:32)
+        tags = [None] * B
+        seen = {}
+        rounds = []
+        for i, s in enumerate(streams):
+            r = seen.get(s, 0)
+            seen[s] = r + 1
+            if r == len(rounds):
+                rounds.append([])
+            rounds[r].append(i)
         try:
-            tags = prosody_launch(pcm, offs, lengths, CAPTURE_RATE, self.hop,
-                                  state_in=st_in, state_out=st_out).tags()
-            self.yin_state.index_copy_(0, idx, st_out)
+            for members in rounds:
+                if len(members) == B:
+                    r_pcm, r_offs, r_len = pcm, offs, lengths
+                else:
+                    r_len = [lengths[i] for i in members]
+                    r_pcm = torch.cat([pcm[int(offs_np[i]):int(offs_np[i]) + lengths[i]] for i in members]
+                                      + [pcm.new_zeros(1)])
+                    r_offs = torch.from_numpy(np.concatenate([[0], np.cumsum(r_len)]).astype(np.int64)).to(self.device)
+                idx = torch.tensor([streams[i] for i in members], dtype=torch.int64, device=self.device)
+                st_in = self.yin_state.index_select(0, idx).contiguous()
+                st_out = torch.empty_like(st_in)
+                r_tags = prosody_launch(r_pcm, r_offs, r_len, CAPTURE_RATE, self.hop,
+                                        state_in=st_in, state_out=st_out).tags()
+                self.yin_state.index_copy_(0, idx, st_out)  # indices distinct within a round
+                for i, t in zip(members, r_tags):
+                    tags[i] = t
         except Exception:                               # engine.py:520-525
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
         texts = w.texts(tokens)

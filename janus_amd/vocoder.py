@@ -39,6 +39,7 @@ class FireflyConfig:
     pre_kernel: int = 13
     post_kernel: int = 13
     n_emotions: int = 16
+    n_voices: int = 16
 
     @property
     def hop(self):
@@ -53,16 +54,38 @@ class janus_vocoder_config(ctypes.Structure):
                 ("post_kernel", ctypes.c_int), ("n_emotions", ctypes.c_int)]
 
 
+def _fnv1a(s: str) -> int:
+    h = 0x811C9DC5
+    for b in s.encode("utf-8"):
+        h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
 def emotion_id(tag: str, n_emotions: int = 16) -> int:
     """Known prompt tags map to fixed rows; any other override string (synthesizer.py:150-151)
     to a stable FNV-1a bucket of the remaining rows."""
     t = str(tag).lower()
     if t in EMOTIONS:
         return EMOTIONS.index(t)
-    h = 0x811C9DC5
-    for b in t.encode("utf-8"):
-        h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
-    return len(EMOTIONS) + h % (n_emotions - len(EMOTIONS))
+    return len(EMOTIONS) + _fnv1a(t) % (n_emotions - len(EMOTIONS))
+
+
+# the reference's stock voice when no recording is loaded (synthesizer.py:189)
+DEFAULT_REFERENCE_ID = "5196af35f6ff4a0dbf541793fc9f2157"
+
+
+def voice_id(reference_id: str, n_voices: int = 16) -> int:
+    """Row of frontend.voice_embed for a Fish voice id (FNV-1a bucket)."""
+    return _fnv1a(str(reference_id)) % n_voices
+
+
+def split_prompt(text: str):
+    """Fish-style prompt "(tag) text" -> (tag, text); no leading tag -> (None, text).
+    The reference builds exactly this form (synthesizer.py:152, :177, :231)."""
+    if text.startswith("(") and ") " in text:
+        i = text.index(") ")
+        return text[1:i], text[i + 2:]
+    return None, text
 
 
 def synthetic_weights(cfg: FireflyConfig, seed: int = 0) -> dict:
@@ -90,6 +113,10 @@ def synthetic_weights(cfg: FireflyConfig, seed: int = 0) -> dict:
                 rn(f"{p}.convs2.{m}.bias", C, std=0.02)
     rn("conv_post.weight", 1, C, cfg.post_kernel, std=0.35 / math.sqrt(C * cfg.post_kernel))
     rn("conv_post.bias", 1, std=0.02)
+    # voice conditioning (appended last: the tensors above keep their seeded values)
+    rn("frontend.speaker_proj", cfg.latent_dim, 80, std=0.5 / math.sqrt(80))
+    rn("frontend.speaker_bias", cfg.latent_dim, std=0.02)
+    rn("frontend.voice_embed", cfg.n_voices, cfg.latent_dim, std=0.5)
     return W
 
 
@@ -130,10 +157,16 @@ class VocoderEngine:
         h = ctypes.c_void_p()
         nat.call("janus_vocoder_create", ctypes.addressof(c), ctypes.addressof(h))
         self._h = h
-        weights = weights if weights is not None else load_weights(cfg, seed)
+        weights = dict(weights if weights is not None else load_weights(cfg, seed))
+        from .whisper import mel_constants  # the speaker path's log-mel front end
+        weights["mel.basis"], weights["mel.filters"] = mel_constants()
         for name, arr in weights.items():
             a = np.ascontiguousarray(arr, dtype=np.float32)
             nat.call("janus_vocoder_set_tensor", self._h, name.encode(), a.ctypes.data, a.size)
+        ve = weights.get("frontend.voice_embed")
+        self._voices = (torch.from_numpy(np.ascontiguousarray(ve, np.float32)).to(self.device)
+                        if ve is not None else None)
+        self.has_speaker = "frontend.speaker_proj" in weights
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -143,8 +176,9 @@ class VocoderEngine:
             except Exception:
                 pass
 
-    def frontend(self, prompts, emotions, frames: int) -> torch.Tensor:
-        """prompts: list of bytes; emotions: list of int ids -> latents fp16 [B][F][latent]."""
+    def frontend(self, prompts, emotions, frames: int, speaker: torch.Tensor = None) -> torch.Tensor:
+        """prompts: list of bytes; emotions: list of int ids; speaker: optional f32 device
+        tensor [B][latent] (voice term per row) -> latents fp16 [B][F][latent]."""
         B = len(prompts)
         offs = np.concatenate([[0], np.cumsum([len(p) for p in prompts])]).astype(np.int64)
         allb = np.frombuffer(b"".join(prompts) + b"\0", np.uint8).copy()
@@ -152,18 +186,46 @@ class VocoderEngine:
         d_offs = torch.from_numpy(offs).to(self.device)
         d_emo = torch.tensor(list(emotions), dtype=torch.int32, device=self.device)
         lat = torch.empty(B, frames, self.cfg.latent_dim, dtype=torch.float16, device=self.device)
-        nat.call("janus_vocoder_frontend", self._h, d_bytes.data_ptr(), d_offs.data_ptr(),
-                 d_emo.data_ptr(), B, frames, lat.data_ptr(), nat.stream_ptr())
+        spk_ptr = None
+        if speaker is not None:
+            assert speaker.shape == (B, self.cfg.latent_dim) and speaker.dtype == torch.float32
+            speaker = speaker.contiguous()
+            spk_ptr = speaker.data_ptr()
+        nat.call("janus_vocoder_frontend_ex", self._h, d_bytes.data_ptr(), d_offs.data_ptr(),
+                 d_emo.data_ptr(), spk_ptr, B, frames, lat.data_ptr(), nat.stream_ptr())
         return lat
 
-    def forward(self, lat: torch.Tensor, want_pcm: bool = True):
+    def speaker_embedding(self, clips16k) -> torch.Tensor:
+        """Voice vectors [B][latent] f32 (device) of reference recordings given as 16 kHz
+        f32 arrays (the first 30 s of each is used)."""
+        if not self.has_speaker:
+            raise RuntimeError("vocoder weights have no frontend.speaker_proj")
+        clips = [np.ascontiguousarray(c, np.float32)[:480000] for c in clips16k]
+        B = len(clips)
+        offs = torch.from_numpy(np.concatenate([[0], np.cumsum([len(c) for c in clips])]).astype(np.int64)).to(self.device)
+        pcm = torch.from_numpy(np.concatenate(clips + [np.zeros(1, np.float32)])).to(self.device)
+        out = torch.empty(B, self.cfg.latent_dim, dtype=torch.float32, device=self.device)
+        nat.call("janus_vocoder_speaker", self._h, pcm.data_ptr(), offs.data_ptr(), B,
+                 out.data_ptr(), nat.stream_ptr())
+        return out
+
+    def voice(self, reference_id: str) -> torch.Tensor:
+        """Voice vector [latent] of a stock voice id (frontend.voice_embed row)."""
+        if self._voices is None:
+            raise RuntimeError("vocoder weights have no frontend.voice_embed")
+        return self._voices[voice_id(reference_id, self._voices.shape[0])]
+
+    def forward(self, lat: torch.Tensor, want_pcm: bool = True, want_pre_tanh: bool = False):
+        """-> (wav f32, pcm int16 | None) or, with want_pre_tanh, (wav, pcm, conv_post out)."""
         B, Fr, _ = lat.shape
         T = Fr * self.cfg.hop
         wav = torch.empty(B, T, dtype=torch.float32, device=self.device)
         pcm = torch.empty(B, T, dtype=torch.int16, device=self.device) if want_pcm else None
-        nat.call("janus_vocoder_forward", self._h, lat.data_ptr(), B, Fr, wav.data_ptr(),
-                 pcm.data_ptr() if pcm is not None else None, nat.stream_ptr())
-        return wav, pcm
+        pre = torch.empty(B, T, dtype=torch.float32, device=self.device) if want_pre_tanh else None
+        nat.call("janus_vocoder_forward_ex", self._h, lat.data_ptr(), B, Fr, wav.data_ptr(),
+                 pcm.data_ptr() if pcm is not None else None,
+                 pre.data_ptr() if pre is not None else None, nat.stream_ptr())
+        return (wav, pcm, pre) if want_pre_tanh else (wav, pcm)
 
     def set_timing(self, on: bool) -> None:
         nat.call("janus_vocoder_set_timing", self._h, int(on))

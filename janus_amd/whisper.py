@@ -163,7 +163,17 @@ def synthetic_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
         mlp(p)
         ln(p + ".final_layer_norm")
     ln("decoder.layer_norm")
-    return W
+    return engine_weights(W)
+
+
+def engine_weights(W: dict) -> dict:
+    """The numbers the engine multiplies: every matrix (conv kernels, projections,
+    embeddings, positional tables; ndim >= 2) rounded to fp16, the precision the GPU keeps
+    them in (a CTranslate2 float16 conversion stores them the same way); biases and
+    LayerNorm parameters stay fp32. The oracle is run on these weights, so parity
+    measures arithmetic, not weight rounding."""
+    return {k: (v.astype(np.float16).astype(np.float32) if v.ndim >= 2 else v.astype(np.float32))
+            for k, v in W.items()}
 
 
 def load_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
@@ -171,8 +181,8 @@ def load_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
     if path and os.path.exists(os.path.join(path, "model.safetensors")):
         from safetensors.numpy import load_file
         raw = load_file(os.path.join(path, "model.safetensors"))
-        return {k[len("model."):] if k.startswith("model.") else k: v.astype(np.float32)
-                for k, v in raw.items()}
+        return engine_weights({k[len("model."):] if k.startswith("model.") else k: v
+                               for k, v in raw.items()})
     return synthetic_weights(cfg, seed)
 
 

@@ -17,24 +17,47 @@ def _t(W, name):
     return torch.from_numpy(np.asarray(W[name], np.float32))
 
 
-def frontend(prompts_bytes, emotion_ids, frames, W):
-    """latents [B][frames][latent] fp32."""
+def frontend(prompts_bytes, emotion_ids, frames, W, speaker=None):
+    """latents [B][frames][latent] fp32; speaker: optional [B][latent] voice rows
+    (janus_vocoder_frontend_ex adds them after text + emotion, in that order)."""
     te, ee = _t(W, "frontend.text_embed"), _t(W, "frontend.emotion_embed")
     out = []
-    for pb, e in zip(prompts_bytes, emotion_ids):
+    for b, (pb, e) in enumerate(zip(prompts_bytes, emotion_ids)):
         n = len(pb)
         if n:
             idx = (np.arange(frames, dtype=np.int64) * n) // frames
             tx = te[torch.from_numpy(np.frombuffer(pb, np.uint8)[idx].astype(np.int64))]
         else:
             tx = torch.zeros(frames, te.shape[1])
-        out.append(tx + ee[e])
+        row = tx + ee[e]
+        if speaker is not None:
+            row = row + torch.as_tensor(np.asarray(speaker[b], np.float32))
+        out.append(row)
     return torch.stack(out)
 
 
+def speaker(clips16k, W):
+    """Voice vectors [B][latent] (float64 -> f32) of 16 kHz clips: the normalised Whisper
+    log-mel (oracle.whisper.logmel, decim 1) averaged over the clip's frames
+    min(3000, max(1, ceil(n / 160))), projected by frontend.speaker_proj / _bias
+    (janus_amd/csrc/vocoder_edge.hip speaker_kernel)."""
+    from janus_amd.whisper import mel_filters
+    from oracle.whisper import logmel
+    P = np.asarray(W["frontend.speaker_proj"], np.float64)
+    bias = np.asarray(W["frontend.speaker_bias"], np.float64)
+    out = []
+    for x in clips16k:
+        x = np.asarray(x, np.float32)[:480000]
+        nf = min(3000, max(1, -(-len(x) // 160)))
+        m = logmel(x, 1, mel_filters()).astype(np.float64)[:nf].mean(0)
+        out.append(bias + P @ m)
+    return np.stack(out).astype(np.float32)
+
+
 @torch.no_grad()
-def generator(lat, W, cfg):
-    """lat [B][F][latent] -> wav [B][F*prod(rates)] (fp32)."""
+def generator(lat, W, cfg, pre_tanh=False):
+    """lat [B][F][latent] -> wav [B][F*prod(rates)] (fp32); with pre_tanh also the
+    conv_post output before tanh."""
     x = torch.as_tensor(lat, dtype=torch.float32).transpose(1, 2)
     x = F.conv1d(x, _t(W, "conv_pre.weight"), _t(W, "conv_pre.bias"), padding=(cfg.pre_kernel - 1) // 2)
     for i, u in enumerate(cfg.up_rates):
@@ -57,7 +80,7 @@ def generator(lat, W, cfg):
         x = torch.stack(outs, 0).mean(0)
     x = F.silu(x)
     x = F.conv1d(x, _t(W, "conv_post.weight"), _t(W, "conv_post.bias"), padding=(cfg.post_kernel - 1) // 2)
-    return torch.tanh(x)[:, 0]
+    return (torch.tanh(x)[:, 0], x[:, 0]) if pre_tanh else torch.tanh(x)[:, 0]
 
 
 def pcm16(wav):

@@ -143,6 +143,74 @@ def apply_rules(logits, sampled, tk, suppress, max_initial=50, timestamps=True):
 
 
 @torch.no_grad()
+def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True):
+    """Batched greedy decode with per-layer K/V caches (fp32), the same algorithm as
+    ``greedy`` (one full forward per step) at O(T) per step instead of O(T^2):
+    enc [B][1500][d] -> per row a dict(tokens=[sampled incl. eot], margins=[top-2 gap
+    of the rule-filtered logits per step], sum_lp=float). Rows that emitted eot stop."""
+    enc = torch.as_tensor(enc, dtype=torch.float32)
+    B, Te, d = enc.shape
+    H, hd = cfg.n_heads, d // cfg.n_heads
+    suppress = tk.suppress_tokens()
+    prompt = list(tk.sot_sequence)
+    E = _t(W, "decoder.embed_tokens.weight")
+    P = _t(W, "decoder.embed_positions.weight")
+
+    def heads(t):
+        return t.view(t.shape[0], -1, H, hd).transpose(1, 2)   # [B][H][T][hd]
+
+    ck, cv = [], []
+    for i in range(cfg.dec_layers):
+        p = f"decoder.layers.{i}.encoder_attn"
+        ck.append(heads(_lin(enc, W, p + ".k_proj", bias=False)))
+        cv.append(heads(_lin(enc, W, p + ".v_proj")))
+    sk = [None] * cfg.dec_layers
+    sv = [None] * cfg.dec_layers
+    seqs = [list(prompt) for _ in range(B)]
+    out = [dict(tokens=[], margins=[], sum_lp=0.0) for _ in range(B)]
+    done = [False] * B
+    for pos in range(max_length - 1):
+        tok = torch.tensor([s[pos] if pos < len(s) else tk.eot for s in seqs])
+        x = (E[tok] + P[pos])[:, None]                          # [B][1][d]
+        for i in range(cfg.dec_layers):
+            p = f"decoder.layers.{i}"
+            h = _ln(x, W, p + ".self_attn_layer_norm")
+            q = heads(_lin(h, W, p + ".self_attn.q_proj"))
+            k = heads(_lin(h, W, p + ".self_attn.k_proj", bias=False))
+            v = heads(_lin(h, W, p + ".self_attn.v_proj"))
+            sk[i] = k if sk[i] is None else torch.cat([sk[i], k], 2)
+            sv[i] = v if sv[i] is None else torch.cat([sv[i], v], 2)
+            s = (q @ sk[i].transpose(-1, -2)) / math.sqrt(hd)
+            o = (s.softmax(-1) @ sv[i]).transpose(1, 2).reshape(B, 1, d)
+            x = x + _lin(o, W, p + ".self_attn.out_proj")
+            h = _ln(x, W, p + ".encoder_attn_layer_norm")
+            q = heads(_lin(h, W, p + ".encoder_attn.q_proj"))
+            s = (q @ ck[i].transpose(-1, -2)) / math.sqrt(hd)
+            o = (s.softmax(-1) @ cv[i]).transpose(1, 2).reshape(B, 1, d)
+            x = x + _lin(o, W, p + ".encoder_attn.out_proj")
+            h = _ln(x, W, p + ".final_layer_norm")
+            x = x + _lin(F.gelu(_lin(h, W, p + ".fc1")), W, p + ".fc2")
+        if pos + 1 < len(prompt):
+            continue                                            # still inside the prompt
+        logits = (_ln(x, W, "decoder.layer_norm") @ E.T)[:, 0].numpy()
+        for b in range(B):
+            if done[b]:
+                continue
+            L, lp = apply_rules(logits[b], out[b]["tokens"], tk, suppress, timestamps=timestamps)
+            nxt = int(np.argmax(L))
+            top2 = np.partition(L[np.isfinite(L)], -2)[-2:] if np.isfinite(L).sum() >= 2 else [L.max(), -np.inf]
+            out[b]["margins"].append(float(top2[-1] - top2[-2]))
+            out[b]["tokens"].append(nxt)
+            out[b]["sum_lp"] += float(lp[nxt])
+            seqs[b].append(nxt)
+            if nxt == tk.eot:
+                done[b] = True
+        if all(done):
+            break
+    return out
+
+
+@torch.no_grad()
 def greedy(enc, W, cfg, tk, max_length=448, timestamps=True):
     """Greedy decode of one utterance (enc [1500][d]); returns sampled tokens incl. eot."""
     suppress = tk.suppress_tokens()

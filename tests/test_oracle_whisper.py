@@ -63,6 +63,29 @@ def test_encoder_decoder_match_transformers():
     assert torch.allclose(logits, ref_logits, atol=1e-3, rtol=1e-4)
 
 
+def test_greedy_cached_matches_full_recompute():
+    """The KV-cached batched greedy (used at full length on the GPU box) takes the same
+    tokens as the full-recompute restatement."""
+    W = synthetic_weights(SMALL, seed=4)
+    tk = tkz.WhisperTokenizer()
+    mels = np.stack([ow.logmel(synth_speech(20 + k, 2.0 + k), decim=3, filters=mel_filters()) for k in range(2)])
+    enc = ow.encoder(mels, W, SMALL)
+    fast = ow.greedy_cached(enc, W, SMALL, tk, max_length=14)
+    for b in range(2):
+        slow = ow.greedy(enc[b], W, SMALL, tk, max_length=14)
+        assert fast[b]["tokens"] == slow, b
+        assert len(fast[b]["margins"]) == len(slow) and min(fast[b]["margins"]) >= 0
+
+
+def test_synthetic_weights_fp16_exact():
+    """Weight matrices are fp16-representable: the GPU holds them as fp16 without rounding,
+    so the fp32 oracle and the engine multiply the same numbers."""
+    W = synthetic_weights(SMALL, seed=1)
+    for k, v in W.items():
+        if v.ndim >= 2:
+            assert np.array_equal(v, v.astype(np.float16).astype(np.float32)), k
+
+
 def test_timestamp_rules():
     tk = tkz.WhisperTokenizer()
     V = tkz.N_VOCAB_EN

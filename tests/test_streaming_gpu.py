@@ -56,37 +56,78 @@ def test_vad_energy(gpu):
     assert vad.is_speech(x[-1]) and not vad.is_speech(x[0])
 
 
-def test_streaming_encoder_matches_oracle(gpu):
-    S, ticks, per_tick = 2, 14, 10                 # 320 ms chunks (10 x 1536 @ 48 kHz)
-    w = WhisperEngine(CONFIGS["tiny.en"], seed=0)
-    enc = StreamingEncoder(S, w, max_length=8)
+@pytest.fixture(scope="module")
+def tiny(gpu):
+    return WhisperEngine(CONFIGS["tiny.en"], seed=0)
+
+
+def _streaming_case(gpu, w, S, ticks, per_tick, mode=None, gap_s=1.0, seed0=300, min_phrases=1):
+    from janus_amd.common.protocol import JanusMode
+    mode = JanusMode.SEMANTIC_VOICE if mode is None else mode
+    enc = StreamingEncoder(S, w, max_length=8, mode=mode)
     total = ticks * per_tick * CHUNK
     audio = np.zeros((S, total), np.float32)
     for s in range(S):  # speech / silence / speech so phrases complete mid-run
-        a = synth_speech(300 + s, 2.0)
-        b = synth_speech(400 + s, 1.2)
+        a = synth_speech(seed0 + s, 2.0)
+        b = synth_speech(seed0 + 100 + s, 1.2)
+        g = int(gap_s * 48000)
         audio[s, 5000:5000 + len(a)] = a
-        audio[s, 5000 + len(a) + 48000:5000 + len(a) + 48000 + len(b)] = b
+        audio[s, 5000 + len(a) + g:5000 + len(a) + g + len(b)] = b
     vad = VoiceActivityDetector()
     dec = vad.is_speech_batch(torch.from_numpy(audio.reshape(-1, CHUNK)).to(gpu)).reshape(S, -1)
+    non_vad = mode in (JanusMode.TEXT_ONLY, JanusMode.MORSE_CODE)
     got = []
     for t in range(ticks):
         blk = audio[:, t * per_tick * CHUNK:(t + 1) * per_tick * CHUNK]
         got += [(t, r) for r in enc.push(blk, timestamp=1700000000.25)]
+    n_ph = 0
     for s in range(S):
         chunks = [audio[s, i * CHUNK:(i + 1) * CHUNK] for i in range(ticks * per_tick)]
-        ref = segment(chunks, list(dec[s]))
+        ref = segment(chunks, list(dec[s]), non_vad=[non_vad] * len(chunks))
         mine = [r for _, r in got if r["stream"] == s]
-        assert len(mine) == len(ref) and len(ref) >= 1
+        assert len(mine) == len(ref), (s, len(mine), len(ref))
+        n_ph += len(ref)
         op = OracleProsody(48000)  # one stateful detector per channel
         for r, (_, ph) in zip(mine, ref):
             tags = op.analyze_buffer(ph)[0]
             assert r["tags"] == tags
             if r["text"].strip():
-                assert r["packet"] == opk.serialize(r["text"], 0, tags, "auto", 1700000000.25)
+                assert r["packet"] == opk.serialize(r["text"], int(mode), tags, "auto", 1700000000.25)
             else:
                 assert r["packet"] is None
+    assert n_ph >= min_phrases
     assert enc.p50_ms() > 0
+    return got
+
+
+def test_streaming_encoder_matches_oracle(gpu, tiny):
+    # 320 ms blocks (10 x 1536 @ 48 kHz), 2 channels
+    _streaming_case(gpu, tiny, S=2, ticks=14, per_tick=10, min_phrases=2)
+
+
+def test_streaming_encoder_16_channels(gpu, tiny):
+    """Config 5's per-GPU share: 16 channels of 320 ms blocks."""
+    _streaming_case(gpu, tiny, S=16, ticks=14, per_tick=10, seed0=700, min_phrases=16)
+
+
+def test_streaming_two_phrases_one_push(gpu, tiny):
+    """One long block completes two phrases on the same channel: the second phrase's YIN
+    must continue from the first one's detector state (duplicate channel)."""
+    got = _streaming_case(gpu, tiny, S=2, ticks=1, per_tick=160, gap_s=0.8, seed0=500, min_phrases=2)
+    per = {}
+    for _, r in got:
+        per[r["stream"]] = per.get(r["stream"], 0) + 1
+    assert max(per.values()) >= 2
+
+
+def test_streaming_text_only_bypasses_gate(gpu, tiny):
+    """TEXT_ONLY / MORSE skip the speech gate (engine.py:473-474): every chunk counts as
+    speech, so the whole run is one phrase that never closes on silence."""
+    from janus_amd.common.protocol import JanusMode
+    enc = StreamingEncoder(1, tiny, max_length=8, mode=JanusMode.TEXT_ONLY)
+    blk = np.zeros((1, 40 * CHUNK), np.float32)  # 1.3 s of digital silence
+    assert enc.push(blk) == []
+    assert len(enc.segmenters[0].audio_buffer) == 40
 
 
 def test_receiver_batch(gpu):

@@ -1,0 +1,79 @@
+"""Free-running greedy decode parity: janus_whisper_decode_greedy vs the fp32 KV-cached
+oracle (oracle.whisper.greedy_cached) on the SAME encoder output, at full length.
+
+Prints one JSON line: per utterance the GPU / oracle token counts, whether the whole
+sequence matches, the first divergence and the oracle's top-2 margin there, and whether
+the MessagePack packet built from each transcript matches. Usage (GPU box):
+  python tools/decode_parity.py [--model base.en] [--n 6] [--max-length 448]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from janus_amd.whisper import CONFIGS, WhisperEngine, synthetic_weights  # noqa: E402
+from janus_amd.workload import synth_speech  # noqa: E402
+from oracle import packet as opk  # noqa: E402
+from oracle import whisper as ow  # noqa: E402
+
+SECONDS = [30.0, 17.0, 8.0, 3.0, 1.0, 0.3, 24.0, 12.0]
+
+
+def compare(eng, W, cfg, enc, max_length):
+    tokens, ntok, slp = eng.decode(enc, max_length=max_length)
+    torch.cuda.synchronize()
+    tk = eng.tokenizer
+    plen = len(tk.sot_sequence)
+    toks, nt = tokens.cpu().numpy(), ntok.cpu().numpy()
+    t0 = time.time()
+    ref = ow.greedy_cached(enc.float().cpu(), W, cfg, tk, max_length)
+    t_oracle = time.time() - t0
+    rows = []
+    tags = {"energy": "Normal", "pitch": "High"}
+    for b in range(enc.shape[0]):
+        g = [int(t) for t in toks[b][plen:plen + int(nt[b])]]
+        r = ref[b]["tokens"]
+        first = next((i for i in range(min(len(g), len(r))) if g[i] != r[i]),
+                     None if len(g) == len(r) else min(len(g), len(r)))
+        pk_g = opk.serialize(tk.transcript(g), 0, tags, "auto", 1.0)
+        pk_r = opk.serialize(tk.transcript(r), 0, tags, "auto", 1.0)
+        rows.append(dict(gpu_len=len(g), ref_len=len(r), match=g == r, first_diff=first,
+                         margin_at_diff=(ref[b]["margins"][first] if first is not None and
+                                         first < len(ref[b]["margins"]) else None),
+                         min_margin=float(min(ref[b]["margins"])) if ref[b]["margins"] else None,
+                         packet_match=pk_g == pk_r))
+    return rows, t_oracle
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="base.en")
+    ap.add_argument("--n", type=int, default=6)
+    ap.add_argument("--max-length", type=int, default=448)
+    ap.add_argument("--seed", type=int, default=7)
+    a = ap.parse_args()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = CONFIGS[a.model]
+    W = synthetic_weights(cfg, a.seed)
+    eng = WhisperEngine(cfg, W)
+    dev = eng.device
+    utts = [synth_speech(140 + k, SECONDS[k % len(SECONDS)]) for k in range(a.n)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    rows, t_oracle = compare(eng, W, cfg, enc, a.max_length)
+    out = dict(model=a.model, n=a.n, max_length=a.max_length, oracle_s=round(t_oracle, 1),
+               seq_match_rate=float(np.mean([r["match"] for r in rows])),
+               packet_match_rate=float(np.mean([r["packet_match"] for r in rows])), rows=rows)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
