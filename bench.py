@@ -58,20 +58,26 @@ def parse():
 
 
 def cpu_baseline(model: str, tokens_per_utt: float):
-    """Oracle (CPU restatement) time for one 30 s utterance, from bounded samples:
-    log-mel of one 30 s clip, the encoder on one window, 32 decoder positions
-    (scaled to the tokens the GPU emitted), 5 s of YIN (scaled x6) and 1 s of vocoder
-    output (scaled x30). ~10-30 s of CPU work."""
+    """Oracle (CPU restatement) time for ONE whole 30 s utterance of the workload, every
+    stage measured, nothing scaled: log-mel of the clip, the encoder on its window, the
+    sequential KV-cache greedy loop for as many tokens as the GPU emitted per utterance
+    (the reference's decode loop shape), YIN over all 30 s, and the vocoder for the
+    30 s (2584 latent frames). ~10-30 s of CPU work."""
     from janus_amd import vocoder as jv
     from janus_amd import whisper as jw
+    from janus_amd.tokenizer import load_tokenizer
     from janus_amd.workload import synth_speech
     from oracle import prosody as op
     from oracle import vocoder as ov
     from oracle import whisper as ow
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    affinity = len(os.sched_getaffinity(0))
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    torch.set_num_threads(threads)
     cfg = jw.CONFIGS[model]
     W = jw.synthetic_weights(cfg, 0)
+    tk = load_tokenizer()
     x = synth_speech(999, AUDIO_SECONDS)
+    n_tok = max(1, int(round(tokens_per_utt)))
     t = {}
     t0 = time.perf_counter()
     mel = ow.logmel(x, 3, jw.mel_filters())
@@ -79,30 +85,30 @@ def cpu_baseline(model: str, tokens_per_utt: float):
     t0 = time.perf_counter()
     enc = ow.encoder(mel[None], W, cfg)
     t["encoder"] = time.perf_counter() - t0
-    toks = np.full((1, 32), 220)
-    toks[0, 0] = 50257
     t0 = time.perf_counter()
-    ow.decoder_logits(toks, enc, W, cfg)
-    t["decoder"] = (time.perf_counter() - t0) / 32 * tokens_per_utt
+    dec = ow.greedy_cached(enc.half().float(), W, cfg, tk, max_length=len(tk.sot_sequence) + n_tok)
+    t["decoder"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    op.yin_stream(x[: 5 * 48000])
-    t["prosody"] = (time.perf_counter() - t0) * AUDIO_SECONDS / 5.0
+    op.yin_stream(x)
+    t["prosody"] = time.perf_counter() - t0
     vc = jv.FireflyConfig()
     VW = jv.synthetic_weights(vc, 0)
-    lat = ov.frontend([b"(auto) sample"], [jv.emotion_id("auto")], 87, VW)
+    lat = ov.frontend([b"(auto) sample"], [jv.emotion_id("auto")], FRAMES_30S, VW)
     t0 = time.perf_counter()
     ov.generator(lat, VW, vc)
-    t["vocoder"] = (time.perf_counter() - t0) * AUDIO_SECONDS / (87 * 512 / 44100)
+    t["vocoder"] = time.perf_counter() - t0
     total = sum(t.values())
     return {
         "value": AUDIO_SECONDS / total,
         "unit": "xRT (audio-s/wall-s)",
-        "cores": torch.get_num_threads(),
+        "cores": threads,
         "kind": "port",
-        "sample": ("oracle CPU restatement (numpy/torch fp32 + C YIN), one 30 s utterance: "
-                   f"mel 30 s, encoder 1 window, decoder 32 positions scaled to {tokens_per_utt:.0f} "
-                   "tokens, YIN 5 s x6 (1 thread), vocoder 1 s x30"),
+        "sample": ("oracle CPU restatement (numpy/torch fp32 + C YIN), one whole 30 s utterance, "
+                   f"every stage measured: mel, encoder window, sequential KV-cache greedy loop "
+                   f"over {len(dec[0]['tokens'])} tokens, YIN over 30 s (1 thread), vocoder 30 s "
+                   f"({FRAMES_30S} frames)"),
         "stage_seconds": {k: round(v, 3) for k, v in t.items()},
+        "affinity_cpus": affinity,
         "cpu_model": _cpu_model(),
     }
 
@@ -126,7 +132,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from janus_amd.dist import gather_packets, shard
+    from janus_amd.dist import gather_results, shard
     from janus_amd.pipeline import JanusPipeline
     from janus_amd.workload import synth_speech
 
@@ -143,6 +149,8 @@ def main():
     pipe = JanusPipeline(args.model, max_length=args.max_length)
     torch.cuda.synchronize()
 
+    last = {}
+
     def step():
         if args.overlap > 0:
             # steady-state serving pipeline: batch i through mel / encoder / decoder / YIN,
@@ -151,6 +159,7 @@ def main():
             enc, wav, pcm16 = pipe.step_overlapped(pcm, offs, lengths, frames, args.overlap)
         else:
             enc, wav, pcm16 = pipe.step(pcm, offs, lengths, frames)
+        last["pcm16"] = pcm16
         return enc
 
     # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
@@ -184,10 +193,27 @@ def main():
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
     total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
     n_packets = sum(p is not None for p in enc.packets)
+    n_stats = int(enc.stats.shape[0]) if enc.stats is not None else 0
     if world > 1:
         dist.all_reduce(total_t, op=dist.ReduceOp.MAX)
-        # result gather (RCCL over xGMI): the job's packets on every rank, untimed
-        n_packets = sum(p is not None for p in gather_packets(enc.packets, dev))
+        # result gather (RCCL over xGMI): the job's packets and per-utterance prosody
+        # stats (rms, mean f0, voiced hops) on every rank, untimed
+        pk_all, st_all = gather_results(enc.packets, enc.stats, dev)
+        n_packets, n_stats = sum(p is not None for p in pk_all), int(st_all.shape[0])
+    # host edges, outside the timed region (value has inputs resident in HBM): the PCM
+    # upload of a batch and the download + RIFF framing of its int16 waveforms
+    from janus_amd.vocoder import wav_bytes
+    host_pcm = np.concatenate(utts + [np.zeros(1, np.float32)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _ = torch.from_numpy(host_pcm).to(dev)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    if last.get("pcm16") is not None:
+        h16 = last["pcm16"].cpu().numpy()
+        _ = [wav_bytes(r) for r in h16]
+    t_down = time.perf_counter() - t0
     wall = float(total_t.item())
     ms_per_step = wall / args.steps * 1000.0
     audio_s = world * B * args.seconds
@@ -229,6 +255,10 @@ def main():
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
             "packets_gathered": n_packets,
+            "stats_gathered": n_stats,
+            "host_edges_ms": {"pcm_upload": round(t_up * 1000.0, 1),
+                              "wav_download_and_framing": round(t_down * 1000.0, 1)},
+            "xrt_incl_host_edges": round(audio_s / (wall / args.steps + t_up + t_down), 2),
             "roofline": {
                 "kernel": "conv1d implicit-GEMM (vocoder, v_mfma_f32_16x16x32_f16)",
                 "bound": "mfma",

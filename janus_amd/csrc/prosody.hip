@@ -21,7 +21,9 @@
 // Roofline: VALU-bound (fp32 non-contracted sub/mul/add), ≈3·2048 flop per tau,
 // up to 2047 taus per hop; HBM traffic is 16 KB window per hop (L2-served overlap).
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include "common.h"
 
 namespace janus {
@@ -56,8 +58,8 @@ template <int kYinThreads>
 __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
     const int64_t* __restrict__ hop_off, int B, int hop, const float* __restrict__ state_in,
-    float tol, float silence_db, unsigned sample_rate, float* __restrict__ f0_out,
-    int64_t total_hops) {
+    float tol, float silence_db, float level_thr, unsigned sample_rate,
+    float* __restrict__ f0_out, int64_t total_hops) {
   __shared__ __attribute__((aligned(16))) float w[kYinBuf];
   __shared__ __attribute__((aligned(16))) float dd[kYinLen];   // d(tau), then yin(tau)
   constexpr int kTauChunk = kYinThreads * 2;
@@ -248,9 +250,11 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
       }
       // aubio_pitch_do_yin: samplerate / (pitch + 0.) in double, stored as float.
       float f0 = period > 0.0f ? (float)((double)sample_rate / (double)period) : 0.0f;
-      // aubio_silence_detection(ibuf, silence): 10*log10f(level) < silence -> 0
-      const float db = (float)(10.0 * (double)log10f(s_level));
-      if (db < silence_db) f0 = 0.0f;
+      // aubio_silence_detection(ibuf, silence): (float)(10 * log10f(level)) < silence -> 0,
+      // decided as level < level_thr: the host found the float where the C library's
+      // log10f crosses the threshold (silence_level_threshold), so the gate follows the
+      // CPU's log10f rounding bit for bit, not the device log10f's
+      if (s_level < level_thr) f0 = 0.0f;
       f0_out[g] = f0;
     }
     __syncthreads();
@@ -332,6 +336,28 @@ __global__ void prosody_state_kernel(const float* __restrict__ pcm, const int64_
   }
 }
 
+// Smallest float level L with (float)(10.0 * log10f(L)) >= silence_db (aubio's level is
+// not silent from there up), by bisection over the ordered bit patterns of [0, +inf]
+// with the host C library's log10f — the one aubio (and the oracle) call. Assumes only
+// that log10f is monotone.
+static float silence_level_threshold(float silence_db) {
+  auto silent = [&](uint32_t bits) {
+    float L;
+    std::memcpy(&L, &bits, 4);
+    return (float)(10.0 * (double)log10f(L)) < silence_db;
+  };
+  uint32_t lo = 0u, hi = 0x7f800000u;  // 0.0f (-inf dB: silent) .. +inf (never silent)
+  if (!silent(lo)) return 0.0f;         // silence_db = -inf: nothing is silent
+  while (hi - lo > 1u) {
+    const uint32_t mid = lo + (hi - lo) / 2u;
+    if (silent(mid)) lo = mid;
+    else hi = mid;
+  }
+  float thr;
+  std::memcpy(&thr, &hi, 4);
+  return thr;
+}
+
 void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* hop_off, int B,
                     int64_t total_hops, int sample_rate, int hop, float tol, float silence_db,
                     const float* state_in, float* state_out, float* f0_out, float* rms_out,
@@ -343,6 +369,7 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
   if (B == 0) return;
   JANUS_CHECK(state_in != state_out || state_in == nullptr, "state_in and state_out must not alias");
   if (total_hops > 0) {
+    const float level_thr = silence_level_threshold(silence_db);
     // max_blocks > 0 caps the grid (blocks loop over hops): the pipeline runs prosody
     // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
     const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
@@ -354,11 +381,11 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 128);
     if (nt == 256)
       yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(
-          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate,
+          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, level_thr, (unsigned)sample_rate,
           f0_out, total_hops);
     else
       yin_hops_kernel<128><<<dim3((unsigned)grid), dim3(128), 0, stream>>>(
-          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, (unsigned)sample_rate,
+          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, level_thr, (unsigned)sample_rate,
           f0_out, total_hops);
     JANUS_LAUNCH_CHECK();
   }

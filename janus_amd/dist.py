@@ -53,3 +53,26 @@ def gather_packets(packets, device, group=None):
             out.append(None if none == -1 else data[pos:pos + n])
             pos += n
     return out
+
+
+def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather per-utterance f32 statistics [n_local][k] (rms, mean f0, voiced hops)
+    from every rank -> [total][k] in rank order, on every rank (ranks may hold different
+    n_local). The tensor stays on its device: RCCL for a GPU tensor under ``nccl``."""
+    world = dist.get_world_size(group)
+    stats = stats.to(torch.float32).contiguous()
+    n_local = torch.tensor([stats.shape[0]], dtype=torch.int64, device=stats.device)
+    counts = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(counts, n_local, group=group)
+    counts = [int(c.item()) for c in counts]
+    maxn = max(max(counts), 1)
+    pad = torch.zeros(maxn, stats.shape[1], dtype=torch.float32, device=stats.device)
+    pad[:stats.shape[0]] = stats
+    parts = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def gather_results(packets, stats: torch.Tensor, device, group=None):
+    """The result gather of SURVEY §8(e): packet bytes and per-utterance stats."""
+    return gather_packets(packets, device, group), gather_stats(stats, group)

@@ -30,9 +30,24 @@ CAPTURE_RATE = 48000
 
 
 class EncodeResult:
-    def __init__(self, texts, tags, packets, tokens, n_tokens):
+    """texts, tags, packets (bytes | None) per utterance, the decoded tokens, and
+    ``stats``: f32 [B][3] device tensor (rms, mean voiced f0, voiced hops; NaN rows when
+    prosody fell back, engine.py:520-525) for the result gather (dist.gather_results)."""
+
+    def __init__(self, texts, tags, packets, tokens, n_tokens, stats=None):
         self.texts, self.tags, self.packets = texts, tags, packets
         self.tokens, self.n_tokens = tokens, n_tokens
+        self.stats = stats
+
+
+def _prosody_stats(parts, B, device):
+    try:
+        if parts and all(p is not None for p in parts):
+            return torch.cat([torch.stack([p.rms[:len(p.hop_off) - 1], p.mean_f0[:len(p.hop_off) - 1],
+                                           p.n_voiced[:len(p.hop_off) - 1].float()], 1) for p in parts])
+    except Exception:
+        pass
+    return torch.full((B, 3), float("nan"), dtype=torch.float32, device=device)
 
 
 class JanusPipeline:
@@ -78,7 +93,8 @@ class JanusPipeline:
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
-        return EncodeResult(texts, tags, packets, tokens, ntok)
+        stats = _prosody_stats(parts if pres is not None else None, B, pcm.device)
+        return EncodeResult(texts, tags, packets, tokens, ntok, stats)
 
     def _hi_stream(self, device):
         if getattr(self, "_hi", None) is None:
@@ -247,7 +263,8 @@ class JanusPipeline:
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
-        return EncodeResult(texts, tags, packets, tokens, ntok)
+        stats = _prosody_stats(parts if pres is not None else None, B, tokens.device)
+        return EncodeResult(texts, tags, packets, tokens, ntok, stats)
 
     def flush(self, frames):
         """Finish and render the batch the last overlapped step left pending:

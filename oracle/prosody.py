@@ -34,8 +34,47 @@ def _load():
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
             ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
         lib.yin_oracle_stream.restype = None
+        lib.yin_oracle_level.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+        lib.yin_oracle_level.restype = ctypes.c_float
+        lib.yin_oracle_db.argtypes = [ctypes.c_float]
+        lib.yin_oracle_db.restype = ctypes.c_float
+        lib.yin_oracle_probe.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        lib.yin_oracle_probe.restype = ctypes.c_int
         _lib = lib
     return _lib
+
+
+def level(hop_samples) -> np.float32:
+    """aubio_level_lin of one hop (sequential float sum / n)."""
+    x = np.ascontiguousarray(hop_samples, np.float32)
+    return np.float32(_load().yin_oracle_level(x.ctypes.data, len(x)))
+
+
+def level_db(lv) -> np.float32:
+    """The dB value aubio_silence_detection compares with the threshold."""
+    return np.float32(_load().yin_oracle_db(float(lv)))
+
+
+def silence_level_threshold(silence_db=DEFAULT_SILENCE_DB) -> np.float32:
+    """Smallest float level that is NOT silent under level_db (bisection over bits)."""
+    lo, hi = 0, 0x7F800000
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if level_db(np.array(mid, np.uint32).view(np.float32)) < silence_db:
+            lo = mid
+        else:
+            hi = mid
+    return np.array(hi, np.uint32).view(np.float32)
+
+
+def yin_probe(buf4096, tol=DEFAULT_TOLERANCE):
+    """(exit tau or -1, CMNDF up to the exit, period) of one detector buffer."""
+    b = np.ascontiguousarray(buf4096, np.float32)
+    assert b.shape == (YIN_BUF,)
+    yin = np.zeros(YIN_BUF // 2, np.float32)
+    per = ctypes.c_float()
+    t = _load().yin_oracle_probe(b.ctypes.data, tol, yin.ctypes.data, ctypes.addressof(per))
+    return t, yin, per.value
 
 
 def yin_stream(x, sample_rate=48000, hop=512, tol=DEFAULT_TOLERANCE,

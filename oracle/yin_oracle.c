@@ -92,6 +92,38 @@ static float pitch_do(float* buf, const float* ibuf, unsigned hop, unsigned sr, 
   return pitch;
 }
 
+/* Probes for edge-case tests: aubio_level_lin, the dB value aubio_silence_detection
+ * compares, and the CMNDF of one 4096-sample buffer with the tau at which the early
+ * exit fired (-1: none, argmin path). */
+float yin_oracle_level(const float* ibuf, unsigned hop) { return level_lin(ibuf, hop); }
+float yin_oracle_db(float level) { return (float)(10. * log10f(level)); }
+int yin_oracle_probe(const float* buf, float tol, float* yin_out, float* period_out) {
+  float yin[YIN_LEN];
+  unsigned tau;
+  float tmp, tmp2 = 0.0f;
+  yin[0] = 1.0f;
+  int exit_tau = -1;
+  for (tau = 1; tau < YIN_LEN; tau++) {
+    yin[tau] = 0.0f;
+    for (unsigned j = 0; j < YIN_LEN; j++) {
+      tmp = buf[j] - buf[j + tau];
+      yin[tau] += tmp * tmp;
+    }
+    tmp2 += yin[tau];
+    if (tmp2 != 0) yin[tau] *= (float)tau / tmp2;
+    else yin[tau] = 1.0f;
+    int period = (int)tau - 3;
+    if (tau > 4 && (yin[period] < tol) && (yin[period] < yin[period + 1])) {
+      exit_tau = (int)tau;
+      break;
+    }
+  }
+  memcpy(yin_out, yin, sizeof(float) * (exit_tau < 0 ? YIN_LEN : (size_t)exit_tau + 1));
+  float scratch[YIN_LEN];
+  *period_out = pitchyin_do(buf, tol, scratch);
+  return exit_tau;
+}
+
 /*
  * One ProsodyExtractor.analyze_buffer pitch loop over x[0..n): f0_out gets
  * ceil(n/hop) values; `state` (4096 floats, zeros for a fresh detector) is the

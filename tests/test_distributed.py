@@ -4,6 +4,7 @@ import os
 import socket
 
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 from janus_amd.dist import shard
@@ -39,7 +40,11 @@ def _worker(rank, world, port, q):
     pk = [opk.serialize(f"utt {i}", 0, {"energy": "Normal", "pitch": "High"}, "auto", float(i))
           if i != 3 else None for i in range(b, e)]
     got = gather_packets(pk, torch.device("cpu"))
-    q.put((rank, got))
+    from janus_amd.dist import gather_results
+    st = torch.tensor([[0.1 * i, 100.0 + i, float(i % 3)] for i in range(b, e)], dtype=torch.float32)
+    pk2, st_all = gather_results(pk, st, torch.device("cpu"))
+    assert pk2 == got
+    q.put((rank, (got, st_all.tolist())))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,4 +63,6 @@ def test_gather_packets_two_ranks():
         assert p.exitcode == 0
     want = [opk.serialize(f"utt {i}", 0, {"energy": "Normal", "pitch": "High"}, "auto", float(i))
             if i != 3 else None for i in range(5)]
-    assert res[0] == want and res[1] == want
+    want_st = torch.tensor([[0.1 * i, 100.0 + i, float(i % 3)] for i in range(5)], dtype=torch.float32).tolist()
+    for r in (0, 1):
+        assert res[r][0] == want and res[r][1] == want_st

@@ -1,23 +1,44 @@
 """GPU parity of the STT path (janus_whisper_*) against the oracle (oracle/whisper.py,
-pinned to transformers): log-mel within 2e-3 (fp16 output), encoder within 2 % relative
-RMS of fp32 (fp16 MFMA operands), greedy tokens consistent with the fp32 oracle's
-filtered argmax under teacher forcing."""
+pinned to transformers), on tiny.en and base.en (the bench model, config 3):
+
+* log-mel within 2e-3 (fp16 output);
+* encoder within 1e-3 relative RMS of the fp32 oracle (measured 3.9e-4 tiny / 4.2e-4
+  base: fp16 MFMA operands, fp32 accumulation, weights fp16-exact for both sides);
+* FREE-RUNNING greedy decode to the full 448-token context against the KV-cached fp32
+  oracle decoder on the same encoder output, and end to end from the same PCM through
+  the oracle's own front end and encoder: token sequences (and the MessagePack packets
+  built from them) must be identical, except where the oracle itself is at a near-tie —
+  a first divergence is allowed only at a step whose rule-filtered top-2 logit margin is
+  below NEAR_TIE. Measured (tools/decode_parity.py, profiles/r02_decode_parity.json):
+  base.en 8/8 sequences identical at 447 tokens (decoder-only and end to end), tiny.en
+  15/16 (the 16th diverges at step 33, oracle margin 1.5e-4).
+"""
 import numpy as np
 import pytest
 import torch
 
 from janus_amd.whisper import CONFIGS, WhisperEngine, mel_filters, synthetic_weights
 from janus_amd.workload import synth_speech
+from oracle import packet as opk
 from oracle import whisper as ow
 
 pytestmark = pytest.mark.gpu
 CFG = CONFIGS["tiny.en"]
+BASE = CONFIGS["base.en"]
+NEAR_TIE = 2e-3   # logit units: fp16-operand decoding may only flip a choice this close
+ENC_TOL = 1e-3    # relative RMS of the encoder output vs fp32
 
 
 @pytest.fixture(scope="module")
 def engine(gpu):
     W = synthetic_weights(CFG, seed=5)
     return WhisperEngine(CFG, W), W
+
+
+@pytest.fixture(scope="module")
+def base_engine(gpu):
+    W = synthetic_weights(BASE, seed=7)
+    return WhisperEngine(BASE, W), W
 
 
 def pack(utts, dev):
@@ -41,52 +62,78 @@ def test_logmel(engine, gpu):
         assert err < 2e-3, (b, err)
 
 
-def test_encoder(engine, gpu):
-    eng, W = engine
+@pytest.mark.parametrize("which", ["tiny.en", "base.en"])
+def test_encoder(engine, base_engine, gpu, which):
+    eng, W = engine if which == "tiny.en" else base_engine
+    cfg = CFG if which == "tiny.en" else BASE
     utts = [synth_speech(30, 30.0), synth_speech(31, 9.0)]
     pcm, offs = pack(utts, gpu)
     mel = eng.logmel(pcm, offs, 2, 3)
     enc = eng.encode(mel)
     torch.cuda.synchronize()
-    ref = ow.encoder(mel.float().cpu().numpy(), W, CFG)
+    ref = ow.encoder(mel.float().cpu().numpy(), W, cfg)
     got = enc.float().cpu()
     rel = float((got - ref).norm() / ref.norm())
-    assert rel < 2e-2, rel
+    per_row = ((got - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()  # no bad head/tile
+    print(f"{which}: encoder rel RMS {rel:.2e}, worst row {per_row:.2e}")
+    assert rel < ENC_TOL, rel
+    assert per_row < 4 * ENC_TOL, per_row
 
 
-def test_greedy_teacher_forced(engine, gpu):
-    eng, W = engine
-    utts = [synth_speech(40, 10.0), synth_speech(41, 4.0)]
+def _check_free_running(gpu_rows, ref_rows, tk, plen, ntok):
+    """-> (sequence identity rate, packet identity rate); asserts the near-tie bound."""
+    tags = {"energy": "Normal", "pitch": "High"}
+    seq = pk = 0
+    for b, r in enumerate(ref_rows):
+        g = [int(t) for t in gpu_rows[b][plen:plen + int(ntok[b])]]
+        rt = r["tokens"]
+        if g == rt:
+            seq += 1
+        else:
+            first = next((i for i in range(min(len(g), len(rt))) if g[i] != rt[i]), min(len(g), len(rt)))
+            margin = r["margins"][first] if first < len(r["margins"]) else 0.0
+            assert margin < NEAR_TIE, (b, first, margin, g[first:first + 3], rt[first:first + 3])
+        pk += opk.serialize(tk.transcript(g), 0, tags, "auto", 1.0) == \
+            opk.serialize(tk.transcript(rt), 0, tags, "auto", 1.0)
+    return seq / len(ref_rows), pk / len(ref_rows)
+
+
+def test_free_running_decode_base(base_engine, gpu):
+    """base.en, 8 utterances (30 s .. 0.3 s), free-running to the 448-token context
+    (synthetic weights never emit eot: 447 sampled tokens each), vs the oracle decoder on
+    the same encoder output (transcriber.py:53-64 -> greedy, beam_size=1)."""
+    eng, W = base_engine
+    secs = [30.0, 17.0, 8.0, 3.0, 1.0, 0.3, 24.0, 12.0]
+    utts = [synth_speech(140 + k, s) for k, s in enumerate(secs)]
     pcm, offs = pack(utts, gpu)
-    enc = eng.encode(eng.logmel(pcm, offs, 2, 3))
-    max_len = 24
-    tokens, ntok, slp = eng.decode(enc, max_length=max_len, check_every=4)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    tokens, ntok, _ = eng.decode(enc, max_length=448)
     torch.cuda.synchronize()
     tk = eng.tokenizer
-    supp = tk.suppress_tokens()
-    toks = tokens.cpu().numpy()
-    encf = enc.float().cpu()
-    agree = total = 0
-    for b in range(2):
-        row = [int(t) for t in toks[b]]
-        sampled = []
-        for pos in range(1, max_len):
-            t = row[pos]
-            if t < 0:
-                break
-            logits = ow.decoder_logits(np.array([row[:pos]]), encf[b:b + 1], W, CFG)[0, -1].numpy()
-            L, lp = ow.apply_rules(logits, sampled, tk, supp)
-            assert np.isfinite(L[t]), f"GPU picked a token the rules forbid: {t}"
-            total += 1
-            agree += int(np.argmax(L) == t)
-            # fp16 vs fp32: the chosen token must be within a small margin of the max
-            assert L.max() - L[t] < 0.05 * max(1.0, abs(L.max())), (b, pos, t, np.argmax(L))
-            sampled.append(t)
-            if t == tk.eot:
-                break
-    assert agree >= 0.9 * total, (agree, total)
-    texts = eng.texts(tokens)
-    assert all(isinstance(s, str) for s in texts)
+    nt = ntok.cpu().numpy()
+    assert (nt >= 128).all()
+    ref = ow.greedy_cached(enc.float().cpu(), W, BASE, tk, 448)
+    seq, pk = _check_free_running(tokens.cpu().numpy(), ref, tk, len(tk.sot_sequence), nt)
+    print(f"base.en free-running: sequences identical {seq:.3f}, packets identical {pk:.3f}")
+    assert seq >= 0.75 and pk >= 0.75
+
+
+def test_free_running_end_to_end_tiny(engine, gpu):
+    """PCM -> tokens: the GPU path vs the oracle's own log-mel + fp32 encoder (output
+    stored fp16, as the engine hands it to the decoder) + oracle greedy decoder."""
+    eng, W = engine
+    utts = [synth_speech(150 + k, s) for k, s in enumerate([30.0, 11.0, 4.0, 1.5])]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    tokens, ntok, _ = eng.decode(enc, max_length=448)
+    torch.cuda.synchronize()
+    mels = np.stack([ow.logmel(u, 3, mel_filters()) for u in utts])
+    enc_ref = ow.encoder(mels, W, CFG)
+    tk = eng.tokenizer
+    ref = ow.greedy_cached(enc_ref.half().float(), W, CFG, tk, 448)
+    seq, pk = _check_free_running(tokens.cpu().numpy(), ref, tk, len(tk.sot_sequence), ntok.cpu().numpy())
+    print(f"tiny.en end to end: sequences identical {seq:.3f}, packets identical {pk:.3f}")
+    assert seq >= 0.75 and pk >= 0.75
 
 
 def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--n", type=int, default=6)
     ap.add_argument("--max-length", type=int, default=448)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--e2e", action="store_true", help="also oracle front end + encoder")
     a = ap.parse_args()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     cfg = CONFIGS[a.model]
@@ -72,6 +73,27 @@ def main():
     out = dict(model=a.model, n=a.n, max_length=a.max_length, oracle_s=round(t_oracle, 1),
                seq_match_rate=float(np.mean([r["match"] for r in rows])),
                packet_match_rate=float(np.mean([r["packet_match"] for r in rows])), rows=rows)
+    if a.e2e:
+        # the oracle's own front end + fp32 encoder (output stored fp16, as the engine
+        # hands it to the decoder), then the oracle decoder, vs the GPU's tokens
+        from janus_amd.whisper import mel_filters
+        t0 = time.time()
+        mels = np.stack([ow.logmel(u, 3, mel_filters()) for u in utts])
+        enc_ref = torch.cat([ow.encoder(mels[i:i + 2], W, cfg) for i in range(0, len(utts), 2)])
+        enc_err = float((enc.float().cpu() - enc_ref).norm() / enc_ref.norm())
+        ref = ow.greedy_cached(enc_ref.half().float(), W, cfg, eng.tokenizer, a.max_length)
+        tokens, ntok, _ = eng.decode(enc, max_length=a.max_length)
+        toks, nt = tokens.cpu().numpy(), ntok.cpu().numpy()
+        plen = len(eng.tokenizer.sot_sequence)
+        e2e = []
+        for b in range(len(utts)):
+            g = [int(t) for t in toks[b][plen:plen + int(nt[b])]]
+            r = ref[b]["tokens"]
+            first = next((i for i in range(min(len(g), len(r))) if g[i] != r[i]), None)
+            e2e.append(dict(match=g == r, first_diff=first,
+                            margin_at_diff=ref[b]["margins"][first] if first is not None else None))
+        out["e2e"] = dict(enc_rel_err=enc_err, seconds=round(time.time() - t0, 1),
+                          seq_match_rate=float(np.mean([r["match"] for r in e2e])), rows=e2e)
     print(json.dumps(out), flush=True)
 
 
