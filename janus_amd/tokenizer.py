@@ -56,6 +56,15 @@ class WhisperTokenizer:
         if path and os.path.exists(os.path.join(path, "tokenizer.json")):
             from tokenizers import Tokenizer
             self._hf = Tokenizer.from_file(os.path.join(path, "tokenizer.json"))
+            # the decoder's prompt and rules use the *.en special-token ids: the file must agree
+            for name, want in (("<|endoftext|>", EOT), ("<|startoftranscript|>", SOT),
+                               ("<|startofprev|>", SOT_PREV), ("<|notimestamps|>", NO_TIMESTAMPS)):
+                got = self._hf.token_to_id(name)
+                if got != want:
+                    raise ValueError(f"tokenizer.json: {name} is {got}, expected {want} (*.en layout)")
+            ts0 = self._hf.token_to_id("<|0.00|>")
+            if ts0 is not None and ts0 != TIMESTAMP_BEGIN:
+                raise ValueError(f"tokenizer.json: <|0.00|> is {ts0}, expected {TIMESTAMP_BEGIN}")
         else:
             self._table = self._synthetic_table(seed)
 

@@ -177,12 +177,24 @@ def engine_weights(W: dict) -> dict:
 
 
 def load_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
+    """``JANUS_WHISPER_DIR/model.safetensors`` (a Hugging Face Whisper checkpoint: names
+    ``model.encoder.*`` / ``model.decoder.*``, fp16 or fp32; ``proj_out.weight`` must be
+    the tied token embedding) mapped to the engine's names, else seeded synthetic weights
+    of the real shapes."""
     path = os.environ.get("JANUS_WHISPER_DIR")
     if path and os.path.exists(os.path.join(path, "model.safetensors")):
         from safetensors.numpy import load_file
         raw = load_file(os.path.join(path, "model.safetensors"))
-        return engine_weights({k[len("model."):] if k.startswith("model.") else k: v
-                               for k, v in raw.items()})
+        W = {k[len("model."):] if k.startswith("model.") else k: v for k, v in raw.items()}
+        proj = W.pop("proj_out.weight", None)
+        if proj is not None and not np.array_equal(proj, W.get("decoder.embed_tokens.weight")):
+            raise ValueError("proj_out.weight differs from decoder.embed_tokens.weight: the "
+                             "engine's vocabulary projection is the tied embedding")
+        emb = W.get("decoder.embed_tokens.weight")
+        if emb is None or emb.shape != (cfg.n_vocab, cfg.d_model):
+            raise ValueError(f"checkpoint does not match {cfg.name}: decoder.embed_tokens.weight "
+                             f"{None if emb is None else emb.shape}")
+        return engine_weights(W)
     return synthetic_weights(cfg, seed)
 
 
