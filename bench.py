@@ -255,6 +255,13 @@ def main():
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
             "packets_gathered": n_packets,
+            # faster-whisper's gates on each T = 0 window (the fallback re-decode is not
+            # run: synthetic weights give avg_logprob far below -1, so every window would
+            # fall back)
+            "gates": {"needs_fallback": int(sum(g[0] for g in enc.gates or [])),
+                      "no_speech_skip": int(sum(g[1] for g in enc.gates or [])),
+                      "mean_avg_logprob": round(float(np.mean([g[2] for g in enc.gates])), 3)
+                      if enc.gates else None},
             "stats_gathered": n_stats,
             "host_edges_ms": {"pcm_upload": round(t_up * 1000.0, 1),
                               "wav_download_and_framing": round(t_down * 1000.0, 1)},

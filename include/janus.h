@@ -221,6 +221,34 @@ int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc, int batch
                                 const janus_decode_options* opt, int32_t* tokens,
                                 int32_t* n_tokens, float* sum_logprob, void* stream);
 
+/*
+ * Per-row prompts and the no-speech probability (faster-whisper's generate_segments /
+ * generate_with_fallback state, transcriber.py:53-57 with its defaults):
+ *   prompts      [host] int32 [B][stride]: row b's prompt (e.g. <|startofprev|>, the
+ *                previous window's last <= 223 tokens, <|startoftranscript|> — the
+ *                condition_on_previous_text prompt), prompt_lens [host] int32 [B];
+ *                NULL prompts = opt->prompt for every row
+ *   no_speech_token  token whose raw (unfiltered) softmax probability at the row's first
+ *                sampled step is reported (<|nocaptions|> 50361 for *.en), -1 = none
+ */
+typedef struct {
+  const int32_t* prompts;
+  const int32_t* prompt_lens;
+  int stride;
+  int no_speech_token;
+} janus_decode_rows;
+
+/*
+ * janus_whisper_decode_greedy with per-row prompts (rows may be NULL): all rows step
+ * together, a row samples from its own prompt length on; tokens [device] int32
+ * [B][max_length] hold row b's prompt in [0, prompt_lens[b]) and its sampled tokens after.
+ * no_speech_prob [device] f32 [B] (nullable).
+ */
+int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                   const janus_decode_options* opt, const janus_decode_rows* rows,
+                                   int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
+                                   float* no_speech_prob, void* stream);
+
 /* ------------------------------------------------------------ vocoder --- */
 /*
  * Local Firefly-GAN decoder (fish-speech HiFiGANGenerator architecture) replacing the

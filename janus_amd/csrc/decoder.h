@@ -10,6 +10,7 @@ struct DecodeRules {
   int ts_begin;                  // first timestamp token id; -1 disables timestamp rules
   int no_timestamps;             // <|notimestamps|> (always suppressed in timestamp mode)
   int max_initial_ts;            // max_initial_timestamp index (-1: none)
+  int target;                    // token whose raw softmax probability is tracked (no-speech), -1: none
 };
 
 // Per-row rule state carried across steps (computed by the selector for the next step).
@@ -29,6 +30,8 @@ struct LogitPart {
   float m_ts, s_ts;       // max / sum exp over allowed timestamp tokens
   float b_all_v; int b_all_i;  // argmax over allowed (first index on ties)
   float b_ts_v; int b_ts_i;    // argmax over allowed timestamps
+  float t_v;              // raw logit of DecodeRules::target (-inf if not in this block)
+  float m_raw, s_raw;     // max / sum exp over ALL tokens (unfiltered softmax)
   float pad;
 };
 
@@ -46,6 +49,9 @@ void kv_store_launch(const _Float16* qkv, int d, int pos, int n_ctx, _Float16* k
                      int B, hipStream_t s);
 void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen, int32_t* done,
                         float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
+// per-row prompts: tokens [B][ld] arrive pre-filled (prompt, then -1); only the counters reset
+void init_counters_launch(int32_t* done, float* sum_lp, int32_t* n_tok, float* nsp, int B,
+                          hipStream_t s);
 void select_launch(const float* logits, int V, const DecodeRules& R, const uint8_t* smask,
                    int32_t* tokens, int ld, int pos, int sample_begin_pos, int32_t* done,
                    float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
@@ -60,9 +66,14 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                            LogitPart* parts, hipStream_t s,
                            const float* lnx = nullptr, int ldx = 0, const float* ln_g = nullptr,
                            const float* ln_b = nullptr, int max_blocks = 256);
+// plen [B] (device, nullable = all rows sample from pos + 1 >= 1): rows with pos + 1 <
+// plen[b] are still inside their own prompt and keep the forced token. At a row's first
+// sampled step (pos + 1 == plen[b]) nsp[b] (nullable) gets the raw softmax probability of
+// DecodeRules::target (Whisper's no_speech_prob).
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
-                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s);
+                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s,
+                            const int32_t* plen = nullptr, float* nsp = nullptr);
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s);
 
 }  // namespace janus

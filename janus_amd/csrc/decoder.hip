@@ -143,6 +143,21 @@ void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen
   JANUS_LAUNCH_CHECK();
 }
 
+__global__ void init_counters_kernel(int32_t* done, float* sum_lp, int32_t* n_tok, float* nsp, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  done[b] = 0;
+  sum_lp[b] = 0.f;
+  n_tok[b] = 0;
+  if (nsp) nsp[b] = 0.f;
+}
+
+void init_counters_launch(int32_t* done, float* sum_lp, int32_t* n_tok, float* nsp, int B,
+                          hipStream_t s) {
+  init_counters_kernel<<<(B + 63) / 64, 64, 0, s>>>(done, sum_lp, n_tok, nsp, B);
+  JANUS_LAUNCH_CHECK();
+}
+
 // ------------------------------------------------------------------ select
 // the rules past the suppress mask, for a token whose mask byte is already in a register
 __device__ __forceinline__ bool allowed_unmasked(int t, const DecodeRules& R, const RowRules& rr,
@@ -402,6 +417,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
   float ba_v = -INFINITY, bt_v = -INFINITY;
   int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+  float m_raw = -INFINITY, s_raw = 0.f, t_v = -INFINITY;  // unfiltered softmax, target logit
   const int stride = gridDim.x * kLgWaves;
   for (int tile = tile0; tile < ntiles; tile += stride) {
     const int col0 = tile * 16;
@@ -425,7 +441,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     // wave-private patch: the wave's own stores are visible to its loads in order
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     const int row = lane;
-    float t_all = -INFINITY, t_text = -INFINITY, t_ts = -INFINITY;
+    float t_all = -INFINITY, t_text = -INFINITY, t_ts = -INFINITY, t_raw = -INFINITY;
     float vals[16];
     unsigned okm = 0;
 #pragma unroll
@@ -433,6 +449,8 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
       const int t = col0 + c;
       const float v = patch[row * 17 + c];
       vals[c] = v;
+      if (t < V) t_raw = fmaxf(t_raw, v);
+      if (t == R.target) t_v = v;
       const unsigned smw = c < 4 ? smc.x : c < 8 ? smc.y : c < 12 ? smc.z : smc.w;
       const bool masked = (smw >> (8 * (c & 3))) & 0xffu;
       const bool ok = row < B && t < V && !masked && allowed_unmasked(t, R, rr, false);
@@ -443,7 +461,9 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
         else t_text = fmaxf(t_text, v);
       }
     }
-    float u_all = 0.f, u_ts = 0.f;
+    float u_all = 0.f, u_ts = 0.f, u_raw = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) u_raw += (col0 + c < V) ? __expf(vals[c] - t_raw) : 0.f;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       if (!((okm >> c) & 1u)) continue;
@@ -459,6 +479,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     float mo;
     s_all = lse_merge(m_all, s_all, t_all, u_all, &mo); m_all = mo;
     s_ts = lse_merge(m_ts, s_ts, t_ts, u_ts, &mo); m_ts = mo;
+    s_raw = lse_merge(m_raw, s_raw, t_raw, u_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, t_text);
   }
   // merge the 8 waves' statistics per row (wave order), one partial per (row, block)
@@ -468,6 +489,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     LogitPart p;
     p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
     p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
+    p.t_v = t_v; p.m_raw = m_raw; p.s_raw = s_raw;
     wp[w * 64 + lane] = p;
   }
   __syncthreads();
@@ -481,6 +503,8 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
       q.m_text = fmaxf(q.m_text, p.m_text);
       if (better(p.b_all_v, p.b_all_i, q.b_all_v, q.b_all_i)) { q.b_all_v = p.b_all_v; q.b_all_i = p.b_all_i; }
       if (better(p.b_ts_v, p.b_ts_i, q.b_ts_v, q.b_ts_i)) { q.b_ts_v = p.b_ts_v; q.b_ts_i = p.b_ts_i; }
+      q.s_raw = lse_merge(q.m_raw, q.s_raw, p.m_raw, p.s_raw, &mo); q.m_raw = mo;
+      q.t_v = fmaxf(q.t_v, p.t_v);
     }
     parts[(int64_t)lane * gridDim.x + blockIdx.x] = q;
   }
@@ -518,10 +542,13 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
 __global__ __launch_bounds__(256) void select_partials_kernel(
     const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
     int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
-    float* __restrict__ sum_lp, int32_t* __restrict__ n_tok) {
+    float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
+    float* __restrict__ nsp) {
   __shared__ LogitPart sh[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   int32_t* row_tok = tokens + (int64_t)b * ld;
+  const int pl = plen ? plen[b] : 1;
+  if (pos + 1 < pl) return;  // still inside this row's prompt: the forced token stays
   if (done[b]) {
     if (tid == 0) row_tok[pos + 1] = R.eot;
     return;
@@ -529,13 +556,16 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
   float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
   float ba_v = -INFINITY, bt_v = -INFINITY;
   int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
+  float m_raw = -INFINITY, s_raw = 0.f, t_v = -INFINITY;
   const LogitPart* pr = parts + (int64_t)b * nblk;
   for (int i = tid; i < nblk; i += 256) {
     const LogitPart p = pr[i];
     float mo;
     s_all = lse_merge(m_all, s_all, p.m_all, p.s_all, &mo); m_all = mo;
     s_ts = lse_merge(m_ts, s_ts, p.m_ts, p.s_ts, &mo); m_ts = mo;
+    s_raw = lse_merge(m_raw, s_raw, p.m_raw, p.s_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, p.m_text);
+    t_v = fmaxf(t_v, p.t_v);
     if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
     if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
   }
@@ -545,7 +575,10 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     s_all = lse_merge(m_all, s_all, om, os, &mo); m_all = mo;
     const float tm = __shfl_xor(m_ts, o), ts = __shfl_xor(s_ts, o);
     s_ts = lse_merge(m_ts, s_ts, tm, ts, &mo); m_ts = mo;
+    const float rm = __shfl_xor(m_raw, o), rs = __shfl_xor(s_raw, o);
+    s_raw = lse_merge(m_raw, s_raw, rm, rs, &mo); m_raw = mo;
     m_text = fmaxf(m_text, __shfl_xor(m_text, o));
+    t_v = fmaxf(t_v, __shfl_xor(t_v, o));
     const float av = __shfl_xor(ba_v, o); const int ai = __shfl_xor(ba_i, o);
     if (better(av, ai, ba_v, ba_i)) { ba_v = av; ba_i = ai; }
     const float tv = __shfl_xor(bt_v, o); const int ti = __shfl_xor(bt_i, o);
@@ -555,6 +588,7 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     LogitPart p;
     p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
     p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i;
+    p.t_v = t_v; p.m_raw = m_raw; p.s_raw = s_raw; p.pad = 0.f;
     sh[w] = p;
   }
   __syncthreads();
@@ -564,10 +598,15 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     float mo;
     s_all = lse_merge(m_all, s_all, p.m_all, p.s_all, &mo); m_all = mo;
     s_ts = lse_merge(m_ts, s_ts, p.m_ts, p.s_ts, &mo); m_ts = mo;
+    s_raw = lse_merge(m_raw, s_raw, p.m_raw, p.s_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, p.m_text);
+    t_v = fmaxf(t_v, p.t_v);
     if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
     if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
   }
+  // no_speech_prob: the raw softmax probability of the target token at the row's first
+  // sampled step (logits at the <|startoftranscript|> position, before any filter)
+  if (nsp && pos + 1 == pl) nsp[b] = R.target >= 0 ? __expf(t_v - (m_raw + __logf(s_raw))) : 0.f;
   const float lse_all = m_all + __logf(s_all);
   int next = ba_i;
   float lp = ba_v - lse_all;
@@ -596,9 +635,10 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
 
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
-                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s) {
+                            float* sum_lp, int32_t* n_tok, int B, hipStream_t s,
+                            const int32_t* plen, float* nsp) {
   select_partials_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp,
-                                           n_tok);
+                                           n_tok, plen, nsp);
   JANUS_LAUNCH_CHECK();
 }
 

@@ -62,7 +62,7 @@ struct LaneArrival {
 // (one host thread and one HIP stream each): every decoder launch is latency-bound at
 // B <= 64, so two half-batch chains overlap their launch and memory round trips.
 struct DecLane {
-  DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt,
+  DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
       d_xc, d_xpc, d_xpml, d_enc;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
@@ -271,8 +271,8 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
 }
 
 static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, int B, const janus_decode_options* opt,
-                          int32_t* tokens_out, int32_t* n_tokens_out, float* sum_lp_out,
-                          hipStream_t s, LaneLatch* latch) {
+                          const janus_decode_rows* rows, int32_t* tokens_out, int32_t* n_tokens_out,
+                          float* sum_lp_out, float* nsp_out, hipStream_t s, LaneLatch* latch) {
   LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
@@ -284,7 +284,27 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                            hipMemcpyDeviceToDevice, s));
   const _Float16* enc = Z.d_enc.as<_Float16>();
   const int maxlen = opt->max_length;
-  JANUS_CHECK(opt->prompt_len >= 1 && opt->prompt_len < maxlen && maxlen <= NC,
+  // per-row prompts (janus_decode_rows): row b samples from position plen[b]; all rows step
+  // together from position 0, rows still inside their prompt keep the forced token
+  const bool per_row = rows && rows->prompts;
+  std::vector<int32_t> h_plen(B, opt->prompt_len);
+  std::vector<int32_t> h_init((size_t)B * maxlen, -1);
+  if (per_row) {
+    JANUS_CHECK(rows->prompt_lens && rows->stride >= 1, "decode: per-row prompts need lengths and a stride");
+    for (int b = 0; b < B; ++b) {
+      h_plen[b] = rows->prompt_lens[b];
+      JANUS_CHECK(h_plen[b] >= 1 && h_plen[b] <= rows->stride && h_plen[b] < maxlen,
+                  "decode: per-row prompt length out of range");
+      for (int i = 0; i < h_plen[b]; ++i) h_init[(size_t)b * maxlen + i] = rows->prompts[(size_t)b * rows->stride + i];
+    }
+  } else {
+    JANUS_CHECK(opt->prompt && opt->prompt_len >= 1, "decode: missing prompt");
+    for (int b = 0; b < B; ++b)
+      for (int i = 0; i < opt->prompt_len; ++i) h_init[(size_t)b * maxlen + i] = opt->prompt[i];
+  }
+  const int min_plen = *std::min_element(h_plen.begin(), h_plen.end());
+  const int max_plen = *std::max_element(h_plen.begin(), h_plen.end());
+  JANUS_CHECK(min_plen >= 1 && max_plen < maxlen && maxlen <= NC,
               "decode: need 1 <= prompt_len < max_length <= n_text_ctx");
   const int64_t Me = (int64_t)B * Te;
   const int nl = c.dec_layers;
@@ -318,10 +338,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   float* part_o = Z.d_part_o.as<float>();
   float* part_ml = Z.d_part_ml.as<float>();
   Z.d_done.ensure(sizeof(int32_t) * B);
-  Z.d_prompt.ensure(sizeof(int32_t) * opt->prompt_len);
+  Z.d_prompt.ensure(sizeof(int32_t) * B);   // per-row prompt lengths
   Z.d_tok.ensure(sizeof(int32_t) * (int64_t)B * maxlen);
   Z.d_ntok.ensure(sizeof(int32_t) * B);
   Z.d_slp.ensure(sizeof(float) * B);
+  Z.d_nsp.ensure(sizeof(float) * B);
   int32_t* tokens = Z.d_tok.as<int32_t>();
   int32_t* n_tokens = Z.d_ntok.as<int32_t>();
   float* sum_lp = Z.d_slp.as<float>();
@@ -331,14 +352,15 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
            *q2 = Z.d_q2.as<_Float16>(), *f = Z.d_f.as<_Float16>();
   int32_t* done = Z.d_done.as<int32_t>();
 
-  JANUS_HIP(hipMemcpyAsync(Z.d_prompt.p, opt->prompt, sizeof(int32_t) * opt->prompt_len,
-                           hipMemcpyHostToDevice, s));
+  // synchronous uploads: the host vectors die with this call
+  JANUS_HIP(hipMemcpyAsync(Z.d_prompt.p, h_plen.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
+  JANUS_HIP(hipMemcpyAsync(tokens, h_init.data(), sizeof(int32_t) * h_init.size(), hipMemcpyHostToDevice, s));
   if (opt->n_suppress > 0)
     JANUS_HIP(hipMemcpyAsync(Z.d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
                              hipMemcpyHostToDevice, s));
+  JANUS_HIP(hipStreamSynchronize(s));
   build_mask_launch(Z.d_supp.as<int32_t>(), opt->n_suppress, Z.d_smask.as<uint8_t>(), V, s);
-  init_tokens_launch(tokens, maxlen, Z.d_prompt.as<int32_t>(), opt->prompt_len, done, sum_lp,
-                     n_tokens, B, s);
+  init_counters_launch(done, sum_lp, n_tokens, Z.d_nsp.as<float>(), B, s);
   rules_init_launch(Z.d_rules.as<RowRules>(), B, s);
 
   // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
@@ -371,10 +393,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   R.ts_begin = opt->timestamp_begin;
   R.no_timestamps = opt->no_timestamps;
   R.max_initial_ts = opt->max_initial_timestamp_index;
+  R.target = rows ? rows->no_speech_token : -1;
   const float scale = 0.125f;
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
-  const int sample_begin = opt->prompt_len;  // index of the first sampled token
+  const int sample_begin = min_plen;  // index of the first sampled token (earliest row)
   // JANUS_FUSED_LN (B <= 64): LayerNorm rides on the projections (row-statistic pieces
   // written by the producer of each residual row, normalised on load by the consumer).
   // Opt-in: with the 16-wave skinny GEMM the separate LayerNorm launch measured faster
@@ -500,7 +523,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
                           ln_pro ? x : nullptr, d, fin_g, fin_b, lg_cap);
     select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
-                           maxlen, pos, done, sum_lp, n_tokens, B, s);
+                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
+                           Z.d_nsp.as<float>());
   };
   const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
   const int chunk = opt->check_every > 0 ? opt->check_every : 16;
@@ -512,7 +536,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
-      R.no_timestamps, R.max_initial_ts};
+      R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -558,6 +582,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                            hipMemcpyDeviceToDevice, s));
   JANUS_HIP(hipMemcpyAsync(n_tokens_out, n_tokens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   JANUS_HIP(hipMemcpyAsync(sum_lp_out, sum_lp, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
+  if (nsp_out)
+    JANUS_HIP(hipMemcpyAsync(nsp_out, Z.d_nsp.p, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
 }
 
 }  // namespace janus
@@ -631,6 +657,15 @@ extern "C" int janus_whisper_encode(janus_whisper* w, const uint16_t* mel, int b
 extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc, int batch,
                                            const janus_decode_options* opt, int32_t* tokens,
                                            int32_t* n_tokens, float* sum_logprob, void* stream) {
+  return janus_whisper_decode_greedy_ex(w, enc, batch, opt, nullptr, tokens, n_tokens, sum_logprob,
+                                        nullptr, stream);
+}
+
+extern "C" int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                              const janus_decode_options* opt,
+                                              const janus_decode_rows* rows, int32_t* tokens,
+                                              int32_t* n_tokens, float* sum_logprob,
+                                              float* no_speech_prob, void* stream) {
   return guarded([&] {
     JANUS_CHECK(w && enc && opt && tokens && n_tokens && sum_logprob, "null argument");
     JANUS_CHECK(batch >= 1, "decode: batch must be >= 1");
@@ -647,7 +682,8 @@ extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc
     nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
     while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
     if (nlanes == 1 && s != nullptr) {
-      decode_greedy(w, *w->lanes[0], e, batch, opt, tokens, n_tokens, sum_logprob, s, nullptr);
+      decode_greedy(w, *w->lanes[0], e, batch, opt, rows, tokens, n_tokens, sum_logprob,
+                    no_speech_prob, s, nullptr);
       return;
     }
     // the null stream cannot be captured, and lanes run concurrently: each lane gets its
@@ -675,8 +711,17 @@ extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc
       DecLane& Z = *w->lanes[i];
       try {
         JANUS_HIP(hipSetDevice(dev));  // a fresh host thread starts on device 0
+        janus_decode_rows sub{};
+        if (rows) {
+          sub = *rows;
+          if (rows->prompts) {
+            sub.prompts = rows->prompts + (int64_t)b0 * rows->stride;
+            sub.prompt_lens = rows->prompt_lens + b0;
+          }
+        }
         decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, opt,
-                      tokens + (int64_t)b0 * maxlen, n_tokens + b0, sum_logprob + b0, Z.stream,
+                      rows ? &sub : nullptr, tokens + (int64_t)b0 * maxlen, n_tokens + b0,
+                      sum_logprob + b0, no_speech_prob ? no_speech_prob + b0 : nullptr, Z.stream,
                       nlanes > 1 ? &latch : nullptr);
       } catch (const std::exception& ex) {
         errs[i] = ex.what();

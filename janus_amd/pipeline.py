@@ -34,10 +34,26 @@ class EncodeResult:
     ``stats``: f32 [B][3] device tensor (rms, mean voiced f0, voiced hops; NaN rows when
     prosody fell back, engine.py:520-525) for the result gather (dist.gather_results)."""
 
-    def __init__(self, texts, tags, packets, tokens, n_tokens, stats=None):
+    def __init__(self, texts, tags, packets, tokens, n_tokens, stats=None, gates=None):
         self.texts, self.tags, self.packets = texts, tags, packets
         self.tokens, self.n_tokens = tokens, n_tokens
         self.stats = stats
+        self.gates = gates   # per utterance (needs_fallback, no_speech_skip, avg_logprob, cr, nsp)
+
+
+def _texts_and_gates(w, dec):
+    """Transcripts of one 30 s window per utterance plus faster-whisper's gates; a
+    no-speech skip (no_speech_prob > 0.6 and avg_logprob <= -1) yields no text, as the
+    reference's generate_segments skips the window (transcriber.py:53-64)."""
+    from .services.transcriber import compression_ratio, gates
+    texts = w.texts(dec.tokens, dec.prompt_lens)
+    out_t, out_g = [], []
+    for t, (toks, avg, nsp) in zip(texts, dec.rows()):
+        text = w.tokenizer.decode(toks).strip()
+        needs, skip = gates(text, avg, nsp)
+        out_t.append("" if skip else t)
+        out_g.append((needs, skip, avg, compression_ratio(text), nsp))
+    return out_t, out_g
 
 
 def _prosody_stats(parts, B, device):
@@ -80,7 +96,7 @@ class JanusPipeline:
         except Exception:  # engine.py:520-525
             pres = None
         with torch.cuda.stream(hi):
-            tokens, ntok, _ = w.decode(enc, self.max_length)
+            dec = w.decode_ex(enc, max_length=self.max_length)
         main.wait_stream(hi)
         try:
             parts = pres if isinstance(pres, tuple) else (pres,)
@@ -89,12 +105,12 @@ class JanusPipeline:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts = w.texts(tokens)
+        texts, gts = _texts_and_gates(w, dec)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
         stats = _prosody_stats(parts if pres is not None else None, B, pcm.device)
-        return EncodeResult(texts, tags, packets, tokens, ntok, stats)
+        return EncodeResult(texts, tags, packets, dec.tokens, dec.n_tokens, stats, gts)
 
     def _hi_stream(self, device):
         if getattr(self, "_hi", None) is None:
@@ -234,8 +250,8 @@ class JanusPipeline:
             # ms); cu_count: the vocabulary projection at one block per CU of the partition
             # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms) and row-split skinny
             # projections from N <= 1024 (vs 2048: 310.5 -> 306.3 ms)
-            tokens, ntok, _ = w.decode(enc, self.max_length, xattn_splits=4,
-                                       cu_count=self._dec_s.n_cus)
+            dec = w.decode_ex(enc, max_length=self.max_length, xattn_splits=4,
+                              cu_count=self._dec_s.n_cus)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
         if timing:
@@ -246,10 +262,10 @@ class JanusPipeline:
             torch.cuda.synchronize()
             print(f"[overlap] vocoder side {ev[0].elapsed_time(ev[1]):.1f} ms, decoder side "
                   f"{ev[2].elapsed_time(ev[3]):.1f} ms", file=sys.stderr, flush=True)
-        self._pending = (tokens, ntok, pres, B, mode, override, timestamp)
+        self._pending = (dec, pres, B, mode, override, timestamp)
         return res_prev, wav, pcm16
 
-    def _finish(self, tokens, ntok, pres, B, mode, override, timestamp) -> EncodeResult:
+    def _finish(self, dec, pres, B, mode, override, timestamp) -> EncodeResult:
         """Host tail of an encode: transcripts, prosody tags (fallback Normal/Normal,
         engine.py:520-525), packets (engine.py:527-548)."""
         try:
@@ -259,12 +275,12 @@ class JanusPipeline:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts = self.whisper.texts(tokens)
+        texts, gts = _texts_and_gates(self.whisper, dec)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
-        stats = _prosody_stats(parts if pres is not None else None, B, tokens.device)
-        return EncodeResult(texts, tags, packets, tokens, ntok, stats)
+        stats = _prosody_stats(parts if pres is not None else None, B, dec.tokens.device)
+        return EncodeResult(texts, tags, packets, dec.tokens, dec.n_tokens, stats, gts)
 
     def flush(self, frames):
         """Finish and render the batch the last overlapped step left pending:

@@ -1,39 +1,71 @@
 """Speech-to-text — drop-in for backend/services/transcriber.py on MI355X.
 
 ``Transcriber`` keeps the reference's constructor and methods (transcriber.py:11-91) and
-even its body: it builds ``WhisperModel(model_size, device=..., compute_type=...)`` and
-iterates ``model.transcribe(audio[::3], beam_size=1, language='en')`` segments. Here
+even its body: it builds ``WhisperModel(model_size, device='cpu', compute_type='int8')``
+and iterates ``model.transcribe(audio[::3], beam_size=1, language='en')`` segments. Here
 ``WhisperModel`` is the GPU engine (log-mel, encoder and greedy decoder in
 libjanus_hip.so) behind faster-whisper's call shape (``transcribe`` returns
-``(segments, info)``; segments carry ``.text``), so module-level patching of
-``WhisperModel`` in tests works exactly as in the reference suite
-(backend/tests/test_input_processing.py:73-90).
+``(segments, info)``; segments carry ``.text`` and the decode statistics), so
+module-level patching of ``WhisperModel`` in tests works exactly as in the reference
+suite (backend/tests/test_input_processing.py:73-90).
 
-Scope: greedy temperature-0 decoding of 30 s windows with the Whisper logit rules;
-faster-whisper's temperature fallback (compression-ratio / log-prob gates with sampling
-at T > 0), no-speech skipping and timestamp-seek re-decoding are not reproduced; audio
-longer than 30 s is cut into consecutive 30 s windows.
+``transcribe`` restates faster-whisper's ``generate_segments`` loop for the reference's
+call (beam_size=1, language='en', every other option at its default):
+
+* windows of 3000 log-mel frames at a moving ``seek``; the next seek is the end of the
+  window when the tokens end in a single timestamp or hold none, else the last
+  consecutive-timestamp pair (the trailing partial segment is re-decoded from there);
+* ``condition_on_previous_text``: each window's prompt is ``<|startofprev|>`` + the
+  last <= 223 tokens of the segments emitted so far + ``<|startoftranscript|>``;
+* the gates, computed per window: ``avg_logprob`` = sum of chosen-token log-probs /
+  (tokens + 1), ``compression_ratio`` = len(text) / len(zlib(text)),
+  ``no_speech_prob`` = raw P(<|nocaptions|>) at the first step (on the GPU);
+  no-speech skip when no_speech_prob > 0.6 and avg_logprob <= -1;
+* segments whose start equals their end or whose text is blank are dropped.
+
+Deliberate deviations: the temperature FALLBACK is not run — a window
+whose gates fail (compression ratio > 2.4 or avg_logprob < -1, outside the no-speech
+case) is flagged (``Segment.needs_fallback``, ``WhisperModel.stats``) and its T = 0
+decode kept, because the T > 0 re-decodes are random samples no offline oracle can pin;
+each window's log-mel is computed from the audio slice at the seek position (faster-
+whisper slices one whole-audio log-mel: the two differ only in the global-max
+normalisation scope); a window that would not advance the seek (a leading
+<|0.00|><|0.00|>) advances by the window size, so the loop always terminates.
 """
 import dataclasses
+import zlib
 
 import numpy as np
 import torch
 
 from .. import _native as nat
 from ..common import wavio
+from ..tokenizer import SOT_PREV
 from ..whisper import CONFIGS, WhisperEngine
 
 WINDOW_16K = 480000
+N_FRAMES = 3000          # log-mel frames per window (hop 160 @ 16 kHz)
+HOP = 160
+TIME_PRECISION = 0.02    # seconds per timestamp step
+INPUT_STRIDE = 2         # mel frames per timestamp step
+COMPRESSION_RATIO_THRESHOLD = 2.4
+LOG_PROB_THRESHOLD = -1.0
+NO_SPEECH_THRESHOLD = 0.6
 
 
 @dataclasses.dataclass
 class Segment:
     id: int
+    seek: int
     start: float
     end: float
     text: str
     tokens: list
+    temperature: float
     avg_logprob: float
+    compression_ratio: float
+    no_speech_prob: float
+    needs_fallback: bool = False
 
 
 @dataclasses.dataclass
@@ -52,14 +84,132 @@ COMPUTE_TYPES = ("default", "auto", "int8", "int8_float32", "int8_float16", "int
                  "int16", "float16", "bfloat16", "float32")
 
 
+def compression_ratio(text: str) -> float:
+    """faster-whisper get_compression_ratio."""
+    b = text.encode("utf-8")
+    return len(b) / len(zlib.compress(b))
+
+
+def gates(text: str, avg_logprob: float, no_speech_prob: float):
+    """(needs_fallback, no_speech_skip) for one T = 0 window, faster-whisper's rules."""
+    needs = compression_ratio(text) > COMPRESSION_RATIO_THRESHOLD or avg_logprob < LOG_PROB_THRESHOLD
+    if no_speech_prob > NO_SPEECH_THRESHOLD and avg_logprob < LOG_PROB_THRESHOLD:
+        needs = False                      # silence: no fallback
+    skip = no_speech_prob > NO_SPEECH_THRESHOLD and not avg_logprob > LOG_PROB_THRESHOLD
+    return needs, skip
+
+
+def split_window(tk, tokens, seek, segment_size):
+    """One window's tokens -> ([(start_s, end_s, tokens)], next seek) as faster-whisper's
+    generate_segments slices them (timestamps included in the token lists)."""
+    tb = tk.timestamp_begin
+    time_offset = seek * HOP / 16000.0
+    single_ending = len(tokens) >= 2 and tokens[-2] < tb <= tokens[-1]
+    consecutive = [i for i in range(1, len(tokens)) if tokens[i] >= tb and tokens[i - 1] >= tb]
+    segs = []
+    if consecutive:
+        slices = list(consecutive)
+        if single_ending:
+            slices.append(len(tokens))
+        last = 0
+        for cur in slices:
+            part = tokens[last:cur]
+            segs.append((time_offset + (part[0] - tb) * TIME_PRECISION,
+                         time_offset + (part[-1] - tb) * TIME_PRECISION, part))
+            last = cur
+        if single_ending:
+            nseek = seek + segment_size
+        else:
+            nseek = seek + (tokens[last - 1] - tb) * INPUT_STRIDE
+    else:
+        duration = segment_size * HOP / 16000.0
+        stamps = [t for t in tokens if t >= tb]
+        if stamps and stamps[-1] != tb:
+            duration = (stamps[-1] - tb) * TIME_PRECISION
+        segs.append((time_offset, time_offset + duration, tokens))
+        nseek = seek + segment_size
+    if nseek <= seek:          # no progress (e.g. <|0.00|><|0.00|>): move on a window
+        nseek = seek + segment_size
+    return segs, nseek
+
+
+class _Stream:
+    """generate_segments state of one utterance."""
+
+    def __init__(self, audio16k):
+        self.audio = audio16k
+        self.content_frames = len(audio16k) // HOP
+        self.seek = 0
+        self.all_tokens = []
+        self.prompt_reset_since = 0
+        self.segments = []
+        self.windows = self.fallbacks = self.skips = 0
+
+    @property
+    def active(self):
+        return self.seek < self.content_frames
+
+    def window(self):
+        size = min(N_FRAMES, self.content_frames - self.seek)
+        a = self.audio[self.seek * HOP:self.seek * HOP + size * HOP]
+        return size, np.ascontiguousarray(a, np.float32)
+
+    def prompt(self, tk, max_length=448):
+        prev = self.all_tokens[self.prompt_reset_since:]
+        p = ([SOT_PREV] + prev[-(max_length // 2 - 1):]) if prev else []   # 223 at 448
+        return p + list(tk.sot_sequence)
+
+
+def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448):
+    """faster-whisper's seek loop for several 16 kHz utterances at once: every round
+    decodes the current window of each unfinished utterance as one GPU batch (per-row
+    prompts). Returns one _Stream (segments + gate counters) per utterance."""
+    tk = engine.tokenizer
+    dev = engine.device
+    streams = [_Stream(np.asarray(a, np.float32)) for a in audios]
+    while True:
+        act = [s for s in streams if s.active]
+        if not act:
+            break
+        for c0 in range(0, len(act), max_batch):
+            grp = act[c0:c0 + max_batch]
+            wins = [s.window() for s in grp]
+            lengths = [len(a) for _, a in wins]
+            offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
+            pcm = torch.from_numpy(np.concatenate([a for _, a in wins] + [np.zeros(1, np.float32)])).to(dev)
+            enc = engine.encode(engine.logmel(pcm, offs, len(grp), 1))
+            out = engine.decode_ex(enc, prompts=[s.prompt(tk, max_length) for s in grp], max_length=max_length)
+            for s, (size, _), (toks, avg_lp, nsp) in zip(grp, wins, out.rows()):
+                s.windows += 1
+                text = tk.decode(toks).strip()
+                cr = compression_ratio(text)
+                needs, skip = gates(text, avg_lp, nsp)
+                s.fallbacks += int(needs)
+                if skip:
+                    s.skips += 1
+                    s.seek += size
+                    continue
+                segs, nseek = split_window(tk, toks, s.seek, size)
+                for (st, en, part) in segs:
+                    txt = tk.decode(part)
+                    if st == en or not txt.strip():
+                        continue
+                    s.all_tokens.extend(part)
+                    s.segments.append(Segment(len(s.segments), s.seek, st, en, txt, part, 0.0,
+                                              avg_lp, cr, nsp, needs))
+                s.seek = nseek
+                # condition_on_previous_text at temperature 0 <= prompt_reset_on_temperature:
+                # the prompt is never reset
+    return streams
+
+
 class WhisperModel:
     """faster-whisper-shaped front of the GPU Whisper engine.
 
     Accepts faster-whisper's constructor arguments, including the reference's
     ``device='cpu', compute_type='int8'`` (transcriber.py:23-27), and maps every
     combination onto the one engine this build has: the gfx950 HIP kernels on the
-    current device, with fp16 weights on MFMA and fp32 accumulation (the decoder's
-    activations carried at fp32 precision as split-fp16 operands). ``device`` and
+    current device, with fp16 weights on MFMA and fp32 accumulation. ``device`` and
     ``compute_type`` are recorded (``requested_device`` / ``requested_compute_type``)
     but select nothing: there is no CPU path (the product fails loudly without a GPU)."""
 
@@ -74,36 +224,25 @@ class WhisperModel:
         self.model_size = model_size
         self.requested_device, self.requested_compute_type = device, compute_type
         self.engine = WhisperEngine(CONFIGS[model_size])
+        self.stats = {"windows": 0, "needs_fallback": 0, "no_speech_skips": 0}
 
     def transcribe(self, audio, beam_size: int = 1, language: str = "en", **_ignored):
         if beam_size != 1:
             raise NotImplementedError("janus_amd decodes greedily (beam_size=1, transcriber.py:55)")
+        if language not in (None, "en"):
+            raise NotImplementedError("*.en models transcribe English only (transcriber.py:56)")
         if isinstance(audio, str):
             audio = read_wav_16k(audio)
         audio = np.ascontiguousarray(audio, dtype=np.float32)
-        eng = self.engine
-        dev = eng.device
-        windows = [audio[i:i + WINDOW_16K] for i in range(0, max(len(audio), 1), WINDOW_16K)]
-        lengths = [len(w) for w in windows]
-        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
-        pcm = torch.from_numpy(np.concatenate(windows + [np.zeros(1, np.float32)])).to(dev)
-        mel = eng.logmel(pcm, offs, len(windows), 1)
-        enc = eng.encode(mel)
-        tokens, ntok, slp = eng.decode(enc)
-        toks = tokens.cpu().numpy()
-        nt = ntok.cpu().numpy()
-        lp = slp.cpu().numpy()
-        tk = eng.tokenizer
-        plen = len(tk.sot_sequence)
-        segs = []
-        for w in range(len(windows)):
-            base = w * 30.0
-            avg = float(lp[w] / max(int(nt[w]), 1))
-            for (s, e, text) in tk.segments(toks[w][plen:]):
-                segs.append(Segment(len(segs), base + s, base + e, text,
-                                    [int(t) for t in toks[w][plen:plen + int(nt[w])]], avg))
-        info = TranscriptionInfo(language, 1.0, len(audio) / 16000.0)
-        return iter(segs), info
+        st = generate_segments(self.engine, [audio])[0]
+        self._count(st)
+        info = TranscriptionInfo("en", 1.0, len(audio) / 16000.0)
+        return iter(st.segments), info
+
+    def _count(self, st):
+        self.stats["windows"] += st.windows
+        self.stats["needs_fallback"] += st.fallbacks
+        self.stats["no_speech_skips"] += st.skips
 
 
 class Transcriber:
@@ -141,15 +280,14 @@ class Transcriber:
         return full_text
 
     def transcribe_batch(self, buffers) -> list:
-        """Batched extension: 48 kHz buffers (<= 30 s each) -> transcripts, one GPU pass."""
-        eng = self.model.engine
-        dev = eng.device
-        bufs = [np.ascontiguousarray(b, dtype=np.float32)[:3 * WINDOW_16K] for b in buffers]
-        lengths = [len(b) for b in bufs]
-        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
-        pcm = torch.from_numpy(np.concatenate(bufs + [np.zeros(1, np.float32)])).to(dev)
-        tokens, _, _ = eng.decode(eng.encode(eng.logmel(pcm, offs, len(bufs), 3)))
-        return eng.texts(tokens)
+        """Batched extension: 48 kHz buffers (any length) -> transcripts, the seek loops
+        of all buffers advanced together (one GPU batch per round)."""
+        auds = [np.ascontiguousarray(np.asarray(b, dtype=np.float32)[::3]) for b in buffers]
+        streams = generate_segments(self.model.engine, auds)
+        for st in streams:
+            self.model._count(st)
+        return [' '.join(s.text.strip() for s in st.segments).strip() for st in streams]
 
 
-__all__ = ["Transcriber", "WhisperModel", "Segment", "TranscriptionInfo", "read_wav_16k", "nat"]
+__all__ = ["Transcriber", "WhisperModel", "Segment", "TranscriptionInfo", "read_wav_16k",
+           "generate_segments", "split_window", "compression_ratio", "gates", "nat"]

@@ -177,7 +177,7 @@ class StreamingEncoder:
         B = len(done)
         w = self.whisper
         mel = w.logmel(pcm, offs, B, 3)                 # transcriber.py:51 [::3]
-        tokens, _, _ = w.decode(w.encode(mel), self.max_length)
+        dec = w.decode_ex(w.encode(mel), max_length=self.max_length)
         # prosody in rounds: round r takes every channel's r-th phrase of this tick, so a
         # channel that completed two phrases runs them in order, the second from the first's
         # end state (one aubio object per channel, prosody.py:32)
@@ -209,7 +209,8 @@ class StreamingEncoder:
                     tags[i] = t
         except Exception:                               # engine.py:520-525
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts = w.texts(tokens)
+        from .pipeline import _texts_and_gates
+        texts, _ = _texts_and_gates(w, dec)
         ts = time.time() if timestamp is None else timestamp
         res = []
         for s, t, g in zip(streams, texts, tags):

@@ -59,6 +59,12 @@ class janus_decode_options(ctypes.Structure):
                 ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int)]
 
 
+class janus_decode_rows(ctypes.Structure):
+    _fields_ = [("prompts", ctypes.POINTER(ctypes.c_int32)),
+                ("prompt_lens", ctypes.POINTER(ctypes.c_int32)),
+                ("stride", ctypes.c_int), ("no_speech_token", ctypes.c_int)]
+
+
 # ----------------------------------------------------------------- front end
 def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
     """Whisper's fixed encoder positional embedding (openai whisper model.sinusoids)."""
@@ -281,8 +287,62 @@ class WhisperEngine:
         del keep
         return tokens, ntok, slp
 
-    def texts(self, tokens: torch.Tensor):
-        """Host-side detokenisation of decoded rows (after the prompt)."""
+    def decode_ex(self, enc: torch.Tensor, prompts=None, max_length: int = 448,
+                  check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
+                  cu_count: int = 0):
+        """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
+        SOT sequence for every row) and the no-speech probability. Returns a DecodeOut."""
+        B = enc.shape[0]
+        opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count)
+        rows = janus_decode_rows()
+        rows.no_speech_token = tok.NO_SPEECH
+        plens = np.full(B, len(self.tokenizer.sot_sequence), np.int32)
+        pr = None
+        if prompts is not None:
+            assert len(prompts) == B
+            plens = np.array([len(p) for p in prompts], np.int32)
+            stride = int(max(plens.max(), 1))
+            pr = np.zeros((B, stride), np.int32)
+            for b, p in enumerate(prompts):
+                pr[b, :len(p)] = p
+            rows.prompts = pr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            rows.prompt_lens = plens.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            rows.stride = stride
+        tokens = torch.empty(B, max_length, dtype=torch.int32, device=self.device)
+        ntok = torch.empty(B, dtype=torch.int32, device=self.device)
+        slp = torch.empty(B, dtype=torch.float32, device=self.device)
+        nsp = torch.empty(B, dtype=torch.float32, device=self.device)
+        nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
+                 ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
+                 nsp.data_ptr(), nat.stream_ptr())
+        del keep, pr
+        return DecodeOut(tokens, ntok, slp, nsp, plens)
+
+    def texts(self, tokens: torch.Tensor, prompt_lens=None):
+        """Host-side detokenisation of decoded rows (after each row's prompt)."""
         t = tokens.cpu().numpy()
         plen = len(self.tokenizer.sot_sequence)
-        return [self.tokenizer.transcript(row[plen:]) for row in t]
+        pl = prompt_lens if prompt_lens is not None else [plen] * len(t)
+        return [self.tokenizer.transcript(row[int(p):]) for row, p in zip(t, pl)]
+
+
+@dataclasses.dataclass
+class DecodeOut:
+    """Device tensors of one batched decode plus the host prompt lengths."""
+    tokens: torch.Tensor          # int32 [B][max_length]: prompt, sampled tokens, -1
+    n_tokens: torch.Tensor        # int32 [B]: sampled tokens incl. <|endoftext|>
+    sum_logprob: torch.Tensor     # f32 [B]: sum of the chosen tokens' (filtered) log-probs
+    no_speech_prob: torch.Tensor  # f32 [B]: raw P(<|nocaptions|>) at the first sampled step
+    prompt_lens: np.ndarray       # int32 [B]
+
+    def rows(self):
+        """Per row: (sampled tokens without <|endoftext|>, avg_logprob, no_speech_prob),
+        avg_logprob as faster-whisper derives it (sum / (len + 1), the +1 for eot)."""
+        t, n = self.tokens.cpu().numpy(), self.n_tokens.cpu().numpy()
+        lp, ns = self.sum_logprob.cpu().numpy(), self.no_speech_prob.cpu().numpy()
+        out = []
+        for b in range(len(n)):
+            s = t[b][int(self.prompt_lens[b]):int(self.prompt_lens[b]) + int(n[b])]
+            s = [int(x) for x in s if x != tok.EOT]
+            out.append((s, float(lp[b]) / (len(s) + 1), float(ns[b])))
+        return out

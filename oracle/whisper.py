@@ -143,16 +143,19 @@ def apply_rules(logits, sampled, tk, suppress, max_initial=50, timestamps=True):
 
 
 @torch.no_grad()
-def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True):
+def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True, prompts=None, no_speech=None):
     """Batched greedy decode with per-layer K/V caches (fp32), the same algorithm as
     ``greedy`` (one full forward per step) at O(T) per step instead of O(T^2):
     enc [B][1500][d] -> per row a dict(tokens=[sampled incl. eot], margins=[top-2 gap
-    of the rule-filtered logits per step], sum_lp=float). Rows that emitted eot stop."""
+    of the rule-filtered logits per step], sum_lp=float, nsp=float). Rows that emitted
+    eot stop. ``prompts``: per-row prompt token lists (default the SOT sequence); row b
+    samples from position len(prompts[b]) on. ``no_speech``: token whose raw softmax
+    probability at the row's first sampled step is reported as nsp."""
     enc = torch.as_tensor(enc, dtype=torch.float32)
     B, Te, d = enc.shape
     H, hd = cfg.n_heads, d // cfg.n_heads
     suppress = tk.suppress_tokens()
-    prompt = list(tk.sot_sequence)
+    prompts = [list(tk.sot_sequence)] * B if prompts is None else [list(p) for p in prompts]
     E = _t(W, "decoder.embed_tokens.weight")
     P = _t(W, "decoder.embed_positions.weight")
 
@@ -166,8 +169,8 @@ def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True):
         cv.append(heads(_lin(enc, W, p + ".v_proj")))
     sk = [None] * cfg.dec_layers
     sv = [None] * cfg.dec_layers
-    seqs = [list(prompt) for _ in range(B)]
-    out = [dict(tokens=[], margins=[], sum_lp=0.0) for _ in range(B)]
+    seqs = [list(p) for p in prompts]
+    out = [dict(tokens=[], margins=[], sum_lp=0.0, nsp=0.0) for _ in range(B)]
     done = [False] * B
     for pos in range(max_length - 1):
         tok = torch.tensor([s[pos] if pos < len(s) else tk.eot for s in seqs])
@@ -190,12 +193,15 @@ def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True):
             x = x + _lin(o, W, p + ".encoder_attn.out_proj")
             h = _ln(x, W, p + ".final_layer_norm")
             x = x + _lin(F.gelu(_lin(h, W, p + ".fc1")), W, p + ".fc2")
-        if pos + 1 < len(prompt):
-            continue                                            # still inside the prompt
+        if pos + 1 < min(len(p) for p in prompts):
+            continue                                            # every row inside its prompt
         logits = (_ln(x, W, "decoder.layer_norm") @ E.T)[:, 0].numpy()
         for b in range(B):
-            if done[b]:
+            if done[b] or pos + 1 < len(prompts[b]):
                 continue
+            if pos + 1 == len(prompts[b]) and no_speech is not None:
+                raw = logits[b].astype(np.float64)
+                out[b]["nsp"] = float(np.exp(raw[no_speech] - raw.max()) / np.exp(raw - raw.max()).sum())
             L, lp = apply_rules(logits[b], out[b]["tokens"], tk, suppress, timestamps=timestamps)
             nxt = int(np.argmax(L))
             top2 = np.partition(L[np.isfinite(L)], -2)[-2:] if np.isfinite(L).sum() >= 2 else [L.max(), -np.inf]
@@ -226,3 +232,65 @@ def greedy(enc, W, cfg, tk, max_length=448, timestamps=True):
         if nxt == tk.eot:
             break
     return sampled
+
+
+def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=True):
+    """faster-whisper generate_segments (beam_size=1, temperature 0, every other option
+    at its default; the T > 0 fallback is not run — janus_amd flags instead) over one
+    16 kHz utterance, restated with this module's log-mel / encoder / greedy:
+    returns (segments [(start, end, text, tokens)], dict(windows, needs_fallback, skips)).
+    The encoder output is rounded to fp16 (``enc_fp16``), as the engine stores it."""
+    import zlib
+    audio16k = np.asarray(audio16k, np.float32)
+    tb = tk.timestamp_begin
+    content = len(audio16k) // 160
+    seek, all_tokens, segs = 0, [], []
+    cnt = dict(windows=0, needs_fallback=0, skips=0)
+    while seek < content:
+        size = min(3000, content - seek)
+        mel = logmel(audio16k[seek * 160:(seek + size) * 160], 1, filters)[None]
+        enc = encoder(mel, W, cfg)
+        if enc_fp16:
+            enc = enc.half().float()
+        prompt = ([tk.sot_prev if hasattr(tk, "sot_prev") else 50360] +
+                  all_tokens[-(max_length // 2 - 1):] if all_tokens else []) + list(tk.sot_sequence)
+        r = greedy_cached(enc, W, cfg, tk, max_length, prompts=[prompt], no_speech=50361)[0]
+        toks = [t for t in r["tokens"] if t != tk.eot]
+        avg = r["sum_lp"] / (len(toks) + 1)
+        text = tk.decode(toks).strip()
+        b = text.encode()
+        cr = len(b) / len(zlib.compress(b))
+        cnt["windows"] += 1
+        needs = cr > 2.4 or avg < -1.0
+        if r["nsp"] > 0.6 and avg < -1.0:
+            needs = False
+        cnt["needs_fallback"] += int(needs)
+        if r["nsp"] > 0.6 and not avg > -1.0:
+            cnt["skips"] += 1
+            seek += size
+            continue
+        t0 = seek * 0.01
+        single = len(toks) >= 2 and toks[-2] < tb <= toks[-1]
+        cons = [i for i in range(1, len(toks)) if toks[i] >= tb and toks[i - 1] >= tb]
+        cur = []
+        if cons:
+            sl = cons + ([len(toks)] if single else [])
+            last = 0
+            for c in sl:
+                part = toks[last:c]
+                cur.append((t0 + (part[0] - tb) * 0.02, t0 + (part[-1] - tb) * 0.02, part))
+                last = c
+            nseek = seek + size if single else seek + (toks[last - 1] - tb) * 2
+        else:
+            st = [t for t in toks if t >= tb]
+            dur = (st[-1] - tb) * 0.02 if st and st[-1] != tb else size * 0.01
+            cur.append((t0, t0 + dur, toks))
+            nseek = seek + size
+        seek = nseek if nseek > seek else seek + size
+        for (s0, s1, part) in cur:
+            txt = tk.decode(part)
+            if s0 == s1 or not txt.strip():
+                continue
+            all_tokens.extend(part)
+            segs.append((s0, s1, txt, part))
+    return segs, cnt

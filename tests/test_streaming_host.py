@@ -64,3 +64,40 @@ def test_short_phrase_dropped_and_preroll_kept():
         seg2.push(z, False)          # fills pre-roll (last 10 kept), counter 16 > 15
     p = seg2.push(z + 1, True)
     assert p is None and len(seg2.audio_buffer) == 11
+
+
+def test_split_window_faster_whisper_rules():
+    """generate_segments' slicing (CPU): consecutive timestamp pairs close segments, a
+    single trailing timestamp moves the seek to the window end, otherwise the seek goes to
+    the last pair; no timestamps -> one segment of the window (or the last stamp)."""
+    from janus_amd.services.transcriber import split_window
+    from janus_amd.tokenizer import WhisperTokenizer
+    tk = WhisperTokenizer()
+    tb = tk.timestamp_begin
+    a, b = 400, 500
+    # <|0.00|> a <|1.00|><|1.00|> b <|2.00|>  (single ending)
+    segs, nseek = split_window(tk, [tb, a, tb + 50, tb + 50, b, tb + 100], 1000, 3000)
+    assert [s[2] for s in segs] == [[tb, a, tb + 50], [tb + 50, b, tb + 100]]
+    assert segs[0][:2] == (10.0, 11.0) and nseek == 4000
+    # trailing partial after the last pair: seek to that pair (1.00 s = 100 frames)
+    segs, nseek = split_window(tk, [tb, a, tb + 50, tb + 50, b], 0, 3000)
+    assert len(segs) == 1 and nseek == 100
+    # no pair: one segment to the last timestamp
+    segs, nseek = split_window(tk, [tb + 5, a, b, tb + 75], 0, 2500)
+    assert segs == [(0.0, 1.5, [tb + 5, a, b, tb + 75])] and nseek == 2500
+    # no timestamps at all: the whole window
+    segs, nseek = split_window(tk, [a, b], 300, 1200)
+    assert segs == [(3.0, 15.0, [a, b])] and nseek == 1500
+    # <|0.00|><|0.00|> would not advance: move on by the window
+    segs, nseek = split_window(tk, [tb, tb, a], 0, 3000)
+    assert nseek == 3000
+
+
+def test_gates():
+    from janus_amd.services.transcriber import compression_ratio, gates
+    assert compression_ratio("ab" * 200) > 2.4
+    assert gates("hello there", -0.3, 0.01) == (False, False)
+    assert gates("hello there", -2.0, 0.01) == (True, False)        # low log-prob: fallback
+    assert gates("ab" * 200, -0.3, 0.01) == (True, False)            # repetitive: fallback
+    assert gates("hello there", -2.0, 0.9) == (False, True)         # silence: skip, no fallback
+    assert gates("hello there", -0.5, 0.9) == (False, False)        # confident text: keep

@@ -107,15 +107,21 @@ def test_free_running_decode_base(base_engine, gpu):
     utts = [synth_speech(140 + k, s) for k, s in enumerate(secs)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    tokens, ntok, _ = eng.decode(enc, max_length=448)
+    dec = eng.decode_ex(enc, max_length=448)
     torch.cuda.synchronize()
     tk = eng.tokenizer
-    nt = ntok.cpu().numpy()
+    nt = dec.n_tokens.cpu().numpy()
     assert (nt >= 128).all()
-    ref = ow.greedy_cached(enc.float().cpu(), W, BASE, tk, 448)
-    seq, pk = _check_free_running(tokens.cpu().numpy(), ref, tk, len(tk.sot_sequence), nt)
+    ref = ow.greedy_cached(enc.float().cpu(), W, BASE, tk, 448, no_speech=50361)
+    seq, pk = _check_free_running(dec.tokens.cpu().numpy(), ref, tk, len(tk.sot_sequence), nt)
     print(f"base.en free-running: sequences identical {seq:.3f}, packets identical {pk:.3f}")
     assert seq >= 0.75 and pk >= 0.75
+    # the gate inputs: sum of chosen log-probs and the no-speech probability
+    slp, nsp = dec.sum_logprob.cpu().numpy(), dec.no_speech_prob.cpu().numpy()
+    for b, r in enumerate(ref):
+        assert abs(nsp[b] - r["nsp"]) <= 5e-3 * r["nsp"] + 1e-12, (b, nsp[b], r["nsp"])
+        if dec.tokens[b].tolist()[1:1 + len(r["tokens"])] == r["tokens"]:
+            assert abs(slp[b] - r["sum_lp"]) <= 1e-3 * abs(r["sum_lp"]), (b, slp[b], r["sum_lp"])
 
 
 def test_free_running_end_to_end_tiny(engine, gpu):
@@ -151,3 +157,24 @@ def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
     t2, n2, _ = eng.decode(enc, 24)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
+
+
+def test_seek_loop_matches_oracle(engine, gpu):
+    """faster-whisper's generate_segments loop (seek by the last timestamp pair, previous
+    text as the <|startofprev|> prompt, gates, no-speech skip, blank-segment drop) on the
+    GPU (per-row prompts, batched over utterances) vs the oracle's restatement of the same
+    loop, for a 40 s (several windows) and a 7 s utterance. max_length 64 bounds the
+    oracle's time; the prompt keeps max_length // 2 - 1 previous tokens as at 448."""
+    from janus_amd.services.transcriber import generate_segments
+    eng, W = engine
+    auds = [synth_speech(160, 40.0, sr=16000), synth_speech(161, 7.0, sr=16000)]
+    streams = generate_segments(eng, auds, max_length=64)
+    tk = eng.tokenizer
+    for a, st in zip(auds, streams):
+        ref, cnt = ow.transcribe_segments(a, W, CFG, tk, mel_filters(), max_length=64)
+        got = [(s.start, s.end, s.text, list(s.tokens)) for s in st.segments]
+        assert st.windows == cnt["windows"] and st.fallbacks == cnt["needs_fallback"] and st.skips == cnt["skips"]
+        assert [g[3] for g in got] == [r[3] for r in ref]
+        assert [g[2] for g in got] == [r[2] for r in ref]
+        assert np.allclose([g[:2] for g in got], [r[:2] for r in ref])
+        print(f"seek loop: {st.windows} windows, {len(got)} segments, {st.fallbacks} flagged for fallback")
