@@ -18,6 +18,8 @@ aubio detector (prosody.py:32). Here S channels advance together:
   encoder, greedy decoder, YIN + RMS) with each channel's persistent 4096-sample detector
   buffer gathered in and scattered back, exactly one aubio object per channel.
 """
+import queue
+import threading
 import time
 from collections import deque
 
@@ -126,12 +128,23 @@ class StreamingEncoder:
     """S channels x one JanusPipeline-style encode per completed phrase batch.
 
     push(block) takes the next [S][n*1536] capture samples of every channel (numpy f32 or
-    a GPU tensor) and returns the phrases completed by it as dicts
-    {stream, text, tags, packet} (packet None when the text is empty, engine.py:536)."""
+    a GPU tensor) and returns completed phrases as dicts {stream, text, tags, packet}
+    (packet None when the text is empty, engine.py:536).
+
+    Synchronous (default): the phrases completed by this block, encoded before push
+    returns. ``asynchronous=True``: push only gates and segments the block (the ingest
+    path the reference's producer / loop threads run, engine.py:351-506) and hands the
+    completed phrases to a worker thread with its own HIP stream, which encodes them (and,
+    with a ``receiver``, renders the returned packets the way the far end would:
+    engine.py:220-286) while the next blocks are ingested; push returns whatever finished
+    since the last call, each with ``latency_s`` = phrase completion -> packet (+ audio).
+    Phrases of one channel are encoded in completion order, so the per-channel aubio
+    state stays sequential. ``flush()`` waits for the queue."""
 
     def __init__(self, n_streams: int, whisper, max_length: int = 448,
                  mode: JanusMode = JanusMode.SEMANTIC_VOICE, override="auto",
-                 vad_threshold: float = 0.5, hop: int = 512):
+                 vad_threshold: float = 0.5, hop: int = 512, asynchronous: bool = False,
+                 receiver=None):
         self.device = nat.require_gpu()
         self.S = n_streams
         self.whisper = whisper
@@ -141,7 +154,18 @@ class StreamingEncoder:
         self.segmenters = [PhraseSegmenter() for _ in range(n_streams)]
         # one aubio detector buffer per channel (prosody.py:32), persistent across phrases
         self.yin_state = torch.zeros(n_streams, YIN_BUF, dtype=torch.float32, device=self.device)
-        self.latencies = []  # seconds per push (chunk block of all channels)
+        self.latencies = []         # seconds per push (chunk block of all channels)
+        self.phrase_latencies = []  # seconds from phrase completion to its result
+        self.receiver = receiver    # JanusPipeline-like .decode(packets, frames), or None
+        self.asynchronous = asynchronous
+        self.max_queue = 0
+        if asynchronous:
+            self._jobs = queue.Queue()
+            self._results = queue.Queue()
+            self._side = torch.cuda.Stream(device=self.device)
+            self._error = None
+            self._worker = threading.Thread(target=self._run, daemon=True)
+            self._worker.start()
 
     def push(self, block, speech=None, timestamp=None):
         t0 = time.perf_counter()
@@ -162,10 +186,80 @@ class StreamingEncoder:
                                              non_vad_mode=non_vad)
                 if ph is not None:
                     done.append((s, ph))
-        out = self._encode(done, timestamp) if done else []
-        torch.cuda.synchronize(self.device)
+        if self.asynchronous:
+            if self._error is not None:
+                raise RuntimeError("streaming worker failed") from self._error
+            if done:
+                self._jobs.put((done, timestamp, t0))
+                self.max_queue = max(self.max_queue, self._jobs.qsize())
+            out = self._drain()
+            self.latencies.append(time.perf_counter() - t0)
+            return out
+        out = self._job(done, timestamp, t0) if done else []
         self.latencies.append(time.perf_counter() - t0)
         return out
+
+    def _job(self, done, timestamp, t_submit):
+        res = self._encode(done, timestamp)
+        if self.receiver is not None:
+            self._render(res, done)
+        torch.cuda.current_stream(self.device).synchronize()
+        t = time.perf_counter()
+        for r in res:
+            r["latency_s"] = t - t_submit
+            self.phrase_latencies.append(t - t_submit)
+        return res
+
+    def _render(self, res, done):
+        """The far end's receiver leg for this job's packets (ReceiverBatch semantics):
+        every packet rendered at its phrase's own duration (longest phrase of the job)."""
+        pk = [r["packet"] for r in res]
+        if not any(p is not None for p in pk):
+            return
+        secs = max(len(ph) for _, ph in done) / CAPTURE_RATE
+        frames = max(1, int(np.ceil(secs * 44100 / 512)))
+        wav, pcm, _ = self.receiver.decode(pk, frames)
+        k = 0
+        for r in res:
+            if r["packet"] is not None and JanusPacket.deserialize(r["packet"]).mode != JanusMode.MORSE_CODE:
+                r["pcm16"] = pcm[k]
+                k += 1
+
+    def _run(self):
+        torch.cuda.set_device(self.device)
+        while True:
+            job = self._jobs.get()
+            try:
+                if job is None:
+                    return
+                with torch.cuda.stream(self._side):
+                    self._results.put(self._job(*job))
+            except BaseException as e:  # surfaced by the next push
+                self._error = e
+            finally:
+                self._jobs.task_done()
+
+    def _drain(self):
+        out = []
+        while True:
+            try:
+                out += self._results.get_nowait()
+            except queue.Empty:
+                return out
+
+    def flush(self):
+        """Asynchronous mode: wait for every queued phrase; returns the remaining results."""
+        if not self.asynchronous:
+            return []
+        self._jobs.join()
+        if self._error is not None:
+            raise RuntimeError("streaming worker failed") from self._error
+        return self._drain()
+
+    def close(self):
+        if self.asynchronous and self._worker.is_alive():
+            self._jobs.put(None)
+            self._worker.join()
 
     def _encode(self, done, timestamp):
         streams = [s for s, _ in done]
@@ -220,6 +314,12 @@ class StreamingEncoder:
 
     def p50_ms(self) -> float:
         return float(np.median(self.latencies) * 1000.0) if self.latencies else float("nan")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 __all__ = ["PhraseSegmenter", "VoiceActivityDetector", "StreamingEncoder", "energy_tag",

@@ -152,3 +152,38 @@ def test_receiver_batch(gpu):
         assert out[k][:44] == ref[k][:44] and len(out[k]) == 44 + 12 * 512 * 2
         assert out[k][44:] == duck(ref[k][44:], True, True, 0.25)
     assert out[1] == duck(ref[1], True, True, 0.25)
+
+
+def test_streaming_async_matches_sync(gpu, tiny):
+    """Asynchronous ingest (encode on a worker stream) returns the same phrases, tags and
+    packets per channel, in order, as the blocking push; the duplex receiver leg renders
+    exactly what JanusPipeline.decode renders for those packets."""
+    from janus_amd.pipeline import JanusPipeline
+    S, ticks, per_tick = 3, 14, 10
+    audio = np.zeros((S, ticks * per_tick * CHUNK), np.float32)
+    for s in range(S):
+        a = synth_speech(800 + s, 2.0)
+        b = synth_speech(900 + s, 1.2)
+        audio[s, 3000:3000 + len(a)] = a
+        audio[s, 3000 + len(a) + 40000:3000 + len(a) + 40000 + len(b)] = b
+    rx = JanusPipeline("tiny.en", max_length=8)
+    res = {}
+    for asyn in (False, True):
+        enc = StreamingEncoder(S, tiny, max_length=8, asynchronous=asyn, receiver=rx)
+        got = []
+        for t in range(ticks):
+            got += enc.push(audio[:, t * per_tick * CHUNK:(t + 1) * per_tick * CHUNK], timestamp=7.0)
+        got += enc.flush()
+        enc.close()
+        res[asyn] = got
+        assert all(r["latency_s"] > 0 for r in got) and enc.max_queue >= (1 if asyn else 0)
+    key = lambda r: (r["stream"], r["text"], tuple(r["tags"].items()), r["packet"])
+    a_s, a_a = sorted(map(key, res[False])), sorted(map(key, res[True]))
+    assert a_s == a_a and len(a_s) >= 2
+    for s in range(S):  # per-channel order preserved
+        assert [r["packet"] for r in res[False] if r["stream"] == s] == \
+            [r["packet"] for r in res[True] if r["stream"] == s]
+    for rs in res.values():
+        for r in rs:
+            if r["packet"] is not None:
+                assert "pcm16" in r and r["pcm16"].dtype == torch.int16
