@@ -90,6 +90,27 @@ int janus_duck_pcm16(int16_t* pcm, int64_t n, float level, void* stream);
 int janus_vad_energy(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
                      float center_db, float width_db, float* prob_out, void* stream);
 
+/*
+ * The neural gate itself: VoiceActivityDetector.is_speech's model(chunk[::3], 16000)
+ * (backend/services/vad.py:40-77; silero-vad v5, 16 kHz graph: 64-sample context + STFT
+ * 256/128 + 4 conv blocks + LSTMCell(128) + sigmoid), from local weights. A context
+ * holds the parameters by their silero state-dict names ("_model.stft.forward_basis_buffer",
+ * "_model.encoder.{0..3}.reparam_conv.{weight,bias}", "_model.decoder.rnn.{weight_ih,
+ * weight_hh,bias_ih,bias_hh}", "_model.decoder.decoder.2.{weight,bias}").
+ * janus_vad_run: pcm [device] f32 [n_streams][n_chunks][chunk_len] (chunk[::decim] must
+ * give 512 samples: 1536 / 3 for the 48 kHz capture chunks); the model state of each
+ * channel, carried across calls as silero's stateful model object carries it
+ * (the reference never resets it, vad.py:79-88): ctx_state [device] f32 [n_streams][64],
+ * hc_state [device] f32 [n_streams][2][128] (zeros = fresh), updated in place;
+ * prob_out [device] f32 [n_streams][n_chunks], channels in parallel, chunks in order.
+ */
+typedef struct janus_vad janus_vad;
+int janus_vad_create(janus_vad** out);
+int janus_vad_destroy(janus_vad* v);
+int janus_vad_set_tensor(janus_vad* v, const char* name, const float* host, int64_t numel);
+int janus_vad_run(janus_vad* v, const float* pcm, int n_streams, int n_chunks, int chunk_len,
+                  int decim, float* ctx_state, float* hc_state, float* prob_out, void* stream);
+
 /* -------------------------------------------------------- packet codec --- */
 enum {
   JANUS_VAL_NIL = 0,

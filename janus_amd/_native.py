@@ -50,6 +50,10 @@ SIGNATURES = {
     "janus_stream_destroy": [_P],
     "janus_duck_pcm16": [_P, _I64, _F32, _P],
     "janus_vad_energy": [_P, _I64, _I32, _I32, _F32, _F32, _P, _P],
+    "janus_vad_create": [_P],
+    "janus_vad_destroy": [_P],
+    "janus_vad_set_tensor": [_P, ctypes.c_char_p, _P, _I64],
+    "janus_vad_run": [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P],
     "janus_prosody_analyze": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
                               _P, _P, _P],
     "janus_prosody_analyze_ex": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,

@@ -144,6 +144,24 @@ bool resunit_supported(int C, int k);
 void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s);
 void resunit_launch(const ResUnitArgs& a, hipStream_t s);
 
+// ------------------------------------------------------------------ VAD
+// Silero-vad v5 16 kHz weights (vad.hip), fp32 device pointers by published name.
+struct VadWeights {
+  const float* basis;                // stft.forward_basis_buffer [258][256]
+  const float* w0; const float* b0;  // encoder.0 [128][129][3]
+  const float* w1; const float* b1;  // encoder.1 [64][128][3]
+  const float* w2; const float* b2;  // encoder.2 [64][64][3]
+  const float* w3; const float* b3;  // encoder.3 [128][64][3]
+  const float* wih; const float* whh; const float* bih; const float* bhh;  // LSTMCell(128, 128)
+  const float* wo; const float* bo;  // decoder.2 Conv1d(128, 1, 1)
+};
+// pcm [device] [n_streams][n_chunks][chunk_len] (each chunk decimated by `decim` to 512
+// samples); ctx_state [n_streams][64], hc_state [n_streams][2][128] in/out; prob
+// [n_streams][n_chunks].
+void silero_vad_launch(const float* pcm, int n_streams, int n_chunks, int chunk_len, int decim,
+                       const VadWeights& W, float* ctx_state, float* hc_state, float* prob,
+                       hipStream_t s);
+
 // ------------------------------------------------------------------ mel
 void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* basis,
                 const float* filters, float* logmel, uint32_t* maxkey, int n_frames_out,

@@ -10,9 +10,9 @@ engine.py:438-506), then transcribes + analyses prosody + packs each phrase
 aubio detector (prosody.py:32). Here S channels advance together:
 
 * the speech gate runs for every chunk of every channel in one launch
-  (``janus_vad_energy``; silero's weights are a remote download, so the gate is the
-  documented energy stand-in of include/janus.h — swap in real probabilities through
-  ``push(..., speech=...)``);
+  (services/vad.py: the silero-v5 network with one model state per channel when local
+  weights are given — ``vad_weights=`` or JANUS_VAD_DIR — else the documented energy
+  stand-in; real probabilities can also be passed through ``push(..., speech=...)``);
 * ``PhraseSegmenter`` is the engine's per-chunk state machine, one per channel;
 * phrases that complete on the same tick are encoded as ONE batch on the GPU (log-mel,
   encoder, greedy decoder, YIN + RMS) with each channel's persistent 4096-sample detector
@@ -29,17 +29,13 @@ import torch
 from . import _native as nat
 from .common.protocol import JanusMode, JanusPacket
 from .services.prosody import YIN_BUF, energy_tag, pitch_tag, prosody_launch
+from .services.vad import VAD_CENTER_DB, VAD_WIDTH_DB, MultiStreamGate, VoiceActivityDetector
 
 CHUNK = 1536                  # audio_io.py:28-31 (48 kHz int16 -> f32 chunks)
 PRE_ROLL_CHUNKS = 10          # engine.py:439
 SILENCE_THRESHOLD_CHUNKS = 15  # engine.py:441
 MIN_PHRASE_SAMPLES = CHUNK * 6  # engine.py:504
 CAPTURE_RATE = 48000
-
-# energy stand-in for silero (vad.py:40-77): P(speech) = sigmoid((dB - center) / width)
-VAD_CENTER_DB = -45.0
-VAD_WIDTH_DB = 3.0
-
 
 class PhraseSegmenter:
     """engine.py:438-506 for one channel: feed every chunk with its gate decision; returns
@@ -94,36 +90,6 @@ class PhraseSegmenter:
         return None
 
 
-class VoiceActivityDetector:
-    """Same constructor / is_speech / reset as vad.py:10-88 plus the batched GPU form;
-    probabilities from the energy stand-in (janus_vad_energy), threshold as the reference."""
-
-    def __init__(self, threshold: float = 0.5, sample_rate: int = 48000) -> None:
-        self.device = nat.require_gpu()
-        self.threshold = threshold
-        self.sample_rate = sample_rate
-        self.decim = 3 if sample_rate in (48000, 44100) else 1  # vad.py:54-61
-
-    def probabilities(self, chunks: torch.Tensor) -> torch.Tensor:
-        """chunks: [N][L] f32 on the GPU -> [N] speech probabilities (device)."""
-        assert chunks.is_cuda and chunks.dtype == torch.float32 and chunks.is_contiguous()
-        n, L = chunks.shape
-        prob = torch.empty(max(n, 1), dtype=torch.float32, device=chunks.device)
-        nat.call("janus_vad_energy", chunks.data_ptr(), n, L, self.decim, VAD_CENTER_DB,
-                 VAD_WIDTH_DB, prob.data_ptr(), nat.stream_ptr(chunks.device))
-        return prob[:n]
-
-    def is_speech_batch(self, chunks: torch.Tensor) -> np.ndarray:
-        return (self.probabilities(chunks) > self.threshold).cpu().numpy()
-
-    def is_speech(self, audio_chunk) -> bool:
-        x = torch.as_tensor(np.ascontiguousarray(audio_chunk, np.float32)).to(self.device)
-        return bool(self.is_speech_batch(x.reshape(1, -1))[0])
-
-    def reset(self) -> None:
-        pass
-
-
 class StreamingEncoder:
     """S channels x one JanusPipeline-style encode per completed phrase batch.
 
@@ -144,13 +110,13 @@ class StreamingEncoder:
     def __init__(self, n_streams: int, whisper, max_length: int = 448,
                  mode: JanusMode = JanusMode.SEMANTIC_VOICE, override="auto",
                  vad_threshold: float = 0.5, hop: int = 512, asynchronous: bool = False,
-                 receiver=None):
+                 receiver=None, vad_weights: dict = None):
         self.device = nat.require_gpu()
         self.S = n_streams
         self.whisper = whisper
         self.max_length = max_length
         self.mode, self.override, self.hop = mode, override, hop
-        self.vad = VoiceActivityDetector(vad_threshold, CAPTURE_RATE)
+        self.vad = MultiStreamGate(n_streams, vad_threshold, CAPTURE_RATE, vad_weights)
         self.segmenters = [PhraseSegmenter() for _ in range(n_streams)]
         # one aubio detector buffer per channel (prosody.py:32), persistent across phrases
         self.yin_state = torch.zeros(n_streams, YIN_BUF, dtype=torch.float32, device=self.device)
@@ -176,7 +142,7 @@ class StreamingEncoder:
         if speech is None:
             dev = block if isinstance(block, torch.Tensor) and block.is_cuda else \
                 torch.from_numpy(np.ascontiguousarray(host)).to(self.device)
-            speech = self.vad.is_speech_batch(dev.reshape(S * n, CHUNK).contiguous()).reshape(S, n)
+            speech = self.vad.is_speech(dev.reshape(S, n, CHUNK).contiguous())
         done = []
         # MORSE / TEXT_ONLY bypass the speech gate (engine.py:473-474, is_non_vad_mode)
         non_vad = self.mode in (JanusMode.TEXT_ONLY, JanusMode.MORSE_CODE)

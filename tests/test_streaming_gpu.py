@@ -187,3 +187,37 @@ def test_streaming_async_matches_sync(gpu, tiny):
         for r in rs:
             if r["packet"] is not None:
                 assert "pcm16" in r and r["pcm16"].dtype == torch.int16
+
+
+def test_silero_gate_matches_oracle(gpu):
+    """The neural gate (csrc/vad.hip, silero-vad v5 graph, seeded weights of the published
+    shapes) vs the oracle restatement, 3 channels x 24 capture chunks with per-channel
+    state carried across two calls; decisions identical away from the threshold."""
+    from janus_amd.services.vad import MultiStreamGate, VoiceActivityDetector, synthetic_weights
+    from oracle.vad import OracleSilero
+    W = synthetic_weights(seed=4)
+    rng = np.random.default_rng(9)
+    S, n = 3, 24
+    x = np.zeros((S, n, CHUNK), np.float32)
+    x[0] = (rng.standard_normal((n, CHUNK)) * 0.1).astype(np.float32)
+    x[1] = synth_speech(31, n * CHUNK / 48000.0)[:n * CHUNK].reshape(n, CHUNK)
+    x[2, 8:] = (0.3 * np.sin(2 * np.pi * 300 * np.arange(16 * CHUNK) / 48000)).reshape(16, CHUNK)
+    gate = MultiStreamGate(S, weights=W)
+    assert gate.neural
+    d = torch.from_numpy(x).to(gpu)
+    p = torch.cat([gate.probabilities(d[:, :10].contiguous()), gate.probabilities(d[:, 10:].contiguous())], 1)
+    p = p.cpu().numpy()
+    for s in range(S):
+        o = OracleSilero(W)
+        ref = np.array([o(x[s, j, ::3]) for j in range(n)])
+        assert np.abs(p[s] - ref).max() < 1e-5, (s, np.abs(p[s] - ref).max())
+        far = np.abs(ref - 0.5) > 1e-4
+        assert np.array_equal((p[s] > 0.5)[far], (ref > 0.5)[far])
+    # the drop-in single-stream detector: the same state machine, one chunk per call
+    det = VoiceActivityDetector(weights=W)
+    o = OracleSilero(W)
+    for j in range(n):
+        pr = o(x[1, j, ::3])
+        got = det.is_speech(x[1, j])
+        if abs(pr - 0.5) > 1e-4:
+            assert got == (pr > 0.5)

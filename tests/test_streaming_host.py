@@ -101,3 +101,22 @@ def test_gates():
     assert gates("ab" * 200, -0.3, 0.01) == (True, False)            # repetitive: fallback
     assert gates("hello there", -2.0, 0.9) == (False, True)         # silence: skip, no fallback
     assert gates("hello there", -0.5, 0.9) == (False, False)        # confident text: keep
+
+
+def test_silero_oracle_basis_and_state():
+    """The silero STFT basis is the Hann-windowed DFT (a 1 kHz tone peaks in bin 16 of
+    256 at 16 kHz); the oracle model is deterministic and stateful across calls."""
+    import torch.nn.functional as F
+    import torch
+    from janus_amd.services.vad import stft_basis, synthetic_weights
+    from oracle.vad import OracleSilero
+    b = stft_basis()
+    t = np.sin(2 * np.pi * 1000 * np.arange(256) / 16000).astype(np.float32)
+    mag = np.hypot(b[:129] @ t, b[129:] @ t)
+    assert int(np.argmax(mag)) == 16
+    W = synthetic_weights(seed=1)
+    a, c = OracleSilero(W), OracleSilero(W)
+    chunk = np.random.default_rng(0).standard_normal(512).astype(np.float32) * 0.1
+    p1, p2 = a(chunk), a(chunk)
+    assert 0.0 < p1 < 1.0 and p1 != p2          # state carried
+    assert c(chunk) == p1                        # deterministic from a fresh state
