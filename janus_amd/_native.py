@@ -11,6 +11,9 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libjanus_hip.so")
+# A/B experiments only: JANUS_LIB names an alternative in-tree build (e.g. libjanus_hip_nt.so)
+if os.environ.get("JANUS_LIB"):
+    LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.path.basename(os.environ["JANUS_LIB"]))
 
 
 class JanusNativeError(RuntimeError):

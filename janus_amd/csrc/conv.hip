@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
       const int row = idx / PER_ROW, cc = idx % PER_ROW;
       const int gr = row_base + row;
       pf[i] = (row < nrows && gr >= 0 && gr < a.T_in)
-                  ? *reinterpret_cast<const uint4*>(inb + (int64_t)gr * a.Cin + c * CK + cc * 8)
+                  ? ld_act(inb + (int64_t)gr * a.Cin + c * CK + cc * 8)
                   : make_uint4(0, 0, 0, 0);
     }
   };
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
       const int gr = row_base + row;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (gr >= 0 && gr < a.T_in) {
-        v = *reinterpret_cast<const uint4*>(inb + (int64_t)gr * a.Cin + c * CK + cc * 8);
+        v = ld_act(inb + (int64_t)gr * a.Cin + c * CK + cc * 8);
         if constexpr (PRE != ACT_NONE) {
           _Float16* hv = reinterpret_cast<_Float16*>(&v);
 #pragma unroll
@@ -272,8 +272,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
     const int t = r * a.out_stride + a.out_off + ph;
     const bool ok = r < a.n_rows && co < a.Cout && t >= 0 && t < a.T_out;
     oo[i] = ok ? (int64_t)t * a.Cout + co : -1;
-    rq[i] = (ok && resb) ? *reinterpret_cast<const uint4*>(resb + oo[i]) : make_uint4(0, 0, 0, 0);
-    pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(outb + oo[i])
+    rq[i] = (ok && resb) ? ld_res(resb + oo[i]) : make_uint4(0, 0, 0, 0);
+    pq[i] = (ok && a.accumulate) ? ld_res(outb + oo[i])
                                  : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int rows_max) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)rv[j]) * a.out_scale + (float)pv[j]);
     }
-    *reinterpret_cast<half8*>(outb + oo[i]) = hv;
+    st_act(outb + oo[i], hv);
   }
 }
 

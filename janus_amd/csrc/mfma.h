@@ -43,6 +43,50 @@ __device__ __forceinline__ float silu(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
 
+// Streaming activation traffic of the vocoder (tiles read once per unit, outputs written
+// once): with JANUS_ACT_NT the accesses carry the non-temporal hint, so the multi-GB
+// vocoder stream does not displace what the concurrently running decoder re-reads
+// (encoder output, weights) from the caches.
+// Measured (overlapped bench step, r02): non-temporal OUTPUT stores are the default —
+// 324.3 -> 319.3 ms, both sides faster (decoder -5.5 ms: its re-read encoder output and
+// weights survive in the caches; vocoder -3 ms); non-temporal loads as well cost the
+// vocoder +4.5 ms (the tile's halo / residual re-reads then miss) for a -3 ms decoder.
+// Switches for A/B builds: JANUS_ACT_NT (loads too), or the parts _LD (tile staging
+// loads), _RES (epilogue residual / accumulator re-reads); JANUS_ACT_ST_PLAIN (plain stores).
+#ifdef JANUS_ACT_NT
+#define JANUS_ACT_NT_LD
+#define JANUS_ACT_NT_RES
+#endif
+#ifndef JANUS_ACT_ST_PLAIN
+#define JANUS_ACT_NT_ST
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const _Float16* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ld_act(const _Float16* p) {  // tile staging
+#ifdef JANUS_ACT_NT_LD
+  return ld_nt(p);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+__device__ __forceinline__ uint4 ld_res(const _Float16* p) {  // epilogue re-reads
+#ifdef JANUS_ACT_NT_RES
+  return ld_nt(p);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+__device__ __forceinline__ void st_act(_Float16* p, const half8& v) {
+#ifdef JANUS_ACT_NT_ST
+  __builtin_nontemporal_store(v, reinterpret_cast<half8*>(p));
+#else
+  *reinterpret_cast<half8*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ half8 zero_half8() {
   half8 z;
 #pragma unroll

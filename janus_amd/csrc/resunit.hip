@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       const int r = idx / CPR, cc = idx % CPR;                                              \
       const int t = t0_ - P2 - P1 + r;                                                      \
       pf[i] = (tl_ < n_tiles && r < R0 && t >= 0 && t < T)                                 \
-                  ? *reinterpret_cast<const uint4*>(xb_ + (int64_t)t * C + cc * 8)          \
+                  ? ld_act(xb_ + (int64_t)t * C + cc * 8)                                 \
                   : make_uint4(0, 0, 0, 0);                                                 \
     }                                                                                       \
   } while (0)
@@ -173,10 +173,10 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const bool ok = r < BM && t0 + r < T;
       if constexpr (!G::RES_LDS)
-        xres[i] = ok ? *reinterpret_cast<const uint4*>(xb + (int64_t)(t0 + r) * C + cg)
+        xres[i] = ok ? ld_res(xb + (int64_t)(t0 + r) * C + cg)
                      : make_uint4(0, 0, 0, 0);
       acc_in[i] = (a.accumulate && ok)
-                      ? *reinterpret_cast<const uint4*>(ob + (int64_t)(t0 + r) * C + cg)
+                      ? ld_res(ob + (int64_t)(t0 + r) * C + cg)
                       : make_uint4(0, 0, 0, 0);
     }
 
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
 #pragma unroll
         for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
       }
-        *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+        st_act(ob + (int64_t)(t0 + r) * C + cg, hv);
       }
     }
   }

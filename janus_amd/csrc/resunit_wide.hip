@@ -173,7 +173,7 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
       const int t = xbase + r;
       // unconditional load of a clamped row, zeroed below (no branch per load)
       const int tc = min(max(t, 0), T - 1);
-      pf[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)tc * C + cc * 8);
+      pf[i] = ld_act(xb + (int64_t)tc * C + cc * 8);
       if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -229,8 +229,8 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const bool ok = r < BM && t0 + r < T;
       const int64_t o = (int64_t)(t0 + r) * C + cg;
-      rq[i] = ok ? *reinterpret_cast<const uint4*>(xb + o) : make_uint4(0, 0, 0, 0);
-      pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(ob + o) : make_uint4(0, 0, 0, 0);
+      rq[i] = ok ? ld_res(xb + o) : make_uint4(0, 0, 0, 0);
+      pq[i] = (ok && a.accumulate) ? ld_res(ob + o) : make_uint4(0, 0, 0, 0);
     }
   };
   if constexpr (G::Cfg::EPF) epi_load();
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
 #pragma unroll
         for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
       }
-      *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+      st_act(ob + (int64_t)(t0 + r) * C + cg, hv);
     }
   }
 }
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
       const int t = xbase + r;
       // unconditional load of a clamped row, zeroed below (no branch per load)
       const int tc = min(max(t, 0), T - 1);
-      pf[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)tc * C + cc * 8);
+      pf[i] = ld_act(xb + (int64_t)tc * C + cc * 8);
       if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
     WIDE_WLOAD(rwA0, rwA1, a.w1, 0);
@@ -513,8 +513,8 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const bool ok = r < BM && t0 + r < T;
       const int64_t o = (int64_t)(t0 + r) * C + cg;
-      rq[i] = ok ? *reinterpret_cast<const uint4*>(xb + o) : make_uint4(0, 0, 0, 0);
-      pq[i] = (ok && a.accumulate) ? *reinterpret_cast<const uint4*>(ob + o) : make_uint4(0, 0, 0, 0);
+      rq[i] = ok ? ld_res(xb + o) : make_uint4(0, 0, 0, 0);
+      pq[i] = (ok && a.accumulate) ? ld_res(ob + o) : make_uint4(0, 0, 0, 0);
     }
   };
   if constexpr (EPF) epi_load();
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
 #pragma unroll
         for (int j = 0; j < 8; ++j) hv[j] = (_Float16)silu((v[j] + (float)xv[j]) * a.scale + (float)pv[j]);
       }
-    *reinterpret_cast<half8*>(ob + (int64_t)(t0 + r) * C + cg) = hv;
+    st_act(ob + (int64_t)(t0 + r) * C + cg, hv);
   }
 }
 

@@ -157,13 +157,11 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
     for (int o = 0; o < kPostR; ++o)
       if (t + o < T) pre_tanh[(int64_t)b * T + t + o] = acc[o];
   }
-  if (t + kPostR <= T && (T & 3) == 0) {  // aligned full group: vector stores
-    *reinterpret_cast<float4*>(wo) = make_float4(y[0], y[1], y[2], y[3]);
-    if (po) {
-      short4 v4;
-      v4.x = q16[0]; v4.y = q16[1]; v4.z = q16[2]; v4.w = q16[3];
-      *reinterpret_cast<short4*>(po) = v4;
-    }
+  if (t + kPostR <= T && (T & 3) == 0) {  // aligned full group: vector stores, non-temporal
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef short s4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{y[0], y[1], y[2], y[3]}, reinterpret_cast<f4v*>(wo));
+    if (po) __builtin_nontemporal_store(s4v{q16[0], q16[1], q16[2], q16[3]}, reinterpret_cast<s4v*>(po));
   } else {
 #pragma unroll
     for (int o = 0; o < kPostR; ++o) {
