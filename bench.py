@@ -113,6 +113,25 @@ def cpu_baseline(model: str, tokens_per_utt: float):
     }
 
 
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
+
+
+def family_lines(fams, cu_share):
+    out = []
+    for f, v in sorted(fams.items()):
+        if v["ms"] <= 0:
+            continue
+        tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+        gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+        mf = tf / (MFMA_F16_PEAK_TFLOPS * cu_share)
+        hf = gbs / (HBM_PEAK_GBS * cu_share)
+        out.append({"family": "conv" if f == 0 else f"unit C={f}", "launches": v["launches"],
+                    "ms": round(v["ms"], 2), "achieved_tflops": round(tf, 1),
+                    "mfma_frac_of_share": round(mf, 3), "hbm_gbs_algorithmic": round(gbs, 1),
+                    "hbm_frac_of_share": round(hf, 3), "bound": "mfma" if mf >= hf else "hbm"})
+    return out
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -189,6 +208,7 @@ def main():
     t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
     tok_counts = [float(n.float().mean().item()) for n in tok_counts]
+    fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
     total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
@@ -280,6 +300,10 @@ def main():
                 # overlapped step: the conv launches own only the vocoder's CU share
                 "cu_share": cu_share,
                 "frac_of_cu_share": round(achieved / (MFMA_F16_PEAK_TFLOPS * cu_share), 4),
+                # per family (fused-unit channel width; 0 = conv_pre + upsamplers): MFMA rate
+                # and algorithmic HBM rate against their peaks on the CU share; "bound" =
+                # the resource nearer its roofline (the narrow units are not MFMA-bound)
+                "families": family_lines(fams, cu_share),
             },
             "cpu_baseline": None,
         }

@@ -348,6 +348,14 @@ int janus_vocoder_set_timing(janus_vocoder* v, int on);
 /* Accumulated conv FLOPs (2*Cin*Cout*taps*rows), kernel milliseconds and launches. */
 int janus_vocoder_conv_stats(janus_vocoder* v, double* flops, double* ms, int64_t* launches,
                              int reset);
+/*
+ * The same per family: fam[i] = channel width C of the fused ResBlock1 units (4*C*C*k
+ * FLOP and 2-3 x C x 2 B of activations per row), or 0 for the conv kernel (conv_pre and
+ * the upsamplers). Up to cap families; *n = how many were written. Algorithmic bytes:
+ * fp16 activations read once and written once (+ the accumulator / residual reads).
+ */
+int janus_vocoder_family_stats(janus_vocoder* v, int cap, int* fam, double* flops, double* bytes,
+                               double* ms, int64_t* launches, int* n, int reset);
 
 #ifdef __cplusplus
 }

@@ -38,8 +38,11 @@ struct VUnit {  // fused (convs1[m], convs2[m]) pair for narrow stages
 };
 struct TimedLaunch {
   hipEvent_t a, b;
-  double flops;
+  double flops, bytes;  // algorithmic: MFMA FLOPs, fp16 activation bytes read once / written once
+  int fam;              // channel width of a fused ResBlock1 unit, 0 for the conv kernel
 };
+// per-family accumulators (index by slot: 0 conv, then C = 16 .. 512)
+struct FamStat { int fam = -1; double flops = 0, bytes = 0, ms = 0; int64_t launches = 0; };
 }  // namespace janus
 
 struct janus_vocoder {
@@ -62,6 +65,7 @@ struct janus_vocoder {
   std::vector<hipEvent_t> pool;
   double t_flops = 0, t_ms = 0;
   int64_t t_launches = 0;
+  janus::FamStat fam[8];
 };
 
 namespace janus {
@@ -156,6 +160,8 @@ static void run_conv(janus_vocoder* v, const VConv& cv, const _Float16* in, int 
     t.b = take_event(v);
     const int taps = cv.transposed ? 2 : cv.taps;
     t.flops = 2.0 * cv.cin * cv.cout * taps * (double)T_out * B;
+    t.bytes = 2.0 * B * ((double)T_in * cv.cin + (double)T_out * cv.cout * (1 + (res ? 1 : 0) + (acc ? 1 : 0)));
+    t.fam = 0;
     JANUS_HIP(hipEventRecord(t.a, s));
     conv_launch(a, s);
     JANUS_HIP(hipEventRecord(t.b, s));
@@ -176,6 +182,8 @@ static void run_unit(janus_vocoder* v, const VUnit& U, const _Float16* x, _Float
     t.a = take_event(v);
     t.b = take_event(v);
     t.flops = 2.0 * 2.0 * U.c * U.c * U.k * (double)T * B;
+    t.bytes = 2.0 * B * (double)T * U.c * (2 + (acc ? 1 : 0));
+    t.fam = U.c;
     JANUS_HIP(hipEventRecord(t.a, s));
     resunit_launch(a, s);
     JANUS_HIP(hipEventRecord(t.b, s));
@@ -252,6 +260,12 @@ static void collect_timing(janus_vocoder* v) {
     v->t_ms += ms;
     v->t_flops += t.flops;
     v->t_launches += 1;
+    for (auto& f : v->fam) {
+      if (f.fam != t.fam && f.fam != -1) continue;
+      f.fam = t.fam;
+      f.flops += t.flops; f.bytes += t.bytes; f.ms += ms; f.launches += 1;
+      break;
+    }
     v->pool.push_back(t.a);
     v->pool.push_back(t.b);
   }
@@ -374,6 +388,24 @@ extern "C" int janus_vocoder_conv_stats(janus_vocoder* v, double* flops, double*
     *flops = v->t_flops;
     *ms = v->t_ms;
     *launches = v->t_launches;
-    if (reset) { v->t_flops = 0; v->t_ms = 0; v->t_launches = 0; }
+    if (reset) { v->t_flops = 0; v->t_ms = 0; v->t_launches = 0; for (auto& f : v->fam) f = FamStat(); }
+  });
+}
+
+extern "C" int janus_vocoder_family_stats(janus_vocoder* v, int cap, int* fam, double* flops,
+                                          double* bytes, double* ms, int64_t* launches, int* n,
+                                          int reset) {
+  return guarded([&] {
+    JANUS_CHECK(v && fam && flops && bytes && ms && launches && n && cap > 0, "null argument");
+    std::lock_guard<std::mutex> lk(v->mu);
+    collect_timing(v);
+    int k = 0;
+    for (auto& f : v->fam) {
+      if (f.fam < 0 || k >= cap) continue;
+      fam[k] = f.fam; flops[k] = f.flops; bytes[k] = f.bytes; ms[k] = f.ms; launches[k] = f.launches;
+      ++k;
+    }
+    *n = k;
+    if (reset) { v->t_flops = 0; v->t_ms = 0; v->t_launches = 0; for (auto& f : v->fam) f = FamStat(); }
   });
 }

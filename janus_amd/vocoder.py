@@ -230,6 +230,18 @@ class VocoderEngine:
     def set_timing(self, on: bool) -> None:
         nat.call("janus_vocoder_set_timing", self._h, int(on))
 
+    def family_stats(self, reset: bool = True):
+        """{family: dict(flops, bytes, ms, launches)} of the timed launches; family = the
+        fused unit's channel width, 0 = conv kernel (conv_pre, upsamplers)."""
+        cap = 8
+        fam = (ctypes.c_int * cap)()
+        fl, by, ms = (ctypes.c_double * cap)(), (ctypes.c_double * cap)(), (ctypes.c_double * cap)()
+        la = (ctypes.c_int64 * cap)()
+        n = ctypes.c_int()
+        nat.call("janus_vocoder_family_stats", self._h, cap, fam, fl, by, ms, la, ctypes.addressof(n),
+                 int(reset))
+        return {fam[i]: dict(flops=fl[i], bytes=by[i], ms=ms[i], launches=la[i]) for i in range(n.value)}
+
     def conv_stats(self, reset: bool = True):
         fl, ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         nat.call("janus_vocoder_conv_stats", self._h, ctypes.addressof(fl), ctypes.addressof(ms),
