@@ -53,7 +53,7 @@ def parse():
                     help="CUs per XCD (of 32) for the greedy decoder in the overlapped serving step "
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
 
 

@@ -117,6 +117,8 @@ struct ConvArgs {
   float out_scale; int accumulate;      // out = (accumulate ? out : 0) + out_scale * y
   int B;
   int post_acc_silu = 0;                // out = silu(out) after the accumulation
+  int remap = -1;                       // tile order: 0 dispatch, 1 XCD runs of row blocks,
+                                        // 2 XCD runs over the whole grid; -1 = default
 };
 struct ConvPack { int ck, kb, chunks, groups; int64_t phase_elems; };
 ConvPack conv_pack_geometry(int Cin, int Cout, int taps);

@@ -122,6 +122,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// The vocoder kernels' tile order (JANUS_NO_TILE_REMAP: plain dispatch order, for A/B
+// builds). Remapped, the standalone vocoder's L2->fabric traffic fell from 1.42x to
+// 1.19x the algorithmic bytes (profiles/traffic_r02.json).
+__device__ __forceinline__ int tile_remap(int bid, int nblocks) {
+#ifdef JANUS_NO_TILE_REMAP
+  return bid;
+#else
+  return xcd_remap(bid, nblocks);
+#endif
+}
+
 // LayerNorm of R fp32 rows by one wave (rows row0 + j*rstep, j < R; d <= 256*MAXV, d % 4
 // == 0): every row, gamma and beta load is issued before the first use (one memory round
 // trip for all R rows); fp16 out rows at out + (lrow0 + j*rstep)*ldo, ALL R of them written

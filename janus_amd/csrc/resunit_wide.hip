@@ -155,7 +155,10 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
   const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
-  const int b = blockIdx.x / tiles_per_utt, t0 = (blockIdx.x % tiles_per_utt) * BM;
+  // consecutive tiles on one XCD: a tile's halo rows are its neighbour's, staged through
+  // the same L2
+  const int tile = tile_remap(blockIdx.x, gridDim.x);
+  const int b = tile / tiles_per_utt, t0 = (tile % tiles_per_utt) * BM;
   const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
   const int wm = wid % WM, wn = wid / WM;
   const _Float16* xb = a.x + (int64_t)b * T * C;
@@ -363,7 +366,10 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
   const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
-  const int b = blockIdx.x / tiles_per_utt, t0 = (blockIdx.x % tiles_per_utt) * BM;
+  // consecutive tiles on one XCD: a tile's halo rows are its neighbour's, staged through
+  // the same L2
+  const int tile = tile_remap(blockIdx.x, gridDim.x);
+  const int b = tile / tiles_per_utt, t0 = (tile % tiles_per_utt) * BM;
   const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
   const int wm = wid % WM, wn = wid / WM;
   const _Float16* xb = a.x + (int64_t)b * T * C;
