@@ -8,6 +8,7 @@
 // ApplyTimestampRules incl. max_initial_timestamp, then argmax) and accumulates the
 // chosen token's log-probability (avg_logprob).
 #include <cfloat>
+#include <cstdlib>
 #include "mfma.h"
 #include "kernels.h"
 #include "decoder.h"
@@ -368,7 +369,9 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
 // running per-row statistics without shuffles; at the end the 8 waves' statistics are
 // merged per row (wave order) into ONE partial per (row, block) for the selector.
 
-template <int NKS>  // K / 32
+// NB: weight tiles in flight per wave (2: two register sets, the tile two strides ahead is
+// issued after this tile's MFMAs, so each load has two tile-times to land)
+template <int NKS, int NB>  // K / 32
 __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
@@ -384,11 +387,22 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   // the first tile's weights and suppress-mask bytes are issued before A is staged (they
   // do not depend on it); later tiles' loads are issued before the previous epilogue
-  half8 bw[NKS];
-  uint4 sm16;
-#define LG_LOAD(TILE)                                                                         do {                                                                                          const int bcol_ = min((TILE) * 16 + (lane & 15), V - 1);                                    const _Float16* wrow_ = W + (int64_t)bcol_ * K + 8 * (lane >> 4);                           _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks)                                            bw[ks] = *reinterpret_cast<const half8*>(wrow_ + 32 * ks);                                /* 16 mask bytes per tile (the mask buffer is padded to a multiple of 16) */                 sm16 = *reinterpret_cast<const uint4*>(smask + (TILE) * 16);                              } while (0)
+  half8 bw[NB][NKS];
+  uint4 sm16[NB];
+#define LG_LOAD(BUF, TILE)                                                                    \
+  do {                                                                                        \
+    const int bcol_ = min((TILE) * 16 + (lane & 15), V - 1);                                  \
+    const _Float16* wrow_ = W + (int64_t)bcol_ * K + 8 * (lane >> 4);                         \
+    _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks)                                        \
+      bw[BUF][ks] = *reinterpret_cast<const half8*>(wrow_ + 32 * ks);                         \
+    /* 16 mask bytes per tile (the mask buffer is padded to a multiple of 16) */             \
+    sm16[BUF] = *reinterpret_cast<const uint4*>(smask + (TILE) * 16);                         \
+  } while (0)
   const int tile0 = blockIdx.x * kLgWaves + w;
-  if (tile0 < ntiles) LG_LOAD(tile0);
+  const int stride = gridDim.x * kLgWaves;
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+    if (tile0 + u * stride < ntiles) LG_LOAD(u, tile0 + u * stride);
   if (lnx) {  // A = the decoder's final LayerNorm of x, computed here (one wave per row)
     // wave w: rows w + 8j (j < 8), all loads up front
     ln_rows_wave<(K + 255) / 256, 64 / kLgWaves>(lnx, ldx, w, kLgWaves, B, ln_g, ln_b, sA, w, AP, K,
@@ -418,8 +432,11 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   float ba_v = -INFINITY, bt_v = -INFINITY;
   int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
   float m_raw = -INFINITY, s_raw = 0.f, t_v = -INFINITY;  // unfiltered softmax, target logit
-  const int stride = gridDim.x * kLgWaves;
-  for (int tile = tile0; tile < ntiles; tile += stride) {
+  for (int tb = tile0; tb < ntiles; tb += NB * stride) {
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int tile = tb + u * stride;
+    if (tile >= ntiles) break;  // wave-uniform
     const int col0 = tile * 16;
     f32x4 acc[4];
 #pragma unroll
@@ -429,15 +446,16 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const half8 a = *reinterpret_cast<const half8*>(sA + (16 * m + lr) * AP + 32 * ks + kc8);
-        acc[m] = mfma16(a, bw[ks], acc[m]);
+        acc[m] = mfma16(a, bw[u][ks], acc[m]);
       }
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) patch[(16 * m + 4 * (lane >> 4) + r) * 17 + lr] = acc[m][r];
-    const uint4 smc = sm16;
-    if (tile + stride < ntiles) LG_LOAD(tile + stride);  // next tile's weights during the epilogue
+    const uint4 smc = sm16[u];
+    // the tile NB strides ahead into the registers just consumed, during the epilogue
+    if (tile + NB * stride < ntiles) LG_LOAD(u, tile + NB * stride);
     // wave-private patch: the wave's own stores are visible to its loads in order
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     const int row = lane;
@@ -482,6 +500,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     s_raw = lse_merge(m_raw, s_raw, t_raw, u_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, t_text);
   }
+  }
   // merge the 8 waves' statistics per row (wave order), one partial per (row, block)
   __syncthreads();  // every wave is done with its patch: reuse sT for the wave partials
   LogitPart* wp = reinterpret_cast<LogitPart*>(sT);  // [kLgWaves][64]
@@ -519,10 +538,14 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   const int ntiles = (V + 15) / 16;
   const int nw = lg_waves(K);
   const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)nw * 64 * 17 * 4 + 64 * sizeof(RowRules);
-  auto kern = K == 384 ? logits_partial_kernel<12> : K == 512 ? logits_partial_kernel<16>
-                                                              : logits_partial_kernel<24>;
-  static bool attr[3] = {false, false, false};
-  const int ai = K == 384 ? 0 : K == 512 ? 1 : 2;
+  // weight tiles in flight per wave (JANUS_LG_DEPTH=2: two)
+  static const int depth = std::getenv("JANUS_LG_DEPTH") ? std::atoi(std::getenv("JANUS_LG_DEPTH")) : 1;
+  auto kern = depth > 1 ? (K == 384 ? logits_partial_kernel<12, 2> : K == 512 ? logits_partial_kernel<16, 2>
+                                                                            : logits_partial_kernel<24, 1>)
+                        : (K == 384 ? logits_partial_kernel<12, 1> : K == 512 ? logits_partial_kernel<16, 1>
+                                                                            : logits_partial_kernel<24, 1>);
+  static bool attr[6] = {false, false, false, false, false, false};
+  const int ai = (K == 384 ? 0 : K == 512 ? 1 : 2) + (depth > 1 ? 3 : 0);
   if (!attr[ai]) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
