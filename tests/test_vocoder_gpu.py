@@ -54,6 +54,34 @@ def test_generator_rms(voc, frames, B):
     assert np.array_equal(pcm.cpu().numpy(), ov.pcm16(got.numpy()))
 
 
+def test_family_stats(voc):
+    """Per-family roofline accounting (janus_vocoder_family_stats): one forward = 6 conv
+    launches (conv_pre + 5 upsamplers) and 9 fused units per channel width; the families
+    sum to the whole-family totals, and the algorithmic FLOPs are the closed forms."""
+    eng, W = voc
+    B, frames = 2, 8
+    lat = eng.frontend([b"(joyful) a", b"(sad) b"], [0, 1], frames)
+    eng.set_timing(True)
+    eng.forward(lat)
+    torch.cuda.synchronize()
+    fams = eng.family_stats(reset=False)
+    flops, ms, launches = eng.conv_stats(reset=True)
+    eng.set_timing(False)
+    assert sorted(fams) == [0, 16, 32, 64, 128, 256]
+    assert fams[0]["launches"] == 6
+    assert all(fams[c]["launches"] == 9 for c in (16, 32, 64, 128, 256))
+    assert sum(v["launches"] for v in fams.values()) == launches
+    assert abs(sum(v["flops"] for v in fams.values()) - flops) <= 1e-6 * flops
+    assert abs(sum(v["ms"] for v in fams.values()) - ms) <= 1e-6 * max(ms, 1e-9)
+    # fused unit at width C, time rows T: both convs, 2*C*C*k FLOP per row each
+    T = {256: frames * 8, 128: frames * 64, 64: frames * 128, 32: frames * 256, 16: frames * 512}
+    for C, t in T.items():
+        want = sum(2 * 2 * C * C * k * B * t for k in CFG.rb_kernels for _ in CFG.rb_dilations)
+        assert abs(fams[C]["flops"] - want) <= 1e-9 * want, (C, fams[C]["flops"], want)
+        assert fams[C]["bytes"] >= 2 * 2 * B * t * C * 9  # read + write of every unit
+        assert fams[C]["ms"] > 0
+
+
 def test_speaker_embedding(voc):
     """Voice vector of reference recordings (janus_vocoder_speaker) vs the oracle, and the
     frontend with it exact to fp16."""
