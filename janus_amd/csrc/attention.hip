@@ -614,12 +614,20 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
 #pragma unroll
   for (int i = 0; i < kHeadRounds; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
+#ifdef JANUS_KV_NT
+    kr[i] = ld_nt(kb + (int64_t)t * kv_rs);
+#else
     kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs);
+#endif
   }
 #pragma unroll
   for (int i = 0; i < kHeadRounds; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
+#ifdef JANUS_KV_NT
+    vr[i] = ld_nt(vb + (int64_t)t * kv_rs);
+#else
     vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs);
+#endif
   }
   float sc[kHeadRounds];
   float m = -INFINITY;

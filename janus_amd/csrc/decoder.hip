@@ -389,12 +389,17 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   // do not depend on it); later tiles' loads are issued before the previous epilogue
   half8 bw[NB][NKS];
   uint4 sm16[NB];
+#ifdef JANUS_W_NT
+#define LG_WLD(P) ([&]() { const uint4 u_ = ld_nt(P); return *reinterpret_cast<const half8*>(&u_); }())
+#else
+#define LG_WLD(P) (*reinterpret_cast<const half8*>(P))
+#endif
 #define LG_LOAD(BUF, TILE)                                                                    \
   do {                                                                                        \
     const int bcol_ = min((TILE) * 16 + (lane & 15), V - 1);                                  \
     const _Float16* wrow_ = W + (int64_t)bcol_ * K + 8 * (lane >> 4);                         \
     _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks)                                        \
-      bw[BUF][ks] = *reinterpret_cast<const half8*>(wrow_ + 32 * ks);                         \
+      bw[BUF][ks] = LG_WLD(wrow_ + 32 * ks);                                                  \
     /* 16 mask bytes per tile (the mask buffer is padded to a multiple of 16) */             \
     sm16[BUF] = *reinterpret_cast<const uint4*>(smask + (TILE) * 16);                         \
   } while (0)
@@ -529,6 +534,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   }
 }
 #undef LG_LOAD
+#undef LG_WLD
 
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,

@@ -251,7 +251,14 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
     for (int g = 0; g < G; ++g) {
       const int kk = k0 + 32 * g + kc8;
       const bool ok = kk < kend;
+#ifdef JANUS_W_NT
+      {
+        const uint4 u = (ok && bcol < N) ? ld_nt(wrow + kk) : make_uint4(0, 0, 0, 0);
+        bw[g] = *reinterpret_cast<const half8*>(&u);
+      }
+#else
       bw[g] = (ok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kk) : zero_half8();
+#endif
 #pragma unroll
       for (int m = 0; m < MTB; ++m) {
         const int r = r0 + m * 16 + lr;

@@ -127,7 +127,14 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
     const _Float16* src = eb + (int64_t)key * D + kh * KH + 8 * lg;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
+#ifdef JANUS_XATTN_NT
+    {
+      const uint4 u = ok ? ld_nt(src + 32 * ks) : make_uint4(0, 0, 0, 0);
+      ef[ks] = *reinterpret_cast<const half8*>(&u);
+    }
+#else
       ef[ks] = ok ? *reinterpret_cast<const half8*>(src + 32 * ks) : zero_half8();
+#endif
   };
 
   f32x4 accc[NT];

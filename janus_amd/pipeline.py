@@ -176,6 +176,8 @@ class JanusPipeline:
             dmask, vmask = nat.split_cu_masks(n, dec_per_xcd)
             self._dec_s = nat.MaskedStream(dmask, device)
             self._voc_s = nat.MaskedStream(vmask, device)
+            # a second stream on the decoder's CUs: YIN beside the latency-bound decoder
+            self._yin_s = nat.MaskedStream(dmask, device)
             self._split_key = key
         return self._dec_s.stream, self._voc_s.stream
 
@@ -215,6 +217,7 @@ class JanusPipeline:
         # 0 / 4 / 8 / 11 -> 328.9 / 327.8 / 326.7 / 327.9 ms per step)
         n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(max(1, B // 8)))))
                  if yin_side == "voc" else 0)
+        ys = self._yin_s.stream if yin_side == "beside" else None
         pres = None
         hi.wait_stream(main)
         if yin_side == "early":  # on the vocoder's CUs, beside the (high-priority) encoder
@@ -243,6 +246,14 @@ class JanusPipeline:
                 pres = yin(n_dec, B)
             if timing:
                 ev[1].record(vs)  # before the decoder call, which blocks the host
+        if ys is not None:  # YIN concurrently with the decoder, on its CUs, capped grid
+            ys.wait_stream(hi)
+            yin_cap = int(os.environ.get("JANUS_YIN_BESIDE_BLOCKS", "128"))
+            with torch.cuda.stream(ys):
+                try:
+                    pres = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=yin_cap)
+                except Exception:  # engine.py:520-525
+                    pres = None
         with torch.cuda.stream(ds):
             if yin_side == "dec":
                 pres = yin()
@@ -250,7 +261,8 @@ class JanusPipeline:
             # ms); cu_count: the vocabulary projection at one block per CU of the partition
             # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms) and row-split skinny
             # projections from N <= 1024 (vs 2048: 310.5 -> 306.3 ms)
-            dec = w.decode_ex(enc, max_length=self.max_length, xattn_splits=4,
+            dec = w.decode_ex(enc, max_length=self.max_length,
+                              xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
                               cu_count=self._dec_s.n_cus)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
@@ -258,6 +270,8 @@ class JanusPipeline:
             ev[3].record(ds)
         main.wait_stream(ds)
         main.wait_stream(vs)
+        if ys is not None:
+            main.wait_stream(ys)
         if timing:
             torch.cuda.synchronize()
             print(f"[overlap] vocoder side {ev[0].elapsed_time(ev[1]):.1f} ms, decoder side "
