@@ -30,6 +30,13 @@ int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, i
                    const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
                    int N, int K, void* stream);
 
+/* The same product on hipBLASLt (the encoder's large-M projections): epi F16 / F32 /
+ * RESID_F32 (C == R in place) / GELU_F16 (bias epilogue, then an exact-erf GELU pass);
+ * bias required. Error when the library has no plan for the shape. */
+int janus_gemm_lt_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                      const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
+                      int N, int K, void* stream);
+
 /* LayerNorm rows of an fp32 [rows][d] tensor into fp16 (eps as given). */
 /* C = epilogue(LayerNorm(x) W^T + bias) for M <= 64 rows: the LayerNorm of each block's
  * rows (fp32 x, row stride ldx; gamma/beta f32 [K]; two-pass fp32 statistics) is computed in

@@ -534,4 +534,24 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }
 
+// exact-erf GELU in place, 8 halves per thread (the library GEMM's fc1 epilogue)
+__global__ void gelu_inplace_f16_kernel(_Float16* __restrict__ x, int64_t ld, int M, int N8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * N8) return;
+  const int64_t r = i / N8, c = (i % N8) * 8;
+  half8* p = reinterpret_cast<half8*>(x + r * ld + c);
+  half8 v = *p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (_Float16)gelu_erf((float)v[j]);
+  *p = v;
+}
+
+void gelu_inplace_f16_launch(_Float16* x, int64_t ld, int M, int N, hipStream_t s) {
+  JANUS_CHECK(N % 8 == 0 && ld % 8 == 0, "gelu_inplace: N and ld must be multiples of 8");
+  const int64_t n = (int64_t)M * (N / 8);
+  if (n == 0) return;
+  gelu_inplace_f16_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(x, ld, M, N / 8);
+  JANUS_LAUNCH_CHECK();
+}
+
 }  // namespace janus

@@ -48,6 +48,19 @@ extern "C" int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uin
   });
 }
 
+extern "C" int janus_gemm_lt_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W,
+                                 int64_t ldw, const float* bias, void* C, int64_t ldc,
+                                 const float* R, int64_t ldr, int M, int N, int K, void* stream) {
+  return guarded([&] {
+    GemmArgs g;
+    g.A = reinterpret_cast<const _Float16*>(A); g.lda = lda;
+    g.W = reinterpret_cast<const _Float16*>(W); g.ldw = ldw;
+    g.bias = bias; g.C = C; g.ldc = ldc; g.R = R; g.ldr = ldr; g.M = M; g.N = N; g.K = K;
+    JANUS_CHECK(gemm_lt_launch(epi, g, (hipStream_t)stream),
+                "gemm_lt: no hipBLASLt plan for this shape / epilogue");
+  });
+}
+
 extern "C" int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const float* gamma,
                                  const float* beta, float eps, const uint16_t* W, int64_t ldw,
                                  const float* bias, void* C, int64_t ldc, int M, int N, int K,

@@ -212,6 +212,13 @@ static void prepare(janus_whisper* w, hipStream_t s) {
   w->prepared = true;
 }
 
+// The encoder's projections (M = B * 1500 rows) go to hipBLASLt where it has a plan
+// (blaslt.cpp; JANUS_ENC_BLASLT=0 keeps them on gemm_nt_kernel).
+static void enc_gemm(int epi, const GemmArgs& g, hipStream_t s) {
+  if (gemm_lt_enabled() && gemm_lt_launch(epi, g, s)) return;
+  gemm_launch(epi, g, s);
+}
+
 static GemmArgs gargs(const _Float16* A, int64_t lda, const _Float16* W, int64_t ldw,
                       const float* bias, void* C, int64_t ldc, int M, int N, int K,
                       const float* R = nullptr, int64_t ldr = 0) {
@@ -259,12 +266,12 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
   for (int l = 0; l < c.enc_layers; ++l) {
     EncLayer& L = w->enc[l];
     layernorm_launch(r, L.ln1g, L.ln1b, a, (int)M, d, 1e-5f, s);
-    gemm_launch(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, (int)M, 3 * d, d), s);
+    enc_gemm(EPI_F16, gargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, (int)M, 3 * d, d), s);
     attention_launch(qkv, o, B, Te, H, scale, s);
-    gemm_launch(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, r, d, (int)M, d, d, r, d), s);
+    enc_gemm(EPI_RESID_F32, gargs(o, d, L.wo.as<_Float16>(), d, L.bo, r, d, (int)M, d, d, r, d), s);
     layernorm_launch(r, L.ln2g, L.ln2b, a, (int)M, d, 1e-5f, s);
-    gemm_launch(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, (int)M, 4 * d, d), s);
-    gemm_launch(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, r, d, (int)M, d, 4 * d, r, d), s);
+    enc_gemm(EPI_GELU_F16, gargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, (int)M, 4 * d, d), s);
+    enc_gemm(EPI_RESID_F32, gargs(f, 4 * d, L.w2.as<_Float16>(), 4 * d, L.b2, r, d, (int)M, d, 4 * d, r, d), s);
   }
   layernorm_launch(r, w->params.get("encoder.layer_norm.weight", d),
                    w->params.get("encoder.layer_norm.bias", d), out, (int)M, d, 1e-5f, s);

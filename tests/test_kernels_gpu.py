@@ -46,6 +46,33 @@ def test_gemm(gpu, M, N, K, epi):
     assert err < (2e-3 if out_dtype == torch.float16 else 1e-4), err
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 1536, 512), (3000, 512, 512), (3000, 2048, 512),
+                                   (3000, 512, 2048), (1500, 384, 1536)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_lt(gpu, M, N, K, epi):
+    """The encoder projections on hipBLASLt (janus_gemm_lt_f16): same contract as the
+    hand-written GEMM, fp64 reference, in-place residual, exact-erf GELU pass."""
+    g = torch.Generator().manual_seed(M + N * 3 + K + epi)
+    A = (torch.randn(M, K, generator=g)).half()
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).half()
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    ref = A.double() @ W.double().T + bias.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = ref + R.double()
+    dA, dW, db = A.to(gpu), W.to(gpu), bias.to(gpu)
+    out_dtype = torch.float16 if epi in (0, 1) else torch.float32
+    C = R.to(gpu).clone() if epi == 2 else torch.empty(M, N, dtype=out_dtype, device=gpu)
+    nat.call("janus_gemm_lt_f16", epi, dA.data_ptr(), K, dW.data_ptr(), K, db.data_ptr(), C.data_ptr(),
+             N, C.data_ptr() if epi == 2 else None, N, M, N, K, stream())
+    torch.cuda.synchronize()
+    err = rel_err(C, ref)
+    # fp16 output: one rounding (two for GELU: the library's fp16 store, then the pass)
+    assert err < (2e-3 if out_dtype == torch.float16 else 1e-4), err
+
+
 def test_layernorm(gpu):
     g = torch.Generator().manual_seed(1)
     for d in (384, 512, 768):
