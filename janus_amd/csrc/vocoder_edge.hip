@@ -106,17 +106,29 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
   float* ws = post_smem + kPostC * kPostRows;   // [kPostC][16] (taps padded to 16)
   const int b = blockIdx.y, t0 = blockIdx.x * kPostT, tid = threadIdx.x;
   const _Float16* xb = x + (int64_t)b * T * kPostC;
+  // stage rows t0-6 .. t0+kPostT+9 (16 channels = two 16-byte halves per row): every load
+  // of the tile in flight before the first convert/store (one memory latency per block;
+  // a load-store loop paid one per iteration: 1.9 ms for the 64 x 30 s pass)
+  constexpr int NPL = (kPostRows * 2 + kPostThreads - 1) / kPostThreads;
+  uint4 pv[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int i = tid + k * kPostThreads;
+    const int t = t0 - kPostK / 2 + (i >> 1);
+    pv[k] = (i < kPostRows * 2 && t >= 0 && t < T)
+                ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * kPostC + (i & 1) * 8)
+                : make_uint4(0, 0, 0, 0);
+  }
   for (int i = tid; i < kPostC * 16; i += kPostThreads) {
     const int c = i >> 4, j = i & 15;
     ws[i] = j < kPostK ? w[c * kPostK + j] : 0.0f;
   }
-  // stage rows t0-6 .. t0+kPostT+9 (16 channels = two 16-byte halves per row)
-  for (int i = tid; i < kPostRows * 2; i += kPostThreads) {
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int i = tid + k * kPostThreads;
+    if (i >= kPostRows * 2) break;
     const int r = i >> 1, half = i & 1;
-    const int t = t0 - kPostK / 2 + r;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (t >= 0 && t < T) v = *reinterpret_cast<const uint4*>(xb + (int64_t)t * kPostC + half * 8);
-    const _Float16* h = reinterpret_cast<const _Float16*>(&v);
+    const _Float16* h = reinterpret_cast<const _Float16*>(&pv[k]);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       xs[(half * 8 + j) * kPostRows + r] = pre_silu ? silu((float)h[j]) : (float)h[j];

@@ -67,6 +67,7 @@ struct DecLane {
       d_xc, d_xpc, d_xpml, d_enc;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t stream = nullptr;  // graph capture needs a non-null stream
+  std::vector<uint32_t> stream_mask;  // CU mask the lane stream was created with (empty: none)
   hipEvent_t ev_done = nullptr;
   DecLane() = default;
   DecLane(const DecLane&) = delete;
@@ -333,7 +334,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const int cus = opt->cu_count > 0 ? opt->cu_count : stream_cu_count(s);
   const int lg_cap = std::getenv("JANUS_LOGITS_BLOCKS") ? std::atoi(std::getenv("JANUS_LOGITS_BLOCKS"))
                                                         : cus;
-  const int msplit_n = cus <= 128 ? 1024 : 0;
+  const int msplit_n = std::getenv("JANUS_DEC_MSPLIT_N") ? std::atoi(std::getenv("JANUS_DEC_MSPLIT_N"))
+                                                         : (cus <= 128 ? 1024 : 0);
   auto dgargs = [&](auto&&... args) {
     GemmArgs g = gargs(args...);
     g.msplit_n = msplit_n;
@@ -699,11 +701,32 @@ extern "C" int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* 
     JANUS_HIP(hipStreamGetPriority(s, &prio));
     if (!w->ev_in) JANUS_HIP(hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming));
     JANUS_HIP(hipEventRecord(w->ev_in, s));
+    // a caller on a CU-masked stream (the overlapped step's decoder partition) gets lanes
+    // on the same CUs
+    std::vector<uint32_t> mask(16, 0xffffffffu);
+    bool masked = false;
+    if (s && hipExtStreamGetCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+      int ncu = 0;
+      JANUS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+      for (int c = 0; c < ncu && c < 32 * (int)mask.size(); ++c)
+        if (!((mask[c / 32] >> (c % 32)) & 1u)) masked = true;
+    }
     for (int i = 0; i < nlanes; ++i) {
       DecLane& Z = *w->lanes[i];
+      if (Z.stream && Z.stream_mask != (masked ? mask : std::vector<uint32_t>())) {
+        JANUS_HIP(hipStreamSynchronize(Z.stream));
+        JANUS_HIP(hipStreamDestroy(Z.stream));
+        Z.stream = nullptr;
+        for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
+        Z.graphs.clear();
+      }
       if (!Z.stream) {
-        JANUS_HIP(hipStreamCreateWithPriority(&Z.stream, hipStreamNonBlocking, prio));
-        JANUS_HIP(hipEventCreateWithFlags(&Z.ev_done, hipEventDisableTiming));
+        if (masked)
+          JANUS_HIP(hipExtStreamCreateWithCUMask(&Z.stream, (uint32_t)mask.size(), mask.data()));
+        else
+          JANUS_HIP(hipStreamCreateWithPriority(&Z.stream, hipStreamNonBlocking, prio));
+        Z.stream_mask = masked ? mask : std::vector<uint32_t>();
+        if (!Z.ev_done) JANUS_HIP(hipEventCreateWithFlags(&Z.ev_done, hipEventDisableTiming));
       }
       JANUS_HIP(hipStreamWaitEvent(Z.stream, w->ev_in, 0));
     }
