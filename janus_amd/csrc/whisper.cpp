@@ -428,21 +428,29 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // Measured slower than the separate launches (616.8 vs 536.5 ms per bench step): the
   // write-through stores and the serial tail cost more than the launch they save.
   const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && std::getenv("JANUS_LN_FUSE") != nullptr;
-  // JANUS_LN_PROLOGUE (opt-in, B <= 64): every pre-LN projection computes LayerNorm(x)
-  // for its rows in the block prologue (GemmArgs::lnin_x), the vocabulary projection the
-  // final LayerNorm — no LayerNorm launches. Measured level with the separate launches
-  // (432.7 / 434.7 vs 435.9 / 434.6 ms per bench step, unconditional 16-byte prologue
-  // loads): the prologue's round trip and row reductions cost what the launch saves.
-  const bool ln_pro = B <= 64 && d <= 512 && !fused_ln && !ln_fuse && std::getenv("JANUS_LN_PROLOGUE") != nullptr;
+  // LayerNorm in the consuming projection's prologue (GemmArgs::lnin_x: each block
+  // normalises its rows of x into an fp16 LDS tile; the vocabulary projection the final
+  // LayerNorm) instead of a LayerNorm launch.
+  // Per LayerNorm (bit mask, JANUS_LN_PROLOGUE overrides): 1 = LN1 into the QKV
+  // projection, 2 = LN2 into the absorbed query projection, 4 = LN3 into fc1, 8 = the final
+  // LayerNorm into the vocabulary projection. Measured per kernel, decoder alone on 16 CUs
+  // per XCD: QKV 9.2 us vs 5.6 + 5.1 (LayerNorm launch), fc1 8.6 vs 5.2 + 5.1, logits 49.4
+  // vs 47.3 + 5.1 — but the absorbed query projection 16.1 vs 9.2 + 5.1 us: its 256
+  // 64-row blocks would each normalise all 64 rows. Beside the vocoder (overlapped
+  // step, decoder side): mask 0 303.5-308.7, 13 305.1-306.8, 9 304.0-304.2, 5 306.6-306.9
+  // ms — within the box's noise; 9 (LN1 + final) is the default.
+  const int ln_pro_mask = (B <= 64 && d <= 512 && !fused_ln && !ln_fuse)
+                              ? (std::getenv("JANUS_LN_PROLOGUE") ? std::atoi(std::getenv("JANUS_LN_PROLOGUE")) : 9)
+                              : 0;
   // the embedding kernel owns whole rows (one block per utterance): it also writes the
   // first layer's LayerNorm of its row, one launch fewer per position
   // (JANUS_NO_EMBED_LN restores the separate launch)
-  const bool embed_ln = !fused_ln && !ln_fuse && !ln_pro && d <= 512 &&
-                        std::getenv("JANUS_NO_EMBED_LN") == nullptr;
-  auto with_ln = [&](GemmArgs g, const float* lg, const float* lb) {
-    if (ln_pro) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
+  const bool embed_ln = !fused_ln && !ln_fuse && d <= 512 && std::getenv("JANUS_NO_EMBED_LN") == nullptr;
+  auto with_ln = [&](GemmArgs g, const float* lg, const float* lb, bool on) {
+    if (on) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
     return g;
   };
+  const bool lnp2 = ln_pro_mask & 2, lnp3 = ln_pro_mask & 4, lnp_fin = ln_pro_mask & 8;
   Z.d_lncnt.ensure(sizeof(int));
   JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int), s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
@@ -468,11 +476,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
-        if (!ln_fuse && !ln_pro && !(embed_ln && l == 0))
+        // layer 0's LN1 comes from the embedding kernel when embed_ln
+        const bool lnp1 = (ln_pro_mask & 1) && !(embed_ln && l == 0);
+        if (!ln_fuse && !lnp1 && !(embed_ln && l == 0))
           layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
         if (B <= 64) {
           GemmArgs g = with_ln(dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
-                               L.ln1g, L.ln1b);
+                               L.ln1g, L.ln1b, lnp1);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
           gemm_launch(EPI_QKV, g, s);
         } else {
@@ -491,9 +501,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse && !lnp2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
-                                       L.ln2g, L.ln2b), s);
+                                       L.ln2g, L.ln2b, lnp2), s);
         }
         xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s);
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
@@ -506,9 +516,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
                                                 nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse && !lnp2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d),
-                                       L.ln2g, L.ln2b), s);
+                                       L.ln2g, L.ln2b, lnp2), s);
         }
         decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                       part_ml, s);
@@ -518,19 +528,19 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
-        if (!ln_fuse && !ln_pro) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+        if (!ln_fuse && !lnp3) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
         gemm_launch(EPI_GELU_F16, with_ln(dgargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d),
-                                          L.ln3g, L.ln3b), s);
+                                          L.ln3g, L.ln3b, lnp3), s);
       }
       // next LayerNorm: the following layer's LN1, or the decoder's final LN
       resid(f, 4 * d, L.w2, L.b2, l + 1 < nl ? w->dec[l + 1].ln1g : fin_g,
             l + 1 < nl ? w->dec[l + 1].ln1b : fin_b);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
-    if (!ln_fuse && !ln_pro) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
+    if (!ln_fuse && !lnp_fin) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
-                          ln_pro ? x : nullptr, d, fin_g, fin_b, lg_cap);
+                          lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap);
     select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                            maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
                            Z.d_nsp.as<float>());
@@ -542,7 +552,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro, (int64_t)embed_ln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};
