@@ -226,6 +226,12 @@ class WhisperEngine:
             a = np.ascontiguousarray(arr, dtype=np.float32)
             nat.call("janus_whisper_set_tensor", self._h, name.encode(), a.ctypes.data, a.size)
 
+    def set_tensor(self, name: str, arr) -> None:
+        """Re-upload one parameter (janus_whisper_set_tensor); the next call re-prepares
+        the derived fp16 weights and re-captures the decode graphs."""
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        nat.call("janus_whisper_set_tensor", self._h, name.encode(), a.ctypes.data, a.size)
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from janus_amd.whisper import CONFIGS, WhisperEngine, mel_filters, synthetic_weights
+from janus_amd.whisper import engine_weights, CONFIGS, WhisperEngine, mel_filters, synthetic_weights
 from janus_amd.workload import synth_speech
 from oracle import packet as opk
 from oracle import whisper as ow
@@ -140,6 +140,27 @@ def test_free_running_end_to_end_tiny(engine, gpu):
     seq, pk = _check_free_running(tokens.cpu().numpy(), ref, tk, len(tk.sot_sequence), ntok.cpu().numpy())
     print(f"tiny.en end to end: sequences identical {seq:.3f}, packets identical {pk:.3f}")
     assert seq >= 0.75 and pk >= 0.75
+
+
+def test_weight_reupload_after_decode(gpu):
+    """A parameter re-uploaded after a decode (janus_whisper_set_tensor) is what the next
+    decode uses: no captured graph may keep pointing at the freed weight memory. The
+    re-uploaded context must decode exactly as a fresh one built with the new weights."""
+    W = synthetic_weights(CFG, seed=11)
+    eng = WhisperEngine(CFG, W)
+    g = torch.Generator().manual_seed(3)
+    enc = (torch.randn(3, CFG.n_audio_ctx, CFG.d_model, generator=g) * 0.5).half().to(gpu)
+    t1, n1, _ = eng.decode(enc, max_length=40)
+    name = "decoder.layers.0.fc1.weight"
+    W2 = dict(W)
+    W2[name] = engine_weights({name: -1.5 * W[name]})[name]
+    eng.set_tensor(name, W2[name])
+    t2, n2, _ = eng.decode(enc, max_length=40)
+    fresh = WhisperEngine(CFG, W2)
+    t3, n3, _ = fresh.decode(enc, max_length=40)
+    torch.cuda.synchronize()
+    assert torch.equal(n2, n3) and all(torch.equal(t2[b, :n2[b]], t3[b, :n3[b]]) for b in range(3))
+    assert not (torch.equal(n1, n2) and all(torch.equal(t1[b, :n1[b]], t2[b, :n2[b]]) for b in range(3)))
 
 
 def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
