@@ -45,9 +45,9 @@ void resunit_pack(const float* w, _Float16* out, int C, int k, hipStream_t s) {
 // c1 covers M1 = BM + 16 rows (>= BM + K - 1, c2's halo); a 16x16x32 MFMA k-step spans
 // TPK = 32 / C taps, so K rounds up to TP taps with zero weights on the padding tap;
 // every row a padding tap touches is staged (and finite), so the MFMA loop has no guards.
-template <int C, int K, int D, int BM>
+template <int C, int K, int D, int BM, int NW = 4>
 struct NarrowGeo {
-  static constexpr int NT = 256;
+  static constexpr int NT = 64 * NW;                    // NW waves per block
   static constexpr int TPK = 32 / C;                    // taps per k-step
   static constexpr int KS = (K + TPK - 1) / TPK;        // k-steps per conv
   static constexpr int KP = KS * 32;                    // packed K (resunit_kp)
@@ -58,7 +58,7 @@ struct NarrowGeo {
   static constexpr int CPR = C / 8;                     // 16-byte chunks per row
   static constexpr int MT1 = BM / 16 + 1, M1 = MT1 * 16;
   static constexpr int MT2 = BM / 16;
-  static constexpr int MW1 = (MT1 + 3) / 4, MW2 = (MT2 + 3) / 4;
+  static constexpr int MW1 = (MT1 + NW - 1) / NW, MW2 = (MT2 + NW - 1) / NW;
   static constexpr int NTL = C / 16;                    // n-tiles (all per wave)
   static constexpr int R0 = M1 + (TP - 1) * D;          // staged x rows
   static constexpr int NPF = (R0 * CPR + NT - 1) / NT;  // prefetch uint4 per thread
@@ -67,7 +67,7 @@ struct NarrowGeo {
   // epilogue passes: at C = 32 the fp32 tile goes out in two row halves so that the
   // block fits in 80 KB of LDS (two blocks per CU)
   static constexpr int NP = C == 32 ? 2 : 1;
-  static constexpr int RP = 64 * (MW2 / NP);            // rows per epilogue pass
+  static constexpr int RP = 16 * NW * (MW2 / NP);       // rows per epilogue pass
   // the residual x rows: kept from the staging in an LDS tile where LDS allows (C = 16),
   // else re-read from global memory (L2-hot) into registers during the convs
   static constexpr bool RES_LDS = C == 16;
@@ -85,9 +85,10 @@ struct NarrowGeo {
 // Persistent: weights staged once; per tile the next tile's x rows are loaded into
 // registers while this tile computes. Edge tiles (the first and last of an utterance)
 // take the guarded epilogue path; interior tiles run unguarded.
-template <int C, int K, int D, int BM>
-__global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_per_utt, int n_tiles) {
-  using G = NarrowGeo<C, K, D, BM>;
+template <int C, int K, int D, int BM, int NW>
+__global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int tiles_per_utt, int n_tiles) {
+  using G = NarrowGeo<C, K, D, BM, NW>;
+  constexpr int NT = G::NT;
   constexpr int LI = G::LI, LW = G::LW, CPR = G::CPR, ES = G::ES, NTL = G::NTL;
   constexpr int MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2, M1 = G::M1;
   constexpr int P1 = G::P1, P2 = G::P2, R0 = G::R0, KS = G::KS, KP = G::KP;
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
   const int T = a.T;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
 
-  for (int idx = tid; idx < C * (KP / 8); idx += 256) {
+  for (int idx = tid; idx < C * (KP / 8); idx += NT) {
     const int co = idx / (KP / 8), cc = idx % (KP / 8);
     *reinterpret_cast<uint4*>(sW1 + co * LW + cc * 8) =
         *reinterpret_cast<const uint4*>(a.w1 + (int64_t)co * KP + cc * 8);
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
     const int b_ = tl_ / tiles_per_utt, t0_ = (tl_ % tiles_per_utt) * BM;                   \
     const _Float16* xb_ = a.x + (int64_t)b_ * T * C;                                        \
     _Pragma("unroll") for (int i = 0; i < G::NPF; ++i) {                                    \
-      const int idx = tid + i * 256;                                                        \
+      const int idx = tid + i * NT;                                                         \
       const int r = idx / CPR, cc = idx % CPR;                                              \
       const int t = t0_ - P2 - P1 + r;                                                      \
       pf[i] = (L_ < n_tiles && r < R0  && t >= 0 && t < T)                                 \
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
     __syncthreads();  // previous tile's epilogue is done with sE / sR
 #pragma unroll
     for (int i = 0; i < G::NPF; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
     uint4 xres[G::NE], acc_in[G::NE];
 #pragma unroll
     for (int i = 0; i < G::NE; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const bool ok = r < BM && t0 + r < T;
       if constexpr (!G::RES_LDS)
@@ -199,29 +200,38 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       for (int j = 0; j < MW1; ++j)
 #pragma unroll
         for (int n = 0; n < NTL; ++n) acc[j][n] = zero_f32x4();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        half8 bw[NTL];
+      // fragments double-buffered across k-steps: step ks+1's LDS reads are issued before
+      // step ks's MFMAs. (Left to the compiler, each A read was followed by an
+      // lgkmcnt(0) wait and two MFMAs: the LDS latency, not the MFMA, paced the loop —
+      // 26 % matrix-core busy on C = 32, k = 11.)
+      half8 bw[2][NTL], av[2][MW1];
+      auto ld1 = [&](int ks, int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int n = 0; n < NTL; ++n)
-          bw[n] = *reinterpret_cast<const half8*>(sW1 + b_off + n * 16 * LW + ks * 32);
+          bw[buf][n] = *reinterpret_cast<const half8*>(sW1 + b_off + n * 16 * LW + ks * 32);
 #pragma unroll
         for (int j = 0; j < MW1; ++j) {
           // a wave past the last m-tile recomputes it (result dropped in the epilogue):
           // no branch around the MFMA — branches there made the compiler shuttle
           // accumulators between AGPRs and overwrite a pending MFMA's srcC (gfx950)
-          const int m = min(w + 4 * j, MT1 - 1);
-          const half8 av = *reinterpret_cast<const half8*>(
-              sX + a1_off + (m * 16 + ks * G::TPK * D) * LI);
-#pragma unroll
-          for (int n = 0; n < NTL; ++n) acc[j][n] = mfma16(av, bw[n], acc[j][n]);
+          const int m = min(w + NW * j, MT1 - 1);
+          av[buf][j] = *reinterpret_cast<const half8*>(sX + a1_off + (m * 16 + ks * G::TPK * D) * LI);
         }
+      };
+      ld1(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) ld1(ks + 1, (ks + 1) & 1);
+#pragma unroll
+        for (int j = 0; j < MW1; ++j)
+#pragma unroll
+          for (int n = 0; n < NTL; ++n) acc[j][n] = mfma16(av[ks & 1][j], bw[ks & 1][n], acc[j][n]);
       }
       __syncthreads();  // every wave is done reading sX
 #pragma unroll
       for (int j = 0; j < MW1; ++j) {
-        const int m = w + 4 * j;
-        if (j >= MT1 / 4 && m >= MT1) continue;
+        const int m = w + NW * j;
+        if (j >= MT1 / NW && m >= MT1) continue;
 #pragma unroll
         for (int n = 0; n < NTL; ++n) {
           const int co = n * 16 + arow;
@@ -246,18 +256,26 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
     for (int j = 0; j < MW2; ++j)
 #pragma unroll
       for (int n = 0; n < NTL; ++n) acc2[j][n] = zero_f32x4();
+    {
+      half8 bw[2][NTL], av[2][MW2];  // double-buffered as in c1
+      auto ld2 = [&](int ks, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      half8 bw[NTL];
+        for (int n = 0; n < NTL; ++n)
+          bw[buf][n] = *reinterpret_cast<const half8*>(sW2 + b_off + n * 16 * LW + ks * 32);
 #pragma unroll
-      for (int n = 0; n < NTL; ++n)
-        bw[n] = *reinterpret_cast<const half8*>(sW2 + b_off + n * 16 * LW + ks * 32);
+        for (int j = 0; j < MW2; ++j) {
+          const int m = min(w + NW * j, MT2 - 1);  // see c1
+          av[buf][j] = *reinterpret_cast<const half8*>(sS + a2_off + (m * 16 + ks * G::TPK) * LI);
+        }
+      };
+      ld2(0, 0);
 #pragma unroll
-      for (int j = 0; j < MW2; ++j) {
-        const int m = min(w + 4 * j, MT2 - 1);  // see c1
-        const half8 av = *reinterpret_cast<const half8*>(sS + a2_off + (m * 16 + ks * G::TPK) * LI);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) ld2(ks + 1, (ks + 1) & 1);
 #pragma unroll
-        for (int n = 0; n < NTL; ++n) acc2[j][n] = mfma16(av, bw[n], acc2[j][n]);
+        for (int j = 0; j < MW2; ++j)
+#pragma unroll
+          for (int n = 0; n < NTL; ++n) acc2[j][n] = mfma16(av[ks & 1][j], bw[ks & 1][n], acc2[j][n]);
       }
     }
     // ---- epilogue in NP row passes: c2 + b2 -> fp32 LDS (over dead sS), then 16-byte
@@ -267,8 +285,8 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       __syncthreads();  // sS reads (p = 0) / the previous pass's sE reads are done
 #pragma unroll
       for (int j = p * (MW2 / G::NP); j < (p + 1) * (MW2 / G::NP); ++j) {
-        const int m = w + 4 * j;
-        if (j >= MT2 / 4 && m >= MT2) continue;
+        const int m = w + NW * j;
+        if (j >= MT2 / NW && m >= MT2) continue;
 #pragma unroll
         for (int n = 0; n < NTL; ++n)
 #pragma unroll
@@ -278,7 +296,7 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
       __syncthreads();
 #pragma unroll
       for (int i = p * (G::NE / G::NP); i < (p + 1) * (G::NE / G::NP); ++i) {
-        const int idx = tid + i * 256;
+        const int idx = tid + i * NT;
         const int r = idx / CPR, cg = (idx % CPR) * 8;
         if (r >= BM || t0 + r >= T) continue;
         const int rl = r - p * G::RP;
@@ -302,11 +320,11 @@ __global__ __launch_bounds__(256) void resunit_kernel(ResUnitArgs a, int tiles_p
 #undef NARROW_PREFETCH
 }
 
-template <int C, int K, int D, int BM>
+template <int C, int K, int D, int BM, int NW>
 static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
-  using G = NarrowGeo<C, K, D, BM>;
+  using G = NarrowGeo<C, K, D, BM, NW>;
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_kernel<C, K, D, BM>;
+  auto kern = resunit_kernel<C, K, D, BM, NW>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -323,17 +341,29 @@ static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
   // one block per tile -> 327.7 ms. JANUS_NARROW_GRID_CUS overrides the 1024.
   static const int gcu = std::getenv("JANUS_NARROW_GRID_CUS") ? std::atoi(std::getenv("JANUS_NARROW_GRID_CUS")) : 1024;
   const int grid = std::min(n_tiles, std::max(1, gcu) * per_cu);
-  kern<<<grid, 256, G::LDS, s>>>(a, tiles_per_utt, n_tiles);
+  kern<<<grid, G::NT, G::LDS, s>>>(a, tiles_per_utt, n_tiles);
   JANUS_LAUNCH_CHECK();
 }
 
+template <int C, int K, int NW>
+static void narrow_dw(const ResUnitArgs& a, hipStream_t s) {
+  constexpr int BM = 240;
+  if (a.d == 1) narrow_cfg<C, K, 1, BM, NW>(a, s);
+  else if (a.d == 3) narrow_cfg<C, K, 3, BM, NW>(a, s);
+  else if (a.d == 5) narrow_cfg<C, K, 5, BM, NW>(a, s);
+  else throw Error("resunit: dilation must be 1, 3 or 5");
+}
+
+// waves per block (JANUS_NARROW_WAVES: 4 or 8). C = 32 runs 8 waves: its blocks (76 KB of
+// LDS, 2 per CU) gave each SIMD only 2 waves to hide the staging, SiLU and epilogue phases
+// behind the other block's MFMAs (overlapped step: C = 32 units 39.7 -> 34.0 ms); C = 16
+// (3 blocks per CU already) is level-to-slower at 8 (29.9 -> 30.4 ms).
 template <int C, int K>
 static void narrow_d(const ResUnitArgs& a, hipStream_t s) {
-  constexpr int BM = 240;
-  if (a.d == 1) narrow_cfg<C, K, 1, BM>(a, s);
-  else if (a.d == 3) narrow_cfg<C, K, 3, BM>(a, s);
-  else if (a.d == 5) narrow_cfg<C, K, 5, BM>(a, s);
-  else throw Error("resunit: dilation must be 1, 3 or 5");
+  static const int nw = std::getenv("JANUS_NARROW_WAVES") ? std::atoi(std::getenv("JANUS_NARROW_WAVES"))
+                                                          : (C == 32 ? 8 : 4);
+  if (nw == 8) narrow_dw<C, K, 8>(a, s);
+  else narrow_dw<C, K, 4>(a, s);
 }
 
 template <int C>
