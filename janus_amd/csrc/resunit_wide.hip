@@ -47,17 +47,22 @@ __global__ void resunit_wide_pack_kernel(const float* __restrict__ w, _Float16* 
   out[idx] = (_Float16)w[((int64_t)co * C + ci) * k + tap];
 }
 
-template <int C> struct WideCfg;
+template <int C, int V = 0> struct WideCfg;
 // BM output rows per block, WM x WN waves (wave tile: every WM-th m-tile x C/WN columns),
 // NPB = weight k-steps in flight per wave (divides the k-step count k*C/32).
 // EPF: residual / accumulator rows loaded before c2 (in flight during it) where the
 // registers allow, else after it.
 // NP: epilogue passes (the fp32 tile in NP row slices so the block fits 3 per CU)
 template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 4, NP = 2; static constexpr bool EPF = false; };
+// 8 waves (2 x 4): half the m-tiles per wave, so fewer registers per wave and two 8-wave
+// blocks per CU (16 waves) instead of three 4-wave blocks (JANUS_WIDE128_WAVES=8).
+// Measured slower (64 x 30 s, whole GPU: C = 128 units 47.5 -> 59.6 ms): each weight
+// fragment is now fetched by two waves; kept as an A/B switch.
+template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN = 4, NPB = 4, NP = 1; static constexpr bool EPF = false; };
 
-template <int C>
+template <int C, int V = 0>
 struct WideGeo {
-  using Cfg = WideCfg<C>;
+  using Cfg = WideCfg<C, V>;
   static constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN, NPB = Cfg::NPB;
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int LI = frag_pitch(C);        // activation row pitch (halves)
@@ -72,7 +77,7 @@ struct WideGeo {
   static constexpr int ES = C + 4;                // fp32 epilogue row pitch
   static constexpr int NE = (BM * CPR + NT - 1) / NT;
   static constexpr int NP = Cfg::NP;
-  static constexpr int RP = 16 * ((MW2 + NP - 1) / NP);  // rows per epilogue pass
+  static constexpr int RP = 16 * WM * ((MW2 + NP - 1) / NP);  // rows per epilogue pass
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
   static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)RP * ES * 4);
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
@@ -139,10 +144,10 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
   }
 }
 
-template <int C>
-__global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnitArgs a,
+template <int C, int V>
+__global__ __launch_bounds__((WideGeo<C, V>::NT), 2) void resunit_wide_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt) {
-  using G = WideGeo<C>;
+  using G = WideGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, NT = G::NT, LI = G::LI;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
   constexpr int NTW = G::NTW, ES = G::ES;
@@ -289,13 +294,13 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 2) void resunit_wide_kernel(ResUnit
   }
 }
 
-template <int C>
+template <int C, int V>
 static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
-  using G = WideGeo<C>;
+  using G = WideGeo<C, V>;
   JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
   JANUS_CHECK((a.k * C / 32) % G::NPB == 0, "resunit (wide): k-step count vs ring depth");
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_wide_kernel<C>;
+  auto kern = resunit_wide_kernel<C, V>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -307,7 +312,7 @@ static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
-template <int C> struct LdsCfg;
+template <int C, int V = 0> struct LdsCfg;
 // ---------------------------------------------------------------------------------
 // Variant with the weights staged through LDS (one copy per block, double-buffered,
 // each k-block's loads issued two k-blocks ahead into registers): measured faster where
@@ -317,10 +322,17 @@ template <int C> struct LdsCfg;
 // BM output rows per block, WM x WN waves, KB = K per weight k-block.
 template <> struct LdsCfg<64> { static constexpr int BM = 176, WM = 4, WN = 1, KB = 32; };
 template <> struct LdsCfg<256> { static constexpr int BM = 112, WM = 2, WN = 4, KB = 32; };
+// twice the waves per block (JANUS_WIDE64_WAVES=8 / JANUS_WIDE256_WAVES=16): fewer m-tiles
+// or n-tiles per wave, fewer registers, more waves per SIMD to hide the block's phases.
+// Measured (64 x 30 s, whole GPU): C = 64 30.4 -> 34.5 ms, C = 256 level (28.4); the
+// narrow units' gain from more waves (resunit.hip) does not carry over to these
+// MFMA-heavier tiles. A/B switches only.
+template <> struct LdsCfg<64, 1> { static constexpr int BM = 176, WM = 4, WN = 2, KB = 32; };
+template <> struct LdsCfg<256, 1> { static constexpr int BM = 112, WM = 4, WN = 4, KB = 32; };
 
-template <int C>
+template <int C, int V = 0>
 struct LdsGeo {
-  using Cfg = LdsCfg<C>;
+  using Cfg = LdsCfg<C, V>;
   static constexpr int BM = Cfg::BM, WM = Cfg::WM, WN = Cfg::WN, KB = Cfg::KB;
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int LI = frag_pitch(C);        // activation row pitch (halves)
@@ -335,24 +347,27 @@ struct LdsGeo {
   static constexpr int NLD = (R0MAX * CPR + NT - 1) / NT;
   static constexpr int ES = C + 4;                // fp32 epilogue row pitch
   static constexpr int NE = (BM * CPR + NT - 1) / NT;
-  static constexpr int WCH = C * KB / 8 / NT;     // weight uint4 per thread per k-block
+  // weight uint4 per thread per k-block (WCH 0: fewer chunks than threads, the first
+  // C*KB/8 threads carry one each)
+  static constexpr int WCH = C * KB / 8 / NT;
+  static constexpr int WACT = C * KB / 8;         // weight chunks per k-block
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
   static constexpr int ACT_H = (ACT + 7) / 8 * 8; // halves
   // the fp32 epilogue tile spans the activation AND weight regions (both dead by then)
   static constexpr size_t LDS = std::max(((size_t)ACT_H + 2 * (size_t)C * LW) * 2,
                                          (size_t)BM * ES * 4);
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0, "tiling");
-  static_assert(C * KB / 8 % NT == 0, "weight k-block split");
+  static_assert(C * KB / 8 % NT == 0 || NT % (C * KB / 8) == 0, "weight k-block split");
   static_assert(KB <= C && C % KB == 0 && KB % 32 == 0, "k-block inside one tap");
   static_assert((C / KB) % 2 == 0, "even k-block count (two register slots)");
 };
 
 // EPF: load the residual / accumulator rows at c2's start (in flight during its MFMAs)
 // instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
-template <int C, bool EPF>
-__global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResUnitArgs a,
+template <int C, bool EPF, int V>
+__global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt) {
-  using G = LdsGeo<C>;
+  using G = LdsGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
   constexpr int NTW = G::NTW, ES = G::ES;
@@ -379,9 +394,11 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
   // weight k-blocks: two register slots, each load issued two k-blocks before its LDS
   // store (an L2 round trip is longer than one k-block of MFMAs at KB = 32). Plain
   // locals + macros: captured by reference in lambdas they were left in scratch memory.
-  static_assert(G::WCH == 1 || G::WCH == 2, "weight slot width");
-  const int wsrc0 = (tid / (KB / 8)) * KB + (tid % (KB / 8)) * 8;
-  const int wdst0 = (tid / (KB / 8)) * LW + (tid % (KB / 8)) * 8;
+  static_assert(G::WCH <= 2, "weight slot width");
+  const int wt = min(tid, G::WACT - 1);  // WCH 0: threads past WACT repeat a chunk, store none
+  const bool wst = G::WCH > 0 || tid < G::WACT;
+  const int wsrc0 = (wt / (KB / 8)) * KB + (wt % (KB / 8)) * 8;
+  const int wdst0 = (wt / (KB / 8)) * LW + (wt % (KB / 8)) * 8;
   const int wsrc1 = ((tid + NT) / (KB / 8)) * KB + ((tid + NT) % (KB / 8)) * 8;
   const int wdst1 = ((tid + NT) / (KB / 8)) * LW + ((tid + NT) % (KB / 8)) * 8;
   uint4 rwA0, rwA1, rwB0, rwB1;
@@ -394,7 +411,7 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
 #define WIDE_WSTORE(R0_, R1_, BUF)                                                      \
   do {                                                                                  \
     _Float16* dst_ = sW + (BUF) * C * LW;                                               \
-    *reinterpret_cast<uint4*>(dst_ + wdst0) = R0_;                                      \
+    if (wst) *reinterpret_cast<uint4*>(dst_ + wdst0) = R0_;                             \
     if constexpr (G::WCH == 2) *reinterpret_cast<uint4*>(dst_ + wdst1) = R1_;            \
   } while (0)
 
@@ -573,12 +590,12 @@ __global__ __launch_bounds__(LdsGeo<C>::NT, 2) void resunit_wide_lds_kernel(ResU
 #undef WIDE_WSTORE
 #undef WIDE_KLOOP
 
-template <int C, bool EPF>
+template <int C, bool EPF, int V>
 static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
-  using G = LdsGeo<C>;
+  using G = LdsGeo<C, V>;
   JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_wide_lds_kernel<C, EPF>;
+  auto kern = resunit_wide_lds_kernel<C, EPF, V>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -604,9 +621,21 @@ void resunit_wide_pack(const float* w, _Float16* out, int C, int k, hipStream_t 
 
 void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
   static const int epf = [] { const char* e = std::getenv("JANUS_WIDE_EPF"); return e ? std::atoi(e) : 1; }();
-  if (a.C == 64) epf ? lds_cfg<64, true>(a, s) : lds_cfg<64, false>(a, s);
-  else if (a.C == 128) wide_cfg<128>(a, s);
-  else if (a.C == 256) epf ? lds_cfg<256, true>(a, s) : lds_cfg<256, false>(a, s);
+  static const int w64 = std::getenv("JANUS_WIDE64_WAVES") ? std::atoi(std::getenv("JANUS_WIDE64_WAVES")) : 4;
+  static const int w256 = std::getenv("JANUS_WIDE256_WAVES") ? std::atoi(std::getenv("JANUS_WIDE256_WAVES")) : 8;
+  if (a.C == 64) {
+    if (w64 == 8) epf ? lds_cfg<64, true, 1>(a, s) : lds_cfg<64, false, 1>(a, s);
+    else epf ? lds_cfg<64, true, 0>(a, s) : lds_cfg<64, false, 0>(a, s);
+  }
+  else if (a.C == 128) {
+    static const int w128 = std::getenv("JANUS_WIDE128_WAVES") ? std::atoi(std::getenv("JANUS_WIDE128_WAVES")) : 4;
+    if (w128 == 8) wide_cfg<128, 1>(a, s);
+    else wide_cfg<128, 0>(a, s);
+  }
+  else if (a.C == 256) {
+    if (w256 == 16) epf ? lds_cfg<256, true, 1>(a, s) : lds_cfg<256, false, 1>(a, s);
+    else epf ? lds_cfg<256, true, 0>(a, s) : lds_cfg<256, false, 0>(a, s);
+  }
   else throw Error("resunit (wide): C must be 64, 128 or 256");
 }
 
