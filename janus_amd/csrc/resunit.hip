@@ -66,7 +66,13 @@ struct NarrowGeo {
   static constexpr int NE = (BM * CPR + NT - 1) / NT;   // epilogue uint4 per thread
   // epilogue passes: at C = 32 the fp32 tile goes out in two row halves so that the
   // block fits in 80 KB of LDS (two blocks per CU)
-  static constexpr int NP = C == 32 ? 2 : 1;
+  // (C = 16 too: the half-size fp32 tile brings its block to 31 KB of LDS, four blocks
+  // per CU instead of three; JANUS_NARROW16_NP=1 builds the single-pass form)
+#ifndef JANUS_NARROW16_NP
+#define JANUS_NARROW16_NP 2
+#endif
+  static constexpr int NP =
+      C == 32 ? 2 : (NE % JANUS_NARROW16_NP == 0 && MW2 % JANUS_NARROW16_NP == 0 ? JANUS_NARROW16_NP : 1);
   static constexpr int RP = 16 * NW * (MW2 / NP);       // rows per epilogue pass
   // the residual x rows: kept from the staging in an LDS tile where LDS allows (C = 16),
   // else re-read from global memory (L2-hot) into registers during the convs
