@@ -446,13 +446,25 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     f32x4 acc[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
+    // A fragments of k-step ks+1 read while k-step ks's MFMAs run (left to the compiler,
+    // every ds_read was followed by an lgkmcnt(0) wait and one MFMA: 64 exposed LDS round
+    // trips per tile)
+    half8 af[2][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[0][m] = *reinterpret_cast<const half8*>(sA + (16 * m + lr) * AP + kc8);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
+      if (ks + 1 < NKS) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const half8 a = *reinterpret_cast<const half8*>(sA + (16 * m + lr) * AP + 32 * ks + kc8);
-        acc[m] = mfma16(a, bw[u][ks], acc[m]);
+        for (int m = 0; m < 4; ++m)
+          af[(ks + 1) & 1][m] = *reinterpret_cast<const half8*>(sA + (16 * m + lr) * AP + 32 * (ks + 1) + kc8);
       }
+      // keep the reads above the MFMAs (the scheduler otherwise sinks each read to just
+      // before its MFMA to save registers, re-serialising the loop)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[m] = mfma16(af[ks & 1][m], bw[u][ks], acc[m]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)

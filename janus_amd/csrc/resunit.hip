@@ -228,10 +228,12 @@ __global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int til
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         if (ks + 1 < KS) ld1(ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);  // reads stay above the MFMAs (see logits)
 #pragma unroll
         for (int j = 0; j < MW1; ++j)
 #pragma unroll
           for (int n = 0; n < NTL; ++n) acc[j][n] = mfma16(av[ks & 1][j], bw[ks & 1][n], acc[j][n]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       __syncthreads();  // every wave is done reading sX
 #pragma unroll
@@ -278,10 +280,12 @@ __global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int til
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         if (ks + 1 < KS) ld2(ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < MW2; ++j)
 #pragma unroll
           for (int n = 0; n < NTL; ++n) acc2[j][n] = mfma16(av[ks & 1][j], bw[ks & 1][n], acc2[j][n]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // ---- epilogue in NP row passes: c2 + b2 -> fp32 LDS (over dead sS), then 16-byte

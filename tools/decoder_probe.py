@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--per-xcd", default="8,12,16,24")
     ap.add_argument("--beside", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--max-length", type=int, default=448)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -51,7 +52,7 @@ def main():
                         pipe.vocoder.forward(lat, want_pcm=True)
                 e[3].record(vs.stream)
                 with torch.cuda.stream(ds.stream):
-                    out = w.decode_ex(enc, max_length=448, xattn_splits=4, cu_count=ds.n_cus)
+                    out = w.decode_ex(enc, max_length=a.max_length, xattn_splits=4, cu_count=ds.n_cus)
                 e[1].record(ds.stream)
                 torch.cuda.synchronize()
                 print(json.dumps({"dec_per_xcd": per, "beside_vocoder": beside, "rep": rep,
