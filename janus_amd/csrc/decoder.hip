@@ -479,36 +479,72 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     float t_all = -INFINITY, t_text = -INFINITY, t_ts = -INFINITY, t_raw = -INFINITY;
     float vals[16];
     unsigned okm = 0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const int t = col0 + c;
-      const float v = patch[row * 17 + c];
-      vals[c] = v;
-      if (t < V) t_raw = fmaxf(t_raw, v);
-      if (t == R.target) t_v = v;
-      const unsigned smw = c < 4 ? smc.x : c < 8 ? smc.y : c < 12 ? smc.z : smc.w;
-      const bool masked = (smw >> (8 * (c & 3))) & 0xffu;
-      const bool ok = row < B && t < V && !masked && allowed_unmasked(t, R, rr, false);
-      okm |= (unsigned)ok << c;
-      if (ok) {
-        t_all = fmaxf(t_all, v);
-        if (R.ts_begin >= 0 && t >= R.ts_begin) t_ts = fmaxf(t_ts, v);
-        else t_text = fmaxf(t_text, v);
-      }
-    }
     float u_all = 0.f, u_ts = 0.f, u_raw = 0.f;
+    auto in_tile = [&](int t) { return t >= col0 && t < col0 + 16; };
+    // Plain tile (wave-uniform): 16 in-vocabulary text or special tokens, none of blank /
+    // eot / no_timestamps, no timestamp: the rules then give one verdict per row for the
+    // whole tile (allowed_unmasked reduces to the row flags below), and when every column
+    // is allowed the filtered softmax sum IS the raw one (same maximum, same terms in the
+    // same order) — half the exponentials. Bit-identical to the general path.
+    const bool plain = col0 + 16 <= V && (R.ts_begin < 0 || col0 + 16 <= R.ts_begin) &&
+                       !in_tile(R.blank) && !in_tile(R.eot) && !in_tile(R.no_timestamps);
+    if (plain) {
+      const bool row_ok = row < B && !(R.ts_begin >= 0 && ((rr.suppress_text && col0 < R.eot) || rr.sample_begin));
 #pragma unroll
-    for (int c = 0; c < 16; ++c) u_raw += (col0 + c < V) ? __expf(vals[c] - t_raw) : 0.f;
+      for (int c = 0; c < 16; ++c) {
+        const float v = patch[row * 17 + c];
+        vals[c] = v;
+        t_raw = fmaxf(t_raw, v);
+        if (col0 + c == R.target) t_v = v;
+        const unsigned smw = c < 4 ? smc.x : c < 8 ? smc.y : c < 12 ? smc.z : smc.w;
+        const bool ok = row_ok && !((smw >> (8 * (c & 3))) & 0xffu);
+        okm |= (unsigned)ok << c;
+        if (ok) t_all = fmaxf(t_all, v);
+      }
+      t_text = t_all;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (!((okm >> c) & 1u)) continue;
-      const int t = col0 + c;
-      const float v = vals[c];
-      u_all += __expf(v - t_all);
-      if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
-      if (R.ts_begin >= 0 && t >= R.ts_begin) {
-        u_ts += __expf(v - t_ts);
-        if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+      for (int c = 0; c < 16; ++c) u_raw += __expf(vals[c] - t_raw);
+      if (okm == 0xffffu) {
+        u_all = u_raw;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if ((okm >> c) & 1u) u_all += __expf(vals[c] - t_all);
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (((okm >> c) & 1u) && better(vals[c], col0 + c, ba_v, ba_i)) { ba_v = vals[c]; ba_i = col0 + c; }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int t = col0 + c;
+        const float v = patch[row * 17 + c];
+        vals[c] = v;
+        if (t < V) t_raw = fmaxf(t_raw, v);
+        if (t == R.target) t_v = v;
+        const unsigned smw = c < 4 ? smc.x : c < 8 ? smc.y : c < 12 ? smc.z : smc.w;
+        const bool masked = (smw >> (8 * (c & 3))) & 0xffu;
+        const bool ok = row < B && t < V && !masked && allowed_unmasked(t, R, rr, false);
+        okm |= (unsigned)ok << c;
+        if (ok) {
+          t_all = fmaxf(t_all, v);
+          if (R.ts_begin >= 0 && t >= R.ts_begin) t_ts = fmaxf(t_ts, v);
+          else t_text = fmaxf(t_text, v);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) u_raw += (col0 + c < V) ? __expf(vals[c] - t_raw) : 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (!((okm >> c) & 1u)) continue;
+        const int t = col0 + c;
+        const float v = vals[c];
+        u_all += __expf(v - t_all);
+        if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
+        if (R.ts_begin >= 0 && t >= R.ts_begin) {
+          u_ts += __expf(v - t_ts);
+          if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+        }
       }
     }
     float mo;
