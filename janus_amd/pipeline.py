@@ -212,11 +212,11 @@ class JanusPipeline:
                                       max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
-        # the YIN of the first B/32 utterances runs on the decoder side, after the decoder,
-        # to even out the two sides (JANUS_YIN_DEC_UTTS; 64 utterances, r02 with the 8-wave
-        # C = 32 units: 8 / 4 / 2 -> 320.3-322.0 / 320.8 / 317.6-318.7 ms per step; r01:
-        # 0 / 4 / 8 / 11 -> 328.9 / 327.8 / 326.7 / 327.9 ms)
-        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(max(1, B // 32)))))
+        # the YIN of the first B/8 utterances runs on the decoder side, after the decoder,
+        # to even out the two sides (JANUS_YIN_DEC_UTTS; 64 utterances, r02 after the
+        # faster vocabulary projection: 2 / 6 / 8 / 10 -> 316.7-317.1 / 314.5-315.2 /
+        # 313.6-314.3 / 315.2-315.7 ms per step)
+        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(max(1, B // 8)))))
                  if yin_side == "voc" else 0)
         ys = self._yin_s.stream if yin_side == "beside" else None
         pres = None
