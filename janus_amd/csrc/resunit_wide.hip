@@ -55,9 +55,11 @@ template <int C, int V = 0> struct WideCfg;
 // NP: epilogue passes (the fp32 tile in NP row slices so the block fits 3 per CU)
 template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 4, NP = 2; static constexpr bool EPF = false; };
 // 8 waves (2 x 4): half the m-tiles per wave, so fewer registers per wave and two 8-wave
-// blocks per CU (16 waves) instead of three 4-wave blocks (JANUS_WIDE128_WAVES=8).
+// blocks per CU (16 waves) instead of three 4-wave blocks (JANUS_WIDE128_CFG=1).
 // Measured slower (64 x 30 s, whole GPU: C = 128 units 47.5 -> 59.6 ms): each weight
 // fragment is now fetched by two waves; kept as an A/B switch.
+// ring depth 2 (the default, JANUS_WIDE128_CFG=2): 16 fewer VGPRs, three blocks per CU
+template <> struct WideCfg<128, 2> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 2, NP = 2; static constexpr bool EPF = false; };
 template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN = 4, NPB = 4, NP = 1; static constexpr bool EPF = false; };
 
 template <int C, int V = 0>
@@ -132,14 +134,21 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
 #pragma unroll
       for (int j = 0; j < MW; ++j)
         av[(s + 1) & 1][j] = *reinterpret_cast<const half8*>(ap + own_tile<MT, WM>(j, wm) * WM * 16 * LI);
+      // sched barriers pin the issue order: next A reads, this step's MFMAs, then the
+      // ring refill. Without them the scheduler sank every weight load to just before its
+      // use (s_waitcnt vmcnt(0) ahead of the MFMA: one exposed L2 round trip per k-step)
+      // and the A reads likewise.
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < MW; ++j)
 #pragma unroll
         for (int n = 0; n < NTW; ++n) acc[j][n] = mfma16(av[s & 1][j], bq[s][n], acc[j][n]);
+      __builtin_amdgcn_sched_barrier(0);
       const int nx = min(ks + NPB, nks - 1);
 #pragma unroll
       for (int n = 0; n < NTW; ++n)
         bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)nx * C + n * 16) * 32);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -628,9 +637,13 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
     else epf ? lds_cfg<64, true, 0>(a, s) : lds_cfg<64, false, 0>(a, s);
   }
   else if (a.C == 128) {
-    static const int w128 = std::getenv("JANUS_WIDE128_WAVES") ? std::atoi(std::getenv("JANUS_WIDE128_WAVES")) : 4;
-    if (w128 == 8) wide_cfg<128, 1>(a, s);
-    else wide_cfg<128, 0>(a, s);
+    // JANUS_WIDE128_CFG: 2 (default) = 4 waves, weight ring 2 deep (166 VGPRs, three blocks
+    // per CU); 0 = ring 4 deep (178 VGPRs, two blocks); 1 = 8 waves. Standalone 64 x 30 s,
+    // C = 128 units: 45.4 / 49.0 / 59.6 ms (46.5 before the issue order was pinned)
+    static const int c128 = std::getenv("JANUS_WIDE128_CFG") ? std::atoi(std::getenv("JANUS_WIDE128_CFG")) : 2;
+    if (c128 == 1) wide_cfg<128, 1>(a, s);
+    else if (c128 == 0) wide_cfg<128, 0>(a, s);
+    else wide_cfg<128, 2>(a, s);
   }
   else if (a.C == 256) {
     if (w256 == 16) epf ? lds_cfg<256, true, 1>(a, s) : lds_cfg<256, false, 1>(a, s);
