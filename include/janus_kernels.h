@@ -49,6 +49,17 @@ int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const float* gamma, 
 int janus_layernorm_f16(const float* x, const float* gamma, const float* beta, uint16_t* out,
                         int rows, int d, float eps, void* stream);
 
+/* x[M][N] += A[M][K] W[N][K]^T + bias (fp32 residual, in place), then out[M][N] =
+ * LayerNorm(x) fp16 (gamma/beta f32 [N], eps) in ONE launch: 16 rows per workgroup over
+ * all N columns. N = K in {384, 512} (tiny.en / base.en d_model). Bit-identical to
+ * janus_gemm_f16(JANUS_EPI_RESID_F32) at M <= 64 followed by janus_layernorm_f16. The
+ * decoder's attention output projections and the LayerNorm after them
+ * (transcriber.py:53-57 -> Whisper decoder layers: self_attn.out_proj + encoder_attn_layer_norm,
+ * encoder_attn.out_proj + final_layer_norm). */
+int janus_resid_ln_f16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                       const float* bias, float* x, const float* gamma, const float* beta,
+                       float eps, uint16_t* out, int M, int N, int K, void* stream);
+
 /* Non-causal multi-head attention, head_dim 64: qkv fp16 [B*T][3*H*64] -> out fp16 [B*T][H*64]. */
 int janus_attention_f16(const uint16_t* qkv, uint16_t* out, int batch, int T, int H, float scale,
                         void* stream);

@@ -87,6 +87,7 @@ SIGNATURES = {
     "janus_gemm_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
     "janus_gemm_lt_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
     "janus_layernorm_f16": [_P, _P, _P, _P, _I32, _I32, _F32, _P],
+    "janus_resid_ln_f16": [_P, _I64, _P, _I64, _P, _P, _P, _P, _F32, _P, _I32, _I32, _I32, _P],
     "janus_gemm_ln_f16": [_I32, _P, _I64, _P, _P, _F32, _P, _I64, _P, _P, _I64, _I32, _I32, _I32, _P],
     "janus_attention_f16": [_P, _P, _I32, _I32, _I32, _F32, _P],
     "janus_conv1d_packed_size": [_I32, _I32, _I32, _I32, _I32],

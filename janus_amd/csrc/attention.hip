@@ -589,6 +589,9 @@ constexpr int kHeadWaves = 8;
 constexpr int kHeadRounds = 8;                               // key groups per wave
 constexpr int kHeadKeys = 8 * kHeadWaves * kHeadRounds;      // 512
 
+// NR: key rounds actually holding keys (ceil(Tkv / 64)): the rounds past the cache end
+// only loaded the clamped last row and added p = 0 — dropping them changes no bit.
+template <int NR>
 __global__ __launch_bounds__(512) void decode_head_kernel(
     const _Float16* __restrict__ q, int64_t q_bs, const _Float16* __restrict__ k,
     const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv, float scale_log2,
@@ -610,9 +613,9 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
   // key of round i: 8 (i * kHeadWaves + w) + kg; rows past the cache clamp to its last
   // row (finite values, weight 0) so every load is unconditional
   const int tl = Tkv - 1;
-  uint4 kr[kHeadRounds], vr[kHeadRounds];
+  uint4 kr[NR], vr[NR];
 #pragma unroll
-  for (int i = 0; i < kHeadRounds; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
 #ifdef JANUS_KV_NT
     kr[i] = ld_nt(kb + (int64_t)t * kv_rs);
@@ -621,7 +624,7 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
 #endif
   }
 #pragma unroll
-  for (int i = 0; i < kHeadRounds; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
 #ifdef JANUS_KV_NT
     vr[i] = ld_nt(vb + (int64_t)t * kv_rs);
@@ -629,10 +632,10 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
     vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs);
 #endif
   }
-  float sc[kHeadRounds];
+  float sc[NR];
   float m = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < kHeadRounds; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const _Float16* h8 = reinterpret_cast<const _Float16*>(&kr[i]);
     float dot = 0.f;
 #pragma unroll
@@ -652,7 +655,7 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
   for (int j = 0; j < 8; ++j) a[j] = 0.f;
   if (m != -INFINITY) {  // wave-uniform: this wave holds at least one key
 #pragma unroll
-    for (int i = 0; i < kHeadRounds; ++i) {
+    for (int i = 0; i < NR; ++i) {
       const float p = exp2f(sc[i] - m);  // -inf -> 0
       l += p;
       const _Float16* h8 = reinterpret_cast<const _Float16*>(&vr[i]);
@@ -701,8 +704,20 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
   if (B <= 0 || Tkv <= 0) return;
   static const bool force_split = std::getenv("JANUS_DEC_SPLIT") != nullptr;
   if (Tkv <= kHeadKeys && (!force_split || part_o == nullptr)) {
-    decode_head_kernel<<<dim3(H, B), 64 * kHeadWaves, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv,
-                                                              scale * 1.4426950408889634f, out, o_bs);
+    static const bool all_rounds = std::getenv("JANUS_HEAD_ALL_ROUNDS") != nullptr;
+    const int nr = all_rounds ? kHeadRounds : (Tkv + 8 * kHeadWaves - 1) / (8 * kHeadWaves);
+    const float sl = scale * 1.4426950408889634f;
+    const dim3 grid(H, B), blk(64 * kHeadWaves);
+    switch (nr) {
+      case 1: decode_head_kernel<1><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 2: decode_head_kernel<2><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 3: decode_head_kernel<3><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 4: decode_head_kernel<4><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 5: decode_head_kernel<5><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 6: decode_head_kernel<6><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 7: decode_head_kernel<7><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      default: decode_head_kernel<kHeadRounds><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+    }
     JANUS_LAUNCH_CHECK();
     return;
   }

@@ -214,12 +214,15 @@ constexpr int kSkWaves = 16;
 
 // MTB: 16-row m-tiles per block (4: all 64 rows; 1: rows split over gridDim.y, for narrow
 // outputs whose N / 16 column tiles alone would leave most CUs idle).
-template <int EPI, int AM, int MTB>
+// K1: K <= 16 waves x 32, one k-step per wave: G = 1 keeps the all-rows form (MTB = 4)
+// under 64 VGPRs, two 16-wave blocks per CU (the 4096-wide absorbed query projection's 256
+// blocks in one round on a 128-CU partition instead of two: 91 VGPRs admitted one).
+template <int EPI, int AM, int MTB, bool K1 = false>
 __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   constexpr bool LNA = AM == AM_LNA, LNX = AM == AM_LNX;
   // k-steps in flight per wave (128-VGPR budget at 1024 threads; the LayerNorm modes run
   // K <= 512, one k-step per wave)
-  constexpr int G = (LNA || LNX) ? 1 : 2;
+  constexpr int G = (LNA || LNX || K1) ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) _Float16 sk_smem[];  // LNX: [16*MTB][AP]
   __shared__ float red[8][16 * MTB][17];
   __shared__ float s_mean[64], s_rstd[64];
@@ -442,6 +445,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
 template <int AM, int EPI, int MTB>
 static void skinny_go(const SkinnyArgs& p, dim3 grid, hipStream_t s) {
   auto kern = gemm_skinny_kernel<EPI, AM, MTB>;
+  if constexpr (AM == AM_F16 && MTB == 4) {
+    if (p.K <= kSkWaves * 32 && std::getenv("JANUS_SKINNY_NO_K1") == nullptr)
+      kern = gemm_skinny_kernel<EPI, AM, MTB, true>;
+  }
   size_t lds = 0;
   if constexpr (AM == AM_LNX) {
     lds = (size_t)16 * MTB * frag_pitch(p.K) * 2;
@@ -551,6 +558,171 @@ void gelu_inplace_f16_launch(_Float16* x, int64_t ld, int M, int N, hipStream_t 
   const int64_t n = (int64_t)M * (N / 8);
   if (n == 0) return;
   gelu_inplace_f16_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(x, ld, M, N / 8);
+  JANUS_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------ residual projection + LayerNorm
+// x[r] += A[r] W^T + bias (fp32 residual, in place) and out[r] = LayerNorm(x[r]) (fp16),
+// 16 rows per block over ALL N = 32 * NW columns, so the block owns whole rows and the
+// LayerNorm needs no second launch and no cross-block hand-off (decoder: the self- and
+// cross-attention output projections, each followed by LN2 / LN3; d = 512: 16 waves).
+// Wave w owns columns [32w, 32w + 32) over the full K; the block streams all of W
+// (0.5 MB at d = 512) through one CU, which a separate LayerNorm launch (≈ 5 µs) more
+// than pays for.
+// Bit-identical to gemm_skinny_kernel<EPI_RESID_F32> (+ layernorm_kernel): that kernel
+// gives each of its 16 waves one 32-deep k-step, p_i = mfma(a_i, b_i, 0), and sums
+// v = (bias + R) + (p_0 + p_8) + (p_1 + p_9) + ... + (p_7 + p_15); here a wave walks its
+// k-steps in the order 0, 8, 1, 9, ... and adds the pairs in the same order. The
+// LayerNorm is layernorm_kernel's arithmetic (lane = float4 column groups, sequential
+// per-lane sums, xor-shuffle trees, two-pass variance).
+template <int NW, int K>
+__global__ __launch_bounds__(NW * 64) void resid_ln_kernel(ResidLnArgs p) {
+  constexpr int N = 32 * NW, NV = N / 4, MAXV = (NV + 63) / 64;
+  constexpr int KS = K / 32, AP = frag_pitch(K);
+  extern __shared__ __attribute__((aligned(16))) unsigned char rl_smem[];
+  _Float16* sA = reinterpret_cast<_Float16*>(rl_smem);                  // [16][AP]
+  float* sX = reinterpret_cast<float*>(rl_smem + 16 * AP * 2);          // [16][N]
+  float* sG = sX + 16 * N;                                              // [N] gamma
+  float* sB = sG + N;                                                   // [N] beta
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int r0 = blockIdx.x * 16, M = p.M;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+
+  // k-step of sequence position j: 0, 8, 1, 9, ... (pairs (i, i + 8) adjacent)
+  auto kstep = [](int j) { return (j & 1) * 8 + (j >> 1); };
+  const _Float16* wr0 = p.W + (int64_t)(32 * w + lr) * p.ldw + kc8;
+  const _Float16* wr1 = wr0 + 16 * p.ldw;
+  constexpr int RING = 4;  // sequence positions in flight (2 x 16 B per lane each)
+  half8 wb[RING][2];
+#pragma unroll
+  for (int j = 0; j < RING; ++j) {
+    const int ks = kstep(j);
+    wb[j][0] = ks < KS ? *reinterpret_cast<const half8*>(wr0 + 32 * ks) : zero_half8();
+    wb[j][1] = ks < KS ? *reinterpret_cast<const half8*>(wr1 + 32 * ks) : zero_half8();
+  }
+  // epilogue operands: bias + residual of this lane's 4 rows x 2 columns
+  float e[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = 32 * w + 16 * t + lr;
+    const float bs = p.bias ? p.bias[col] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * (lane >> 4) + r;
+      e[t][r] = bs + (row < M ? p.x[(int64_t)row * p.ldx + col] : 0.0f);
+    }
+  }
+  // A rows and gamma / beta -> LDS
+  for (int i = tid; i < 16 * (K / 8); i += NW * 64) {
+    const int rr = i / (K / 8), c8 = (i % (K / 8)) * 8;
+    const int row = min(r0 + rr, M - 1);
+    *reinterpret_cast<half8*>(sA + rr * AP + c8) =
+        *reinterpret_cast<const half8*>(p.A + (int64_t)row * p.lda + c8);
+  }
+  for (int i = tid; i < NV; i += NW * 64) {
+    reinterpret_cast<float4*>(sG)[i] = reinterpret_cast<const float4*>(p.g)[i];
+    reinterpret_cast<float4*>(sB)[i] = reinterpret_cast<const float4*>(p.b)[i];
+  }
+  __syncthreads();
+
+  f32x4 v[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) v[t] = f32x4{e[t][0], e[t][1], e[t][2], e[t][3]};
+  f32x4 pl[2];
+#pragma unroll
+  for (int j = 0; j < 2 * 8; ++j) {
+    // keep each refill at its iteration: hoisted, all 32 weight loads of the wave would be
+    // live at once (164 VGPRs; spills under the 16-wave 128-VGPR budget)
+    __builtin_amdgcn_sched_barrier(0);
+    const int ks = kstep(j);
+    const int slot = j % RING;
+    half8 af = ks < KS ? *reinterpret_cast<const half8*>(sA + lr * AP + 32 * ks + kc8) : zero_half8();
+    f32x4 pc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) pc[t] = mfma16(af, wb[slot][t], zero_f32x4());
+    // refill the slot with sequence position j + RING
+    if (j + RING < 16) {
+      const int kn = kstep(j + RING);
+      wb[slot][0] = kn < KS ? *reinterpret_cast<const half8*>(wr0 + 32 * kn) : zero_half8();
+      wb[slot][1] = kn < KS ? *reinterpret_cast<const half8*>(wr1 + 32 * kn) : zero_half8();
+    }
+    if ((j & 1) == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) pl[t] = pc[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) v[t] += pl[t] + pc[t];
+    }
+  }
+  // new residual rows -> global (fp32) and LDS
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = 32 * w + 16 * t + lr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = 4 * (lane >> 4) + r;
+      sX[rr * N + col] = v[t][r];
+      if (r0 + rr < M) p.x[(int64_t)(r0 + rr) * p.ldx + col] = v[t][r];
+    }
+  }
+  __syncthreads();
+  // LayerNorm, one wave per row (layernorm_kernel's arithmetic)
+  for (int rr = w; rr < 16; rr += NW) {
+    if (r0 + rr >= M) break;
+    const float4* xr = reinterpret_cast<const float4*>(sX + rr * N);
+    float4 xv[MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int i = lane + k * 64;
+      xv[k] = i < NV ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      s += ln_sum4(xv[k]);
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)N;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int i = lane + k * 64;
+      if (i < NV) q += ln_sq4(xv[k], mean);
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = rsqrtf(q / (float)N + p.eps);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int i = lane + k * 64;
+      if (i >= NV) continue;
+      const float4 gg = reinterpret_cast<const float4*>(sG)[i];
+      const float4 bb = reinterpret_cast<const float4*>(sB)[i];
+      reinterpret_cast<half4*>(p.out + (int64_t)(r0 + rr) * N)[i] = ln_norm4(xv[k], mean, rstd, gg, bb);
+    }
+  }
+}
+
+template <int NW, int K>
+static void resid_ln_go(const ResidLnArgs& p, hipStream_t s) {
+  auto kern = resid_ln_kernel<NW, K>;
+  const size_t lds = (size_t)16 * frag_pitch(p.K) * 2 + (size_t)(16 + 2) * 32 * NW * 4;
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr = true;
+  }
+  kern<<<(p.M + 15) / 16, NW * 64, lds, s>>>(p);
+}
+
+bool resid_ln_supported(int N, int K) { return (N == 384 || N == 512) && K == N; }
+
+void resid_ln_launch(const ResidLnArgs& p, hipStream_t s) {
+  JANUS_CHECK(resid_ln_supported(p.N, p.K), "resid_ln: N = K in {384, 512}");
+  JANUS_CHECK(p.ldx == p.N && p.lda % 8 == 0 && p.ldw % 8 == 0, "resid_ln: ldx == N, lda / ldw % 8 == 0");
+  JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0 && ((uintptr_t)p.x & 15) == 0 &&
+                  ((uintptr_t)p.g & 15) == 0 && ((uintptr_t)p.b & 15) == 0 && ((uintptr_t)p.out & 7) == 0,
+              "resid_ln: operands must be aligned");
+  if (p.M <= 0) return;
+  if (p.N == 512) resid_ln_go<16, 512>(p, s);
+  else resid_ln_go<12, 384>(p, s);
   JANUS_LAUNCH_CHECK();
 }
 

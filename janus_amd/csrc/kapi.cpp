@@ -76,6 +76,20 @@ extern "C" int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const flo
   });
 }
 
+extern "C" int janus_resid_ln_f16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                                  const float* bias, float* x, const float* gamma, const float* beta,
+                                  float eps, uint16_t* out, int M, int N, int K, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(A && W && x && gamma && beta && out, "resid_ln: null argument");
+    ResidLnArgs p;
+    p.A = reinterpret_cast<const _Float16*>(A); p.lda = lda;
+    p.W = reinterpret_cast<const _Float16*>(W); p.ldw = ldw;
+    p.bias = bias; p.x = x; p.ldx = N; p.g = gamma; p.b = beta; p.eps = eps;
+    p.out = reinterpret_cast<_Float16*>(out); p.M = M; p.N = N; p.K = K;
+    resid_ln_launch(p, (hipStream_t)stream);
+  });
+}
+
 extern "C" int janus_layernorm_f16(const float* x, const float* gamma, const float* beta,
                                    uint16_t* out, int rows, int d, float eps, void* stream) {
   return guarded([&] {

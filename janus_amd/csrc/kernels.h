@@ -38,6 +38,20 @@ struct GemmArgs {
   const float* lnin_g = nullptr; const float* lnin_b = nullptr; float lnin_eps = 1e-5f;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
+// x[M][N] += A W^T + bias (fp32, in place), then out[M][N] = LayerNorm(x) fp16 (gamma g,
+// beta b, eps) — one launch for the decoder's attention output projection + the next
+// LayerNorm (resid_ln_kernel in gemm.hip; bit-identical to the two launches it replaces).
+struct ResidLnArgs {
+  const _Float16* A; int64_t lda;  // [M][K]
+  const _Float16* W; int64_t ldw;  // [N][K]
+  const float* bias;               // [N] or null
+  float* x; int64_t ldx;           // [M][N] residual stream, ldx == N
+  const float* g; const float* b; float eps;
+  _Float16* out;                   // [M][N]
+  int M, N, K;
+};
+bool resid_ln_supported(int N, int K);
+void resid_ln_launch(const ResidLnArgs& p, hipStream_t s);
 
 // M <= 64 GEMM with the LayerNorm of its fp32 A operand fused (decoder pre-LN blocks).
 // EPI_QKV: columns [0, d) -> C, [d, 2d) -> kc[row][pos], [2d, 3d) -> vc[row][pos].

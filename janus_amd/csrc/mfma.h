@@ -133,6 +133,26 @@ __device__ __forceinline__ int tile_remap(int bid, int nblocks) {
 #endif
 }
 
+// LayerNorm arithmetic shared by layernorm_kernel and resid_ln_kernel (gemm.hip), written
+// with explicit fmaf and no other contraction so the two kernels round alike: left to the
+// compiler, a*a + b*b may become fma(a, a, b*b) in one kernel and fma(b, b, a*a) in the
+// other.
+__device__ __forceinline__ float ln_sum4(const float4& v) {
+#pragma clang fp contract(off)
+  return ((v.x + v.y) + v.z) + v.w;
+}
+__device__ __forceinline__ float ln_sq4(const float4& v, float mean) {
+#pragma clang fp contract(off)
+  const float a = v.x - mean, b = v.y - mean, c = v.z - mean, e = v.w - mean;
+  return fmaf(e, e, fmaf(c, c, fmaf(b, b, a * a)));
+}
+__device__ __forceinline__ half4 ln_norm4(const float4& v, float mean, float rstd, const float4& g,
+                                          const float4& b) {
+#pragma clang fp contract(off)
+  return half4{(_Float16)fmaf((v.x - mean) * rstd, g.x, b.x), (_Float16)fmaf((v.y - mean) * rstd, g.y, b.y),
+               (_Float16)fmaf((v.z - mean) * rstd, g.z, b.z), (_Float16)fmaf((v.w - mean) * rstd, g.w, b.w)};
+}
+
 // LayerNorm of R fp32 rows by one wave (rows row0 + j*rstep, j < R; d <= 256*MAXV, d % 4
 // == 0): every row, gamma and beta load is issued before the first use (one memory round
 // trip for all R rows); fp16 out rows at out + (lrow0 + j*rstep)*ldo, ALL R of them written

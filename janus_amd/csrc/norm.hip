@@ -1,6 +1,7 @@
 // LayerNorm over the fp32 residual stream (Whisper pre-LN blocks, eps 1e-5), one
 // wavefront per row; two-pass mean/variance from registers, wave-shuffle reductions,
-// 16-byte loads/stores. HBM-bound: 4·d B read + 2·d B written per row.
+// 16-byte loads/stores. HBM-bound: 4·d B read + 2·d B written per row. The fp16 path's
+// arithmetic is mfma.h's ln_sum4 / ln_sq4 / ln_norm4 (shared with resid_ln_kernel).
 #include "mfma.h"
 #include "kernels.h"
 
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int k = 0; k < MAXV; ++k) {
     const int i = lane + k * 64;
     v[k] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    s += v[k].x + v[k].y + v[k].z + v[k].w;
+    s += ln_sum4(v[k]);
   }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   const float mean = s / d;
@@ -40,10 +41,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int i = lane + k * 64;
-    if (i < nv) {
-      const float a = v[k].x - mean, bb = v[k].y - mean, c = v[k].z - mean, e = v[k].w - mean;
-      q += a * a + bb * bb + c * c + e * e;
-    }
+    if (i < nv) q += ln_sq4(v[k], mean);
   }
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
   const float rstd = rsqrtf(q / d + eps);
@@ -51,16 +49,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int k = 0; k < MAXV; ++k) {
     const int i = lane + k * 64;
     if (i >= nv) continue;
-    float4 y;
-    y.x = (v[k].x - mean) * rstd * gg[k].x + bb[k].x;
-    y.y = (v[k].y - mean) * rstd * gg[k].y + bb[k].y;
-    y.z = (v[k].z - mean) * rstd * gg[k].z + bb[k].z;
-    y.w = (v[k].w - mean) * rstd * gg[k].w + bb[k].w;
     if constexpr (F32OUT) {
+      float4 y;
+      y.x = (v[k].x - mean) * rstd * gg[k].x + bb[k].x;
+      y.y = (v[k].y - mean) * rstd * gg[k].y + bb[k].y;
+      y.z = (v[k].z - mean) * rstd * gg[k].z + bb[k].z;
+      y.w = (v[k].w - mean) * rstd * gg[k].w + bb[k].w;
       reinterpret_cast<float4*>(static_cast<float*>(out) + (int64_t)row * d)[i] = y;
     } else {
-      half4 h = {(_Float16)y.x, (_Float16)y.y, (_Float16)y.z, (_Float16)y.w};
-      reinterpret_cast<half4*>(static_cast<_Float16*>(out) + (int64_t)row * d)[i] = h;
+      reinterpret_cast<half4*>(static_cast<_Float16*>(out) + (int64_t)row * d)[i] =
+          ln_norm4(v[k], mean, rstd, gg[k], bb[k]);
     }
   }
 }

@@ -451,6 +451,14 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     return g;
   };
   const bool lnp2 = ln_pro_mask & 2, lnp3 = ln_pro_mask & 4, lnp_fin = ln_pro_mask & 8;
+  // Opt-in (JANUS_RESID_LN): the attention output projections and the LayerNorm after
+  // them (LN2 / LN3) in one launch (resid_ln_kernel: 16 rows per block over all d columns,
+  // bit-identical to the residual GEMM + LayerNorm pair). Measured 72 ms per step SLOWER
+  // on the decoder side (361 vs 289 ms): at B = 64 only 4 blocks stream the 0.5 MB weight
+  // each, at ~25 GB/s per CU (≈ 24 µs per launch against 5.6 + 5.0 µs for the pair).
+  const bool rln = B <= 64 && !fused_ln && !ln_fuse && resid_ln_supported(d, d) &&
+                   std::getenv("JANUS_RESID_LN") != nullptr;
+  const bool rln2 = rln && !lnp2, rln3 = rln && !lnp3;
   Z.d_lncnt.ensure(sizeof(int));
   JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int), s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
@@ -461,6 +469,14 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     if (fused_ln) g.ln_part = lnp;
     if (ln_fuse) { g.ln_g = ng; g.ln_b = nb; g.ln_out = a; g.ln_cnt = Z.d_lncnt.as<int>(); }
     gemm_launch(EPI_RESID_F32, g, s);
+  };
+  auto resid_ln = [&](const _Float16* A, const DevMem& W, const float* bias, const float* ng,
+                      const float* nb) {
+    ResidLnArgs p;
+    p.A = A; p.lda = d; p.W = W.as<_Float16>(); p.ldw = d; p.bias = bias;
+    p.x = x; p.ldx = d; p.g = ng; p.b = nb; p.eps = 1e-5f; p.out = a;
+    p.M = B; p.N = d; p.K = d;
+    resid_ln_launch(p, s);
   };
   auto step = [&](int pos) {
     embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
@@ -492,7 +508,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s);
-      resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
+      if (rln2) resid_ln(o, L.wo, L.bo, L.ln2g, L.ln2b);
+      else resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
       if (xabs) {
         const int hd = H * d;
         _Float16* xqk = Z.d_xqk.as<_Float16>();
@@ -501,7 +518,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wqk.as<_Float16>(), L.bqk.as<float>(),
                                                 xqk, hd, hd, nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse && !lnp2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse && !lnp2 && !rln2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
                                        L.ln2g, L.ln2b, lnp2), s);
         }
@@ -510,25 +527,27 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         GemmArgs gv = dgargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
         gv.a_group_cols = 64;
         gemm_launch(EPI_F16, gv, s);
-        resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
+        if (rln3) resid_ln(o, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
+        else resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
       } else {
         if (fused_ln) {
           gemm_skinny_ln_launch(EPI_F16, lnargs(L.ln2g, L.ln2b, L.wq_c.as<_Float16>(), L.bq_c, q2, d, d,
                                                 nullptr, nullptr, pos), s);
         } else {
-          if (!ln_fuse && !lnp2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
+          if (!ln_fuse && !lnp2 && !rln2) layernorm_launch(x, L.ln2g, L.ln2b, a, B, d, 1e-5f, s);
           gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wq_c.as<_Float16>(), d, L.bq_c, q2, d, B, d, d),
                                        L.ln2g, L.ln2b, lnp2), s);
         }
         decode_attention_split_launch(q2, d, ck, cv, (int64_t)Te * d, d, Te, o, d, B, H, scale, part_o,
                                       part_ml, s);
-        resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
+        if (rln3) resid_ln(o, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
+        else resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
       }
       if (fused_ln) {
         gemm_skinny_ln_launch(EPI_GELU_F16, lnargs(L.ln3g, L.ln3b, L.w1.as<_Float16>(), L.b1, f, 4 * d,
                                                    4 * d, nullptr, nullptr, pos), s);
       } else {
-        if (!ln_fuse && !lnp3) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
+        if (!ln_fuse && !lnp3 && !rln3) layernorm_launch(x, L.ln3g, L.ln3b, a, B, d, 1e-5f, s);
         gemm_launch(EPI_GELU_F16, with_ln(dgargs(a, d, L.w1.as<_Float16>(), d, L.b1, f, 4 * d, B, 4 * d, d),
                                           L.ln3g, L.ln3b, lnp3), s);
       }
@@ -552,7 +571,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};

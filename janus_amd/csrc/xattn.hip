@@ -25,11 +25,11 @@
 // then per-split partial (C, m, l) in fp32; xattn_combine merges the splits into
 // c[b][h*D + j] fp16, the A operand of the per-head Wv GEMM.
 #include "mfma.h"
+#include <cstdlib>
 #include "kernels.h"
 
 namespace janus {
 
-constexpr int kXKeys = 32;  // keys per chunk
 
 typedef short short4v __attribute__((ext_vector_type(4)));
 
@@ -81,28 +81,33 @@ __device__ __forceinline__ int xkappa_inv(int key) {
   return 8 * (2 * g2 + g1) + 4 * hf + q;
 }
 
-template <int D>
+template <int D, int CH>
 struct XGeo {
+  static constexpr int NW = CH / 8;          // waves: CH / 16 key tiles x 2 dim halves
+  static constexpr int NKT = CH / 16;        // S-phase key tiles
   static constexpr int QP = D + 16;          // sE row pitch (halves)
-  static constexpr int PP = 48;              // sP pitch (halves), frag_pitch(32)
+  static constexpr int PP = CH + 16;         // sP pitch (halves): frag_pitch(CH)
   static constexpr int KH = D / 2;           // dims per S-phase k-half
   static constexpr int KS = KH / 32;         // S-phase k-steps per wave
-  static constexpr int NT = D / 64;          // C-phase 16-col tiles per wave
-  static constexpr int LDS = (kXKeys * QP + 16 * PP) * 2 + 2 * 16 * kXKeys * 4 + 16 * 4;
+  static constexpr int NT = D / (16 * NW);   // C-phase 16-col tiles per wave
+  static constexpr int HPW = 16 / NW;        // softmax heads per wave
+  static constexpr int LDS = (CH * QP + 16 * PP) * 2 + 2 * 16 * CH * 4 + 16 * 4;
 };
 
-template <int D>
-__global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Float16* __restrict__ qk,
-                                                    const _Float16* __restrict__ enc, int Te,
-                                                    int H, int kps, float* __restrict__ part_c,
-                                                    float* __restrict__ part_ml) {
-  using G = XGeo<D>;
-  constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT;
+// CH keys per chunk: 32 (4 waves, three blocks per CU) or 64 (8 waves: half the serial
+// chunk steps per split at the same registers per wave).
+template <int D, int CH>
+__global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xattn_kernel(
+    const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
+    float* __restrict__ part_c, float* __restrict__ part_ml) {
+  using G = XGeo<D, CH>;
+  constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT, NW = G::NW,
+                NKT = G::NKT, HPW = G::HPW;
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
-  _Float16* sE = smem;                         // [32][QP] keys x dims
-  _Float16* sP = sE + kXKeys * QP;             // [16][PP] heads x (permuted) keys
-  float* sS = reinterpret_cast<float*>(sP + 16 * PP);  // [2][16][32] partial scores
-  float* sA = sS + 2 * 16 * kXKeys;            // [16] rescale factors
+  _Float16* sE = smem;                         // [CH][QP] keys x dims
+  _Float16* sP = sE + CH * QP;                 // [16][PP] heads x (permuted) keys
+  float* sS = reinterpret_cast<float*>(sP + 16 * PP);  // [2][16][CH] partial scores
+  float* sA = sS + 2 * 16 * CH;                // [16] rescale factors
 
   const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
@@ -111,14 +116,14 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
 
   // S-phase role: key tile nt (16 keys), dims half kh; the wave's Qk fragments (rows =
   // heads, zero rows >= H) stay in registers for the whole split
-  const int nt = w & 1, kh = w >> 1;
+  const int nt = w % NKT, kh = w / NKT;
   const int lr = lane & 15, lg = lane >> 4;
   half8 qa[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
     qa[ks] = lr < H ? *reinterpret_cast<const half8*>(qk + ((int64_t)b * H + lr) * D + kh * KH + 32 * ks + 8 * lg)
                     : zero_half8();
-  for (int i = tid; i < 16 * PP; i += 256) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
+  for (int i = tid; i < 16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
 
   half8 ef[KS];
   auto load_e = [&](int t) {
@@ -140,13 +145,13 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
   f32x4 accc[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) accc[n] = zero_f32x4();
-  float m_run[4], l_run[4];
+  float m_run[HPW], l_run[HPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
+  for (int i = 0; i < HPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 
   if (t0 < t1) load_e(t0);
   __syncthreads();
-  for (int t = t0; t < t1; t += kXKeys) {
+  for (int t = t0; t < t1; t += CH) {
     // ---- S partial: rows = heads, cols = keys 16nt.., k = dims of half kh
     f32x4 accs = zero_f32x4();
 #pragma unroll
@@ -156,18 +161,18 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
     for (int ks = 0; ks < KS; ++ks)
       *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = ef[ks];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sS[(kh * 16 + 4 * lg + r) * kXKeys + 16 * nt + lr] = accs[r];
-    if (t + kXKeys < t1) load_e(t + kXKeys);  // next chunk in flight during softmax + P.E
+    for (int r = 0; r < 4; ++r) sS[(kh * 16 + 4 * lg + r) * CH + 16 * nt + lr] = accs[r];
+    if (t + CH < t1) load_e(t + CH);  // next chunk in flight during softmax + P.E
     __syncthreads();
 
-    // ---- online softmax: wave w owns heads w, w+4, w+8, w+12; lane = key (lanes < 32)
-    const int nk = min(kXKeys, t1 - t);
+    // ---- online softmax: wave w owns heads w, w + NW, ...; lane = key (lanes < CH)
+    const int nk = min(CH, t1 - t);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int h = w + 4 * i;
+    for (int i = 0; i < HPW; ++i) {
+      const int h = w + NW * i;
       if (h >= H) break;  // wave-uniform
       const bool valid = lane < nk;
-      const float sc = valid ? sS[h * kXKeys + lane] + sS[(16 + h) * kXKeys + lane] : -INFINITY;
+      const float sc = valid ? sS[h * CH + lane] + sS[(16 + h) * CH + lane] : -INFINITY;
       float mc = sc;
       for (int o = 32; o > 0; o >>= 1) mc = fmaxf(mc, __shfl_xor(mc, o));
       const float m_new = fmaxf(m_run[i], mc);
@@ -177,12 +182,12 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
       for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
       l_run[i] = l_run[i] * alpha + ps;
       m_run[i] = m_new;
-      if (lane < kXKeys) sP[h * PP + xkappa_inv(lane)] = (_Float16)p;
+      if (lane < CH) sP[h * PP + (lane & ~31) + xkappa_inv(lane & 31)] = (_Float16)p;
       if (lane == 0) sA[h] = alpha;
     }
     __syncthreads();
 
-    // ---- C += P . E over this chunk; wave w owns dims [w*D/4, (w+1)*D/4)
+    // ---- C += P . E over this chunk; wave w owns dims [w*D/NW, (w+1)*D/NW)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * lg + r;
@@ -190,22 +195,25 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
 #pragma unroll
       for (int n = 0; n < NT; ++n) accc[n][r] *= al;
     }
-    const half8 pa = *reinterpret_cast<const half8*>(sP + lr * PP + 8 * lg);
     const int q = lr >> 2, pcol = 4 * (lr & 3);
     const int row0 = 16 * (lg >> 1) + 4 * (lg & 1) + q;  // kappa(8lg + q), hf = 0
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int c0 = w * (D / 4) + 16 * n + pcol;
-      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) short4v*)(sE + row0 * QP + c0));
-      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) short4v*)(sE + (row0 + 8) * QP + c0));
-      half8 bv;
-      const _Float16* l4 = reinterpret_cast<const _Float16*>(&lo);
-      const _Float16* h4 = reinterpret_cast<const _Float16*>(&hi);
+    for (int kk = 0; kk < CH / 32; ++kk) {
+      const half8 pa = *reinterpret_cast<const half8*>(sP + lr * PP + 32 * kk + 8 * lg);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { bv[j] = l4[j]; bv[4 + j] = h4[j]; }
-      accc[n] = mfma16(pa, bv, accc[n]);
+      for (int n = 0; n < NT; ++n) {
+        const int c0 = w * (D / NW) + 16 * n + pcol;
+        const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)(sE + (32 * kk + row0) * QP + c0));
+        const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)(sE + (32 * kk + row0 + 8) * QP + c0));
+        half8 bv;
+        const _Float16* l4 = reinterpret_cast<const _Float16*>(&lo);
+        const _Float16* h4 = reinterpret_cast<const _Float16*>(&hi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { bv[j] = l4[j]; bv[4 + j] = h4[j]; }
+        accc[n] = mfma16(pa, bv, accc[n]);
+      }
     }
     __syncthreads();  // sE / sS / sP are rewritten by the next chunk
   }
@@ -217,12 +225,12 @@ __global__ __launch_bounds__(256, D > 512 ? 2 : 3) void xattn_kernel(const _Floa
     const int row = 4 * lg + r;
     if (row >= H) continue;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) pc[(int64_t)row * D + w * (D / 4) + 16 * n + lr] = accc[n][r];
+    for (int n = 0; n < NT; ++n) pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr] = accc[n][r];
   }
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int h = w + 4 * i;
+    for (int i = 0; i < HPW; ++i) {
+      const int h = w + NW * i;
       if (h < H) {
         float* pm = part_ml + (((int64_t)b * nsplit + s) * H + h) * 2;
         pm[0] = m_run[i];
@@ -316,23 +324,23 @@ __global__ __launch_bounds__(128) void xattn_combine_wide_kernel(const float* __
 int xattn_split_count(int Te, int requested) {
   int n = requested > 0 ? requested : 8;  // 512 blocks at batch 64 (bench sweep: 8 < 6, 10, 12)
   n = std::min(n, 63);
-  n = std::min(n, (Te + kXKeys - 1) / kXKeys);
+  n = std::min(n, (Te + 63) / 64);  // at least one 64-key chunk per split
   return std::max(n, 1);
 }
 
-template <int D>
+template <int D, int CH>
 static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
                       float* part_c, float* part_ml, hipStream_t s) {
-  const int chunks = (Te + kXKeys - 1) / kXKeys;
-  const int kps = (chunks + nsplit - 1) / nsplit * kXKeys;
-  auto kern = xattn_kernel<D>;
+  const int chunks = (Te + CH - 1) / CH;
+  const int kps = (chunks + nsplit - 1) / nsplit * CH;
+  auto kern = xattn_kernel<D, CH>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
     attr = true;
   }
-  kern<<<dim3(nsplit, B), 256, XGeo<D>::LDS, s>>>(qk, enc, Te, H, kps, part_c, part_ml);
+  kern<<<dim3(nsplit, B), CH * 8, XGeo<D, CH>::LDS, s>>>(qk, enc, Te, H, kps, part_c, part_ml);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -345,9 +353,17 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   JANUS_CHECK(xattn_supported(D, H), "xattn: need D = 64 H in {384, 512, 768}");
   if (B <= 0 || Te <= 0) return;
   JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
-  if (D == 384) xattn_cfg<384>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
-  else if (D == 512) xattn_cfg<512>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
-  else xattn_cfg<768>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  // 64-key chunks (8 waves) unless JANUS_XATTN_CH32
+  static const bool ch32 = std::getenv("JANUS_XATTN_CH32") != nullptr;
+  if (D == 384) {
+    if (ch32) xattn_cfg<384, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+    else xattn_cfg<384, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  } else if (D == 512) {
+    if (ch32) xattn_cfg<512, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+    else xattn_cfg<512, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  } else {
+    xattn_cfg<768, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+  }
   if (nsplit <= kXCombMax && D <= 512)
     xattn_combine_wide_kernel<<<dim3(H, B), 128, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
   else

@@ -275,3 +275,37 @@ def test_gemm_layernorm_prologue(gpu, M, N, epi):
              dW.data_ptr(), K, dbias.data_ptr(), out.data_ptr(), N, M, N, K, stream())
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 2e-3
+
+
+@pytest.mark.parametrize("M,d", [(64, 512), (37, 512), (5, 384), (64, 384)])
+def test_resid_ln_matches_two_launches(gpu, M, d):
+    """janus_resid_ln_f16 (the decoder's attention output projection + the following
+    LayerNorm in one launch) is bit-identical to the residual skinny GEMM followed by the
+    LayerNorm launch it replaces, and within fp32 rounding of a float64 reference."""
+    g = torch.Generator().manual_seed(M + d)
+    A = torch.randn(M, d, generator=g).half()
+    W = (torch.randn(d, d, generator=g) / math.sqrt(d)).half()
+    bias = torch.randn(d, generator=g) * 0.1
+    x0 = torch.randn(M, d, generator=g) * 2.0 + 0.3
+    gam = torch.randn(d, generator=g) * 0.2 + 1.0
+    bet = torch.randn(d, generator=g) * 0.1
+    dA, dW, db, dg, dbt = A.to(gpu), W.to(gpu), bias.to(gpu), gam.to(gpu), bet.to(gpu)
+    # two launches
+    x1 = x0.to(gpu)
+    out1 = torch.empty(M, d, dtype=torch.float16, device=gpu)
+    nat.call("janus_gemm_f16", 2, dA.data_ptr(), d, dW.data_ptr(), d, db.data_ptr(), x1.data_ptr(), d,
+             x1.data_ptr(), d, M, d, d, stream())
+    nat.call("janus_layernorm_f16", x1.data_ptr(), dg.data_ptr(), dbt.data_ptr(), out1.data_ptr(), M, d,
+             1e-5, stream())
+    # one launch
+    x2 = x0.to(gpu)
+    out2 = torch.empty(M, d, dtype=torch.float16, device=gpu)
+    nat.call("janus_resid_ln_f16", dA.data_ptr(), d, dW.data_ptr(), d, db.data_ptr(), x2.data_ptr(),
+             dg.data_ptr(), dbt.data_ptr(), 1e-5, out2.data_ptr(), M, d, d, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(x1, x2)
+    assert torch.equal(out1, out2)
+    ref_x = x0.double() + A.double() @ W.double().T + bias.double()
+    assert rel_err(x2, ref_x) < 1e-6
+    ref = F.layer_norm(ref_x, (d,), gam.double(), bet.double(), 1e-5)
+    assert rel_err(out2, ref) < 1e-3
