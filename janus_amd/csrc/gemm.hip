@@ -398,15 +398,18 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores drained
       __syncthreads();                                   // ... and every other wave's
+      // one counter per row block: the last of its gridDim.x column blocks to arrive
+      // normalises the block's rows (one row per wave), in parallel over row blocks
+      int* cnt = p.ln_cnt + blockIdx.y;
       if (tid == 0)
-        s_last = __hip_atomic_fetch_add(p.ln_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (int)(gridDim.x * gridDim.y) - 1;
+        s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (int)gridDim.x - 1;
       __syncthreads();
       if (!s_last) return;
-      for (int r = w; r < M; r += kSkWaves)
+      for (int r = r0 + w; r < min(M, r0 + 16 * MTB); r += kSkWaves)
         ln_row_wave<true>(static_cast<const float*>(p.C) + (int64_t)r * p.ldc, p.ln_g, p.ln_b,
                           p.ln_out + (int64_t)r * N, N, p.ln_eps, lane);
-      if (tid == 0) __hip_atomic_store(p.ln_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     if (eok) static_cast<float*>(p.C)[(int64_t)erow * p.ldc + ecol] = v;

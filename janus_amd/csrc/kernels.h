@@ -26,9 +26,11 @@ struct GemmArgs {
   // (0 = JANUS_SKINNY_MSPLIT_N or 2048, tuned on a whole GPU; 1024 on a half-GPU CU mask)
   int msplit_n = 0;
   // EPI_RESID_F32 (M <= 64 only): the LayerNorm of the NEW residual rows, fused: the
-  // output rows are stored write-through (sc1), every block adds to ln_cnt once its
-  // stores have drained, and the last block to arrive normalises all M rows (sc1 loads)
-  // into ln_out [M][N] fp16 with (ln_g, ln_b, ln_eps) and re-arms ln_cnt (zero on entry).
+  // output rows are stored write-through (sc1), every block adds to its row block's
+  // counter ln_cnt[blockIdx.y] once its stores have drained, and the last block of each
+  // row block to arrive normalises that block's rows (sc1 loads, one row per wave) into
+  // ln_out [M][N] fp16 with (ln_g, ln_b, ln_eps) and re-arms its counter (ln_cnt: at
+  // least ceil(M / 16) ints, zero on entry).
   const float* ln_g = nullptr; const float* ln_b = nullptr; float ln_eps = 1e-5f;
   _Float16* ln_out = nullptr; int* ln_cnt = nullptr;
   // M <= 64 only: A = LayerNorm(lnin_x) (fp32 [M][K], row stride lnin_ldx) computed in

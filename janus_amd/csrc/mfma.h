@@ -133,6 +133,39 @@ __device__ __forceinline__ int tile_remap(int bid, int nblocks) {
 #endif
 }
 
+// Store an MFMA output fragment (lane = column col = tile column (lane & 15), rows row0 + rr,
+// rr < 4, row0 = m*16 + 4*(lane >> 4)) as fp16 into an LDS tile with 4-byte stores: lanes
+// l and l^1 trade two packed halves (one DPP quad_perm move), then the even lane writes rows
+// 0-1 and the odd lane rows 2-3 of the column pair (col & ~1, col | 1): half the store
+// instructions of per-element 2-byte stores. Opt-in build switch JANUS_C1_PAIRS: measured
+// slower (standalone 64 x 30 s vocoder 154.0 vs 151.9 ms), so the LDS bank conflicts of
+// the wide units do not come from these stores; the default is the 2-byte form.
+__device__ __forceinline__ void st_frag_f16_pairs(_Float16* tile, int ld, int row0, int col,
+                                                  const float (&v)[4], int lane) {
+#ifndef JANUS_C1_PAIRS
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) tile[(row0 + rr) * ld + col] = (_Float16)v[rr];
+#else
+  const bool odd = lane & 1;
+  const half2v mine_lo = {(_Float16)v[0], (_Float16)v[1]}, mine_hi = {(_Float16)v[2], (_Float16)v[3]};
+  const half2v send = odd ? mine_lo : mine_hi;
+  const int got_i = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), 0xB1 /* quad_perm [1,0,3,2] */,
+                                                0xF, 0xF, false);
+  const half2v got = __builtin_bit_cast(half2v, got_i);
+  half2v ra, rb;
+  if (odd) {  // rows 2, 3: (partner's column, mine)
+    ra = half2v{got[0], mine_hi[0]};
+    rb = half2v{got[1], mine_hi[1]};
+  } else {    // rows 0, 1: (mine, partner's column)
+    ra = half2v{mine_lo[0], got[0]};
+    rb = half2v{mine_lo[1], got[1]};
+  }
+  const int r = row0 + (odd ? 2 : 0), c0 = col & ~1;
+  *reinterpret_cast<half2v*>(tile + r * ld + c0) = ra;
+  *reinterpret_cast<half2v*>(tile + (r + 1) * ld + c0) = rb;
+#endif
+}
+
 // LayerNorm arithmetic shared by layernorm_kernel and resid_ln_kernel (gemm.hip), written
 // with explicit fmaf and no other contraction so the two kernels round alike: left to the
 // compiler, a*a + b*b may become fma(a, a, b*b) in one kernel and fma(b, b, a*a) in the

@@ -243,16 +243,17 @@ __global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int til
 #pragma unroll
         for (int n = 0; n < NTL; ++n) {
           const int co = n * 16 + arow;
+          float v[4];
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int r = m * 16 + 4 * (lane >> 4) + rr;
-            float v = silu(acc[j][n][rr] + bias1[n]);
+            v[rr] = silu(acc[j][n][rr] + bias1[n]);
             if (edge) {  // c2 zero-pads its input outside [0, T)
               const int t = t0 - P2 + r;
-              v = (t >= 0 && t < T) ? v : 0.0f;
+              v[rr] = (t >= 0 && t < T) ? v[rr] : 0.0f;
             }
-            sS[r * LI + co] = (_Float16)v;
           }
+          st_frag_f16_pairs(sS, LI, m * 16 + 4 * (lane >> 4), co, v, lane);
         }
       }
     }

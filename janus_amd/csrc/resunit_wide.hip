@@ -224,14 +224,15 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), 2) void resunit_wide_kernel(Re
       for (int j = 0; j < MW1; ++j) {
         const int m = wm + j * WM;
         if (j >= MT1 / WM && m >= MT1) break;
+        float v[4];
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
           // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
-          const float v = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
-          sS[r * LI + co] = (_Float16)v;
+          v[rr] = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
         }
+        st_frag_f16_pairs(sS, LI, m * 16 + 4 * (lane >> 4), co, v, lane);
       }
     }
   }
@@ -522,14 +523,15 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
       for (int j = 0; j < MW1; ++j) {
         const int m = wm + j * WM;
         if (j >= MT1 / WM && m >= MT1) break;
+        float v[4];
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
           // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
-          const float v = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
-          sS[r * LI + co] = (_Float16)v;
+          v[rr] = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
         }
+        st_frag_f16_pairs(sS, LI, m * 16 + 4 * (lane >> 4), co, v, lane);
       }
     }
     WIDE_WSTORE(rwA0, rwA1, 0);

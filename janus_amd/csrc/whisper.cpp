@@ -459,8 +459,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const bool rln = B <= 64 && !fused_ln && !ln_fuse && resid_ln_supported(d, d) &&
                    std::getenv("JANUS_RESID_LN") != nullptr;
   const bool rln2 = rln && !lnp2, rln3 = rln && !lnp3;
-  Z.d_lncnt.ensure(sizeof(int));
-  JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int), s));
+  Z.d_lncnt.ensure(sizeof(int) * 64);  // one arrival counter per 16-row block (JANUS_LN_FUSE)
+  JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int) * 64, s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
   const float* fin_b = w->params.get("decoder.layer_norm.bias", d);
   auto resid = [&](const _Float16* A, int K, const DevMem& W, const float* bias, const float* ng,
