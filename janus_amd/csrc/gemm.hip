@@ -445,6 +445,74 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
   }
 }
 
+// 64 rows x 32 columns per block (two 16-column tiles per wave), 16 waves split K at one
+// 32-deep k-step each (K <= 512): for plain fp16 projections wider than one 16-column tile
+// per CU (the decoder's 4096-wide absorbed query projection), one block per CU with half
+// the A re-reads of the 16-column form. Bit-identical to gemm_skinny_kernel<EPI_F16,
+// AM_F16, 4, K1> (same single-k-step MFMA per wave, same reduction order).
+__global__ __launch_bounds__(1024) void gemm_skinny2_kernel(SkinnyArgs p) {
+  __shared__ float red[2][8][64][17];
+  const int M = p.M, N = p.N, K = p.K;
+  const int col0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int kbeg = w * 32;
+  const bool kok = kbeg < K;  // wave-uniform
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  half8 bw[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int bcol = col0 + 16 * t + lr;
+    const _Float16* wrow = p.W + (int64_t)min(bcol, N - 1) * p.ldw;
+    bw[t] = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kbeg + kc8) : zero_half8();
+  }
+  half8 ah[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int r = m * 16 + lr;
+    ah[m] = (kok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kbeg + kc8)
+                           : zero_half8();
+  }
+  const int elr = tid >> 4, ec = tid & 15;
+  float e_add[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ecol = col0 + 16 * t + ec;
+    e_add[t] = (p.bias && elr < M && ecol < N) ? p.bias[ecol] : 0.0f;
+  }
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[m][t] = mfma16(ah[m], bw[t], zero_f32x4());
+  if (w < 8) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[t][w][m * 16 + 4 * (lane >> 4) + r][lr] = acc[m][t][r];
+  }
+  __syncthreads();
+  if (w >= 8) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[t][w - 8][m * 16 + 4 * (lane >> 4) + r][lr] += acc[m][t][r];
+  }
+  __syncthreads();
+  if (elr >= M) return;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ecol = col0 + 16 * t + ec;
+    float v = e_add[t];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[t][i][elr][ec];
+    if (ecol < N) static_cast<_Float16*>(p.C)[(int64_t)elr * p.ldc + ecol] = (_Float16)v;
+  }
+}
+
 template <int AM, int EPI, int MTB>
 static void skinny_go(const SkinnyArgs& p, dim3 grid, hipStream_t s) {
   auto kern = gemm_skinny_kernel<EPI, AM, MTB>;
@@ -485,6 +553,16 @@ static void launch_skinny_m(int epi, const SkinnyArgs& p, hipStream_t s) {
 
 template <int AM>
 static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
+  // plain fp16 outputs wider than 2048 columns (more 16-column tiles than a 128-CU
+  // partition holds in one round) at K <= 512: 32 columns per block
+  static const bool nct2 = std::getenv("JANUS_SKINNY_NO_NCT2") == nullptr;
+  if constexpr (AM == AM_F16) {
+    if (nct2 && epi == EPI_F16 && p.N > 2048 && p.K <= kSkWaves * 32 && p.a_group_cols == 0 && p.M <= 64) {
+      gemm_skinny2_kernel<<<(p.N + 31) / 32, 1024, 0, s>>>(p);
+      JANUS_LAUNCH_CHECK();
+      return;
+    }
+  }
   // narrow outputs (N <= JANUS_SKINNY_MSPLIT_N, default 2048: <= 128 column tiles) split the
   // rows over 16-row blocks as well, so 4x as many CUs share the latency-bound product
   static const int msplit_n = [] {
