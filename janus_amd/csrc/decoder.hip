@@ -376,7 +376,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
     LogitPart* __restrict__ parts, int ntiles, const float* __restrict__ lnx, int ldx,
-    const float* __restrict__ ln_g, const float* __restrict__ ln_b) {
+    const float* __restrict__ ln_g, const float* __restrict__ ln_b, int rot) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   constexpr int K = NKS * 32;
   constexpr int kLgWaves = lg_waves(K);
@@ -394,14 +394,16 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
 #else
 #define LG_WLD(P) (*reinterpret_cast<const half8*>(P))
 #endif
+  // logical tile t -> physical tile (t + rot) mod ntiles (see logits_partial_launch)
+  auto phys = [&](int t) { const int q = t + rot; return q >= ntiles ? q - ntiles : q; };
 #define LG_LOAD(BUF, TILE)                                                                    \
   do {                                                                                        \
-    const int bcol_ = min((TILE) * 16 + (lane & 15), V - 1);                                  \
+    const int bcol_ = min(phys(TILE) * 16 + (lane & 15), V - 1);                              \
     const _Float16* wrow_ = W + (int64_t)bcol_ * K + 8 * (lane >> 4);                         \
     _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks)                                        \
       bw[BUF][ks] = LG_WLD(wrow_ + 32 * ks);                                                  \
     /* 16 mask bytes per tile (the mask buffer is padded to a multiple of 16) */             \
-    sm16[BUF] = *reinterpret_cast<const uint4*>(smask + (TILE) * 16);                         \
+    sm16[BUF] = *reinterpret_cast<const uint4*>(smask + phys(TILE) * 16);                     \
   } while (0)
   const int tile0 = blockIdx.x * kLgWaves + w;
   const int stride = gridDim.x * kLgWaves;
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   for (int u = 0; u < NB; ++u) {
     const int tile = tb + u * stride;
     if (tile >= ntiles) break;  // wave-uniform
-    const int col0 = tile * 16;
+    const int col0 = phys(tile) * 16;
     f32x4 acc[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = zero_f32x4();
@@ -606,10 +608,27 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
     attr[ai] = true;
   }
   const int grid = logits_partial_blocks(V, K, max_blocks);
+  // Tile rotation: waves take tiles t, t + stride, ...; the first ntiles % stride waves get
+  // one tile more and set the kernel's length. The special tiles (eot / no_timestamps /
+  // timestamps at the top of the vocabulary, and the blank token's tile) run the general
+  // rule-filter epilogue, several times a plain tile's VALU work; rotated so they land in
+  // the first round of the waves with one tile fewer. Order-dependent only in the last
+  // bits of the softmax sums (the argmax ties break by index either way).
+  static const bool no_rot = std::getenv("JANUS_LG_NO_ROT") != nullptr;
+  int rot = 0;
+  {
+    const int stride = grid * nw, rem = ntiles % stride;
+    int s0 = ntiles;
+    for (int t : {R.eot, R.no_timestamps, R.ts_begin})
+      if (t >= 0 && t < V) s0 = std::min(s0, t / 16);
+    const int nspec = ntiles - s0;
+    if (!no_rot && rem > 0 && nspec > 0 && rem + nspec + (R.blank >= 0 ? 1 + R.blank / 16 : 0) <= stride)
+      rot = ((s0 - rem) % ntiles + ntiles) % ntiles;
+  }
   for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
     kern<<<grid, nw * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
                                           smask, rules + r0, parts + (int64_t)r0 * grid, ntiles,
-                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b);
+                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b, rot);
   JANUS_LAUNCH_CHECK();
 }
 
