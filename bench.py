@@ -148,7 +148,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    # JANUS_DIST_FORCE=1: the RCCL path (process group, barriers, max-over-ranks all-reduce,
+    # result gather) at world size 1 too — exercises it on a one-GPU box
+    use_dist = world > 1 or os.environ.get("JANUS_DIST_FORCE") == "1"
+    if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from janus_amd.dist import gather_results, shard
@@ -186,13 +189,13 @@ def main():
     for _ in range(args.warmup + (1 if args.overlap > 0 else 0)):
         enc = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     pipe.vocoder.conv_stats(reset=True)
     pipe.vocoder.set_timing(True)
     times = []
     tok_counts = []
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t_begin = time.perf_counter()
@@ -203,7 +206,7 @@ def main():
         times.append(time.perf_counter() - t0)
         tok_counts.append(enc.n_tokens)  # bookkeeping reduced after the timed region
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
@@ -214,7 +217,7 @@ def main():
     total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
     n_packets = sum(p is not None for p in enc.packets)
     n_stats = int(enc.stats.shape[0]) if enc.stats is not None else 0
-    if world > 1:
+    if use_dist:
         dist.all_reduce(total_t, op=dist.ReduceOp.MAX)
         # result gather (RCCL over xGMI): the job's packets and per-utterance prosody
         # stats (rms, mean f0, voiced hops) on every rank, untimed
@@ -313,7 +316,7 @@ def main():
             except Exception as e:  # reported, never fatal to the bench line
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 
