@@ -31,9 +31,9 @@ namespace janus {
 constexpr int kYinBuf = 4096;          // aubio pitch buffer (prosody.py:32)
 constexpr int kYinLen = kYinBuf / 2;   // yin fvec length
 // Block = NT threads, each lane owns 2 consecutive taus, so one pass covers 2·NT taus.
-// NT = 128 (256-tau passes, the default): voiced hops with F0 >= 190 Hz at 48 kHz exit
-// after one pass and F0 >= 95 Hz after two, so a 160 / 260 Hz voice computes half the
-// taus of a 512-tau pass. NT = 256 (512-tau passes) kept for A/B (JANUS_YIN_THREADS).
+// NT = 64 (128-tau passes, the default for an uncapped grid): a voiced hop stops within
+// 128 taus of its period (F0 >= 190 Hz at 48 kHz after two passes); NT = 128 / 256 (256- /
+// 512-tau passes) by JANUS_YIN_THREADS; 256 for a grid capped beside the decoder.
 
 __device__ __forceinline__ int find_utt(const int64_t* offs, int B, int64_t g) {
   // largest b with offs[b] <= g (offs is non-decreasing, offs[0]=0, offs[B]=total)
@@ -374,13 +374,18 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
     const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
     const int64_t grid = std::min<int64_t>(total_hops, cap);
-    // 128-thread blocks (256-tau passes) for an uncapped grid on its own CUs (overlapped
-    // step: 33.5 vs 36 ms); a capped grid beside the greedy decoder keeps the 256-thread
-    // blocks (back-to-back step: 422 vs 449 ms per step with 128)
+    // one-wave blocks (128-tau passes) for an uncapped grid on its own CUs (overlapped
+    // step, vocoder side: 297.3 vs 298.9 ms against 128-thread blocks, which had measured
+    // 33.5 vs 36 ms against 256); a capped grid beside the greedy decoder keeps the
+    // 256-thread blocks (back-to-back step: 422 vs 449 ms per step with 128)
     static const int nt_env = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 0;
-    const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 128);
+    const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 64);
     if (nt == 256)
       yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(
+          pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, level_thr, (unsigned)sample_rate,
+          f0_out, total_hops);
+    else if (nt == 64)  // 128-tau passes
+      yin_hops_kernel<64><<<dim3((unsigned)grid), dim3(64), 0, stream>>>(
           pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, level_thr, (unsigned)sample_rate,
           f0_out, total_hops);
     else
