@@ -456,8 +456,8 @@ __global__ __launch_bounds__(1024) void gemm_skinny2_kernel(SkinnyArgs p) {
   const int col0 = blockIdx.x * 32;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int kbeg = w * 32;
-  const bool kok = kbeg < K;  // wave-uniform
   const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const bool kok = kbeg + kc8 < K;  // this lane's 8 halves (K % 8 == 0)
   half8 bw[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {

@@ -23,7 +23,7 @@ def rel_err(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 200, 64), (64, 1536, 512), (1, 24, 8), (1500, 512, 2048),
-                                   (129, 130, 136), (64, 4096, 512), (20, 2056, 384)])
+                                   (129, 130, 136), (64, 4096, 512), (20, 2056, 384), (7, 2304, 200)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 def test_gemm(gpu, M, N, K, epi):
     g = torch.Generator().manual_seed(M * 7 + N + K + epi)
