@@ -107,7 +107,16 @@ int xattn_split_count(int Te, int requested);
 void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int H,
                   _Float16* wqk, float* bqk, hipStream_t s);
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
-                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s);
+                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
+                  bool combine = true);
+// The split merge of xattn_launch(..., combine = false) fused with the per-head value
+// projection: out[b][64h + j] = merge_s(part)[b][h] . wv[64h + j]^T + bv[64h + j]
+// (wv [H*64][D] fp16, out row stride ldo); bit-identical to the merge kernel followed by the
+// block-diagonal skinny GEMM.
+bool xattn_cvp_supported(int D, int H);
+void xattn_combine_vproj_launch(const float* part_c, const float* part_ml, int nsplit, int B, int H,
+                                int D, const _Float16* wv, const float* bv, _Float16* out, int64_t ldo,
+                                hipStream_t s);
 
 int decode_split_count(int Tkv);
 void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,

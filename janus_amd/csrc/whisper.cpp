@@ -459,6 +459,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const bool rln = B <= 64 && !fused_ln && !ln_fuse && resid_ln_supported(d, d) &&
                    std::getenv("JANUS_RESID_LN") != nullptr;
   const bool rln2 = rln && !lnp2, rln3 = rln && !lnp3;
+  // cross-attention split merge + per-head value projection in one launch
+  // (xattn_combine_vproj_kernel, bit-identical; JANUS_NO_CVP restores the two launches)
+  const bool cvp = xattn_cvp_supported(d, H) && xsplit <= 16 && std::getenv("JANUS_NO_CVP") == nullptr;
   Z.d_lncnt.ensure(sizeof(int) * 64);  // one arrival counter per 16-row block (JANUS_LN_FUSE)
   JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int) * 64, s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
@@ -522,11 +525,18 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           gemm_launch(EPI_F16, with_ln(dgargs(a, d, L.wqk.as<_Float16>(), d, L.bqk.as<float>(), xqk, hd, B, hd, d),
                                        L.ln2g, L.ln2b, lnp2), s);
         }
-        xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s);
-        // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo
-        GemmArgs gv = dgargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
-        gv.a_group_cols = 64;
-        gemm_launch(EPI_F16, gv, s);
+        // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo; the
+        // split merge and the value projection in one launch (cvp) where supported
+        xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s,
+                     !cvp);
+        if (cvp) {
+          xattn_combine_vproj_launch(Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xsplit, B, H, d,
+                                     L.wv_c.as<_Float16>(), L.bv_c, o, d, s);
+        } else {
+          GemmArgs gv = dgargs(xc, hd, L.wv_c.as<_Float16>(), d, L.bv_c, o, d, B, d, d);
+          gv.a_group_cols = 64;
+          gemm_launch(EPI_F16, gv, s);
+        }
         if (rln3) resid_ln(o, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
         else resid(o, d, L.wo_c, L.bo_c, L.ln3g, L.ln3b);
       } else {
@@ -571,7 +581,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)cvp, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};

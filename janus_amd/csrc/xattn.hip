@@ -311,14 +311,130 @@ __global__ __launch_bounds__(128) void xattn_combine_wide_kernel(const float* __
   for (int s = 0; s < kXCombMax; ++s) {
     if (s < nsplit) {
       const float wgt = exp2f(ml[s].x - M);  // empty split: m = -inf -> 0
-      L += wgt * ml[s].y;
-      acc.x += wgt * v[s].x; acc.y += wgt * v[s].y; acc.z += wgt * v[s].z; acc.w += wgt * v[s].w;
+      // explicit fmaf: the fused merge + value projection below rounds identically
+      L = fmaf(wgt, ml[s].y, L);
+      acc.x = fmaf(wgt, v[s].x, acc.x); acc.y = fmaf(wgt, v[s].y, acc.y);
+      acc.z = fmaf(wgt, v[s].z, acc.z); acc.w = fmaf(wgt, v[s].w, acc.w);
     }
   }
   if (e >= D) return;
   const float il = 1.0f / L;
   half4 o = {(_Float16)(acc.x * il), (_Float16)(acc.y * il), (_Float16)(acc.z * il), (_Float16)(acc.w * il)};
   *reinterpret_cast<half4*>(out + (int64_t)b * HD + (int64_t)h * D + e) = o;
+}
+
+// Split merge + per-head value projection in ONE launch: block = (head h, 4 rows); phase
+// 1 merges the rows' split partials of head h (xattn_combine_wide_kernel's arithmetic) into
+// an fp16 LDS tile, phase 2 is the block-diagonal projection o[r][64h + j] = c[r][h] .
+// Wv[64h + j]^T + bv (gemm_skinny_kernel's arithmetic: 16 waves, one 32-deep k-step each,
+// partials summed as (p_0 + p_8) + ... + (p_7 + p_15)) — bit-identical to the two launches
+// it replaces. Each block reads its rows' partials once (4 x nsplit x D fp32) and the
+// head's 64 x D weight slice.
+constexpr int kCvpRows = 4;
+template <int D>
+__global__ __launch_bounds__(1024) void xattn_combine_vproj_kernel(
+    const float* __restrict__ part_c, const float* __restrict__ part_ml, int nsplit, int H, int B,
+    const _Float16* __restrict__ wv, const float* __restrict__ bv, _Float16* __restrict__ out,
+    int64_t ldo) {
+  constexpr int AP = frag_pitch(D);
+  constexpr int KS = D / 32;  // k-steps (<= 16: one per wave)
+  static_assert(KS <= 16, "D <= 512");
+  __shared__ __attribute__((aligned(16))) _Float16 sA[16 * AP];
+  __shared__ float red[4][8][16][17];
+  const int h = blockIdx.x, r0 = blockIdx.y * kCvpRows;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int HD = H * D;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  // weight fragments of this wave's k-step for the head's 4 column tiles: in flight first
+  half8 bw[4];
+  const bool kok = w < KS;  // wave-uniform
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const _Float16* wr = wv + (int64_t)(h * 64 + 16 * t + lr) * D + 32 * w + kc8;
+    bw[t] = kok ? *reinterpret_cast<const half8*>(wr) : zero_half8();
+  }
+  const int ecol = tid & 63, erow = tid >> 6;  // epilogue: rows < kCvpRows, 64 columns
+  const float e_add = (erow < kCvpRows && bv) ? bv[h * 64 + ecol] : 0.0f;
+  // phase 1: merge, 2 dims per thread (rows r0 + tid / (D/2))
+  for (int i = tid; i < 16 * (D / 2); i += 1024) {
+    const int rr = i / (D / 2), e = (i % (D / 2)) * 2;
+    const int b = r0 + rr;
+    half2v o = {(_Float16)0.0f, (_Float16)0.0f};
+    if (rr < kCvpRows && b < B) {
+      const float* pml = part_ml + (int64_t)b * nsplit * H * 2;
+      const float* pc = part_c + (int64_t)b * nsplit * HD + (int64_t)h * D + e;
+      float2 ml[kXCombMax], v[kXCombMax];
+#pragma unroll
+      for (int s = 0; s < kXCombMax; ++s) {
+        if (s < nsplit) {
+          ml[s] = *reinterpret_cast<const float2*>(pml + ((int64_t)s * H + h) * 2);
+          v[s] = *reinterpret_cast<const float2*>(pc + (int64_t)s * HD);
+        }
+      }
+      float M = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < kXCombMax; ++s)
+        if (s < nsplit) M = fmaxf(M, ml[s].x);
+      float L = 0.f, a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int s = 0; s < kXCombMax; ++s) {
+        if (s < nsplit) {
+          const float wgt = exp2f(ml[s].x - M);
+          L = fmaf(wgt, ml[s].y, L);
+          a0 = fmaf(wgt, v[s].x, a0);
+          a1 = fmaf(wgt, v[s].y, a1);
+        }
+      }
+      const float il = 1.0f / L;
+      o = half2v{(_Float16)(a0 * il), (_Float16)(a1 * il)};
+    }
+    *reinterpret_cast<half2v*>(sA + rr * AP + e) = o;
+  }
+  __syncthreads();
+  // phase 2: one k-step per wave, four column tiles
+  f32x4 acc[4];
+  {
+    const half8 af = kok ? *reinterpret_cast<const half8*>(sA + lr * AP + 32 * w + kc8) : zero_half8();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bw[t], zero_f32x4());
+  }
+  if (w < 8) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[t][w][4 * (lane >> 4) + r][lr] = acc[t][r];
+  }
+  __syncthreads();
+  if (w >= 8) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[t][w - 8][4 * (lane >> 4) + r][lr] += acc[t][r];
+  }
+  __syncthreads();
+  if (erow < kCvpRows && r0 + erow < B) {
+    const int t = ecol >> 4, c = ecol & 15;
+    float v = e_add;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[t][i][erow][c];
+    out[(int64_t)(r0 + erow) * ldo + h * 64 + ecol] = (_Float16)v;
+  }
+}
+
+bool xattn_cvp_supported(int D, int H) { return H * 64 == D && (D == 384 || D == 512); }
+
+void xattn_combine_vproj_launch(const float* part_c, const float* part_ml, int nsplit, int B, int H,
+                                int D, const _Float16* wv, const float* bv, _Float16* out, int64_t ldo,
+                                hipStream_t s) {
+  JANUS_CHECK(xattn_cvp_supported(D, H), "xattn combine+vproj: D = 64 H in {384, 512}");
+  JANUS_CHECK(nsplit >= 1 && nsplit <= kXCombMax, "xattn combine+vproj: 1..16 key splits");
+  if (B <= 0) return;
+  const dim3 grid(H, (B + kCvpRows - 1) / kCvpRows);
+  if (D == 512)
+    xattn_combine_vproj_kernel<512><<<grid, 1024, 0, s>>>(part_c, part_ml, nsplit, H, B, wv, bv, out, ldo);
+  else
+    xattn_combine_vproj_kernel<384><<<grid, 1024, 0, s>>>(part_c, part_ml, nsplit, H, B, wv, bv, out, ldo);
+  JANUS_LAUNCH_CHECK();
 }
 
 int xattn_split_count(int Te, int requested) {
@@ -349,7 +465,8 @@ bool xattn_supported(int D, int H) {
 }
 
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
-                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s) {
+                  int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
+                  bool combine) {
   JANUS_CHECK(xattn_supported(D, H), "xattn: need D = 64 H in {384, 512, 768}");
   if (B <= 0 || Te <= 0) return;
   JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
@@ -364,6 +481,7 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   } else {
     xattn_cfg<768, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
   }
+  if (!combine) return;  // the caller merges (xattn_combine_vproj_launch)
   if (nsplit <= kXCombMax && D <= 512)
     xattn_combine_wide_kernel<<<dim3(H, B), 128, 0, s>>>(part_c, part_ml, nsplit, H, D, out);
   else

@@ -199,3 +199,22 @@ def test_seek_loop_matches_oracle(engine, gpu):
         assert [g[2] for g in got] == [r[2] for r in ref]
         assert np.allclose([g[:2] for g in got], [r[:2] for r in ref])
         print(f"seek loop: {st.windows} windows, {len(got)} segments, {st.fallbacks} flagged for fallback")
+
+
+@pytest.mark.parametrize("which", ["tiny", "base"])
+def test_fused_xattn_merge_vproj_bit_identical(engine, base_engine, gpu, monkeypatch, which):
+    """The cross-attention split merge fused with the per-head value projection
+    (xattn_combine_vproj_kernel, default) decodes bit-identically to the two launches it
+    replaces (JANUS_NO_CVP): same tokens, same summed log-probabilities."""
+    eng, _ = engine if which == "tiny" else base_engine
+    utts = [synth_speech(80 + k, 4.0 + 2 * k) for k in range(6)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    monkeypatch.setenv("JANUS_NO_CVP", "1")
+    t1, n1, s1 = eng.decode(enc, 48)
+    t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
+    monkeypatch.delenv("JANUS_NO_CVP")
+    t2, n2, s2 = eng.decode(enc, 48)
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
+    assert torch.equal(s1, s2.cpu())
