@@ -74,6 +74,12 @@ void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules&
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
                             float* sum_lp, int32_t* n_tok, int B, hipStream_t s,
                             const int32_t* plen = nullptr, float* nsp = nullptr);
+// select_partials_launch at pos followed by embed_launch at pos + 1, in one launch
+void select_embed_launch(const LogitPart* parts, int nblk, const DecodeRules& R, RowRules* rules,
+                         int32_t* tokens, int ld, int pos, int32_t* done, float* sum_lp,
+                         int32_t* n_tok, int B, hipStream_t s, const int32_t* plen, float* nsp,
+                         const _Float16* tok_emb, const float* pos_emb, int d, float* x,
+                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out);
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s);
 
 }  // namespace janus

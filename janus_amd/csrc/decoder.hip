@@ -55,18 +55,15 @@ __device__ __forceinline__ float2 ln_piece8x2(float v0, float v1) {
   return make_float2(s, q);
 }
 
-__global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__ tok_emb,
-                                                    const float* __restrict__ pos_emb,
-                                                    const int32_t* __restrict__ tokens,
-                                                    int ld_tokens, int pos, int d,
-                                                    float* __restrict__ x,
-                                                    float2* __restrict__ part,
-                                                    const float* __restrict__ ln_g,
-                                                    const float* __restrict__ ln_b,
-                                                    _Float16* __restrict__ ln_out) {
+// row b's embedding at position pos (token tok) -> x[b] (+ LayerNorm pieces / the first
+// layer's LayerNorm of the row); 256 threads
+__device__ __forceinline__ void embed_row(const _Float16* __restrict__ tok_emb,
+                                          const float* __restrict__ pos_emb, int tok, int b,
+                                          int pos, int d, float* __restrict__ x,
+                                          float2* __restrict__ part, const float* __restrict__ ln_g,
+                                          const float* __restrict__ ln_b,
+                                          _Float16* __restrict__ ln_out) {
   __shared__ float red[2][4];
-  const int b = blockIdx.x;
-  const int tok = tokens[(int64_t)b * ld_tokens + pos];
   float v0 = 0.f, v1 = 0.f;
   for (int base = 0; base < d; base += 512) {
     const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece
@@ -99,6 +96,20 @@ __global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__
       ln_out[(int64_t)b * d + col + 1] = (_Float16)((v1 - mean) * rstd * ln_g[col + 1] + ln_b[col + 1]);
     }
   }
+}
+
+__global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__ tok_emb,
+                                                    const float* __restrict__ pos_emb,
+                                                    const int32_t* __restrict__ tokens,
+                                                    int ld_tokens, int pos, int d,
+                                                    float* __restrict__ x,
+                                                    float2* __restrict__ part,
+                                                    const float* __restrict__ ln_g,
+                                                    const float* __restrict__ ln_b,
+                                                    _Float16* __restrict__ ln_out) {
+  const int b = blockIdx.x;
+  embed_row(tok_emb, pos_emb, tokens[(int64_t)b * ld_tokens + pos], b, pos, d, x, part, ln_g, ln_b,
+            ln_out);
 }
 
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
@@ -635,8 +646,10 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
 
 // One block per row: reduce the partials, apply the timestamp-probability rule, pick
 // the token, accumulate its log-probability and derive the next step's row rules.
-__global__ __launch_bounds__(256) void select_partials_kernel(
-    const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
+// Row b's selection at position pos; returns (in thread 0) the row's token at pos + 1:
+// the selected one, eot for a finished row, the forced one inside the row's prompt.
+__device__ __forceinline__ int select_row(
+    const LogitPart* __restrict__ parts, int nblk, const DecodeRules& R, RowRules* __restrict__ rules,
     int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
     float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
     float* __restrict__ nsp) {
@@ -644,10 +657,10 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   int32_t* row_tok = tokens + (int64_t)b * ld;
   const int pl = plen ? plen[b] : 1;
-  if (pos + 1 < pl) return;  // still inside this row's prompt: the forced token stays
+  if (pos + 1 < pl) return row_tok[pos + 1];  // inside this row's prompt: the forced token stays
   if (done[b]) {
     if (tid == 0) row_tok[pos + 1] = R.eot;
-    return;
+    return R.eot;
   }
   float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
   float ba_v = -INFINITY, bt_v = -INFINITY;
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     sh[w] = p;
   }
   __syncthreads();
-  if (tid != 0) return;
+  if (tid != 0) return -1;
   for (int k = 1; k < 4; ++k) {
     const LogitPart& p = sh[k];
     float mo;
@@ -727,6 +740,44 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
   if (last_ts) r.last_stamp = next;
   r.ts_floor = r.last_stamp >= 0 ? ((last_ts && !pen_ts) ? r.last_stamp : r.last_stamp + 1) : -1;
   rules[b] = r;
+  return next;
+}
+
+__global__ __launch_bounds__(256) void select_partials_kernel(
+    const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
+    int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
+    float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
+    float* __restrict__ nsp) {
+  (void)select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp);
+}
+
+// The selection at position pos and the embedding of the chosen token at pos + 1 in one
+// launch (both are per row: one block per utterance): one launch per position fewer.
+// Bit-identical to select_partials_kernel followed by embed_kernel at pos + 1.
+__global__ __launch_bounds__(256) void select_embed_kernel(
+    const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
+    int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
+    float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
+    float* __restrict__ nsp, const _Float16* __restrict__ tok_emb, const float* __restrict__ pos_emb,
+    int d, float* __restrict__ x, float2* __restrict__ part, const float* __restrict__ ln_g,
+    const float* __restrict__ ln_b, _Float16* __restrict__ ln_out) {
+  __shared__ int s_tok;
+  const int t = select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp);
+  if (threadIdx.x == 0) s_tok = t;
+  __syncthreads();
+  embed_row(tok_emb, pos_emb, s_tok, blockIdx.x, pos + 1, d, x, part, ln_g, ln_b, ln_out);
+}
+
+void select_embed_launch(const LogitPart* parts, int nblk, const DecodeRules& R, RowRules* rules,
+                         int32_t* tokens, int ld, int pos, int32_t* done, float* sum_lp,
+                         int32_t* n_tok, int B, hipStream_t s, const int32_t* plen, float* nsp,
+                         const _Float16* tok_emb, const float* pos_emb, int d, float* x,
+                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out) {
+  JANUS_CHECK(d % 16 == 0, "embed: d % 16 != 0");
+  JANUS_CHECK(!ln_out || d <= 512, "embed: fused LayerNorm needs d <= 512");
+  select_embed_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok,
+                                        plen, nsp, tok_emb, pos_emb, d, x, part, ln_g, ln_b, ln_out);
+  JANUS_LAUNCH_CHECK();
 }
 
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,

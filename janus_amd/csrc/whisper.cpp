@@ -481,10 +481,15 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     p.M = B; p.N = d; p.K = d;
     resid_ln_launch(p, s);
   };
+  // the selection at pos and the embedding at pos + 1 in one launch (select_embed_kernel,
+  // bit-identical; JANUS_NO_SEL_EMBED restores the two launches): a step from the first
+  // sampled position on finds its row already embedded by the previous step's selection
+  const bool fuse_se = std::getenv("JANUS_NO_SEL_EMBED") == nullptr;
   auto step = [&](int pos) {
-    embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
-                 fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
-                 (ln_fuse || embed_ln) ? a : nullptr);
+    if (!(fuse_se && pos >= sample_begin && pos > 0))
+      embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
+                   fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
+                   (ln_fuse || embed_ln) ? a : nullptr);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = Z.d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
@@ -570,9 +575,16 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
                           lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap);
-    select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
-                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
-                           Z.d_nsp.as<float>());
+    if (fuse_se && pos + 1 < maxlen - 1)
+      select_embed_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
+                          maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
+                          Z.d_nsp.as<float>(), w->tok16.as<_Float16>(), pos_emb, d, x,
+                          fused_ln ? lnp : nullptr, w->dec[0].ln1g, w->dec[0].ln1b,
+                          (ln_fuse || embed_ln) ? a : nullptr);
+    else
+      select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
+                             maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
+                             Z.d_nsp.as<float>());
   };
   const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
   const int chunk = opt->check_every > 0 ? opt->check_every : 16;
@@ -581,7 +593,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       B, maxlen, sample_begin, chunk, (int64_t)x, (int64_t)a, (int64_t)qkv, (int64_t)o,
       (int64_t)q2, (int64_t)f, (int64_t)Z.d_kc.p, (int64_t)Z.d_vc.p, (int64_t)Z.d_ck.p,
       (int64_t)Z.d_cv.p, (int64_t)part_o, (int64_t)part_ml, (int64_t)Z.d_parts.p,
-      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)cvp, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
+      (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)cvp, (int64_t)fuse_se, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};

@@ -218,3 +218,20 @@ def test_fused_xattn_merge_vproj_bit_identical(engine, base_engine, gpu, monkeyp
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
     assert torch.equal(s1, s2.cpu())
+
+
+def test_fused_select_embed_bit_identical(base_engine, gpu, monkeypatch):
+    """The token selection at position p fused with the embedding of the chosen token at
+    p + 1 (select_embed_kernel, default) decodes bit-identically to the two launches
+    (JANUS_NO_SEL_EMBED), including rows that finish early and the last position."""
+    eng, _ = base_engine
+    utts = [synth_speech(90 + k, 3.0 + 3 * k) for k in range(5)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    monkeypatch.setenv("JANUS_NO_SEL_EMBED", "1")
+    t1, n1, s1 = eng.decode(enc, 37, check_every=8)
+    t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
+    monkeypatch.delenv("JANUS_NO_SEL_EMBED")
+    t2, n2, s2 = eng.decode(enc, 37, check_every=8)
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
