@@ -450,8 +450,13 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
 // per CU (the decoder's 4096-wide absorbed query projection), one block per CU with half
 // the A re-reads of the 16-column form. Bit-identical to gemm_skinny_kernel<EPI_F16,
 // AM_F16, 4, K1> (same single-k-step MFMA per wave, same reduction order).
+// LNX: A = LayerNorm(x) of all 64 rows computed in the block's prologue into an fp16 LDS
+// tile (ln_rows_wave: layernorm_kernel's arithmetic, so bit-identical to a LayerNorm launch
+// followed by the plain form).
+template <bool LNX>
 __global__ __launch_bounds__(1024) void gemm_skinny2_kernel(SkinnyArgs p) {
   __shared__ float red[2][8][64][17];
+  extern __shared__ __attribute__((aligned(16))) _Float16 s2_smem[];  // LNX: [64][AP]
   const int M = p.M, N = p.N, K = p.K;
   const int col0 = blockIdx.x * 32;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
@@ -466,11 +471,21 @@ __global__ __launch_bounds__(1024) void gemm_skinny2_kernel(SkinnyArgs p) {
     bw[t] = (kok && bcol < N) ? *reinterpret_cast<const half8*>(wrow + kbeg + kc8) : zero_half8();
   }
   half8 ah[4];
+  if constexpr (LNX) {
+    const int AP = frag_pitch(K);
+    // wave w normalises rows w + 16j (j < 4), all loads in one round trip
+    ln_rows_wave<2, 4>(p.x, p.ldx, w, kSkWaves, M, p.lnin_g, p.lnin_b, s2_smem, w, AP, K, p.eps, lane);
+    __syncthreads();
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int r = m * 16 + lr;
-    ah[m] = (kok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kbeg + kc8)
-                           : zero_half8();
+    for (int m = 0; m < 4; ++m)
+      ah[m] = kok ? *reinterpret_cast<const half8*>(s2_smem + (m * 16 + lr) * AP + kbeg + kc8) : zero_half8();
+  } else {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int r = m * 16 + lr;
+      ah[m] = (kok && r < M) ? *reinterpret_cast<const half8*>(p.A + (int64_t)r * p.lda + kbeg + kc8)
+                             : zero_half8();
+    }
   }
   const int elr = tid >> 4, ec = tid & 15;
   float e_add[2];
@@ -556,9 +571,20 @@ static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
   // plain fp16 outputs wider than 2048 columns (more 16-column tiles than a 128-CU
   // partition holds in one round) at K <= 512: 32 columns per block
   static const bool nct2 = std::getenv("JANUS_SKINNY_NO_NCT2") == nullptr;
-  if constexpr (AM == AM_F16) {
+  if constexpr (AM == AM_F16 || AM == AM_LNX) {
     if (nct2 && epi == EPI_F16 && p.N > 2048 && p.K <= kSkWaves * 32 && p.a_group_cols == 0 && p.M <= 64) {
-      gemm_skinny2_kernel<<<(p.N + 31) / 32, 1024, 0, s>>>(p);
+      if constexpr (AM == AM_LNX) {
+        auto kern = gemm_skinny2_kernel<true>;
+        static bool attr = false;
+        if (!attr) {
+          JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        88 * 1024));
+          attr = true;
+        }
+        kern<<<(p.N + 31) / 32, 1024, (size_t)64 * frag_pitch(p.K) * 2, s>>>(p);
+      } else {
+        gemm_skinny2_kernel<false><<<(p.N + 31) / 32, 1024, 0, s>>>(p);
+      }
       JANUS_LAUNCH_CHECK();
       return;
     }

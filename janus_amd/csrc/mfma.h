@@ -228,20 +228,17 @@ __device__ __forceinline__ void ln_rows_wave(const float* x, int64_t ldx, int ro
       if (lane + 64 * k >= nv) v[j][k] = z;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
+    // layernorm_kernel's arithmetic (ln_sum4 / ln_sq4 / ln_norm4): a LayerNorm in a GEMM
+    // prologue rounds exactly as the separate LayerNorm launch it replaces
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) s += (v[j][k].x + v[j][k].y) + (v[j][k].z + v[j][k].w);
+    for (int k = 0; k < MAXV; ++k) s += ln_sum4(v[j][k]);
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     const float mean = s / d;
     float q = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      if (lane + 64 * k < nv) {
-        const float a0 = v[j][k].x - mean, a1 = v[j][k].y - mean, a2 = v[j][k].z - mean,
-                    a3 = v[j][k].w - mean;
-        q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-      }
-    }
+    for (int k = 0; k < MAXV; ++k)
+      if (lane + 64 * k < nv) q += ln_sq4(v[j][k], mean);
     for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
     const float rstd = rsqrtf(q / d + eps);
     const bool rok = row0 + j * rstep < nrows;
@@ -250,10 +247,7 @@ __device__ __forceinline__ void ln_rows_wave(const float* x, int64_t ldx, int ro
     for (int k = 0; k < MAXV; ++k) {
       const int i = lane + 64 * k;
       if (i < nv) {
-        half4 h = {(_Float16)((v[j][k].x - mean) * rstd * gg[k].x + bb[k].x),
-                   (_Float16)((v[j][k].y - mean) * rstd * gg[k].y + bb[k].y),
-                   (_Float16)((v[j][k].z - mean) * rstd * gg[k].z + bb[k].z),
-                   (_Float16)((v[j][k].w - mean) * rstd * gg[k].w + bb[k].w)};
+        half4 h = ln_norm4(v[j][k], mean, rstd, gg[k], bb[k]);
         if (!rok) h = half4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
         *reinterpret_cast<half4*>(orow + 4 * i) = h;
       }

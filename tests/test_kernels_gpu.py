@@ -309,3 +309,28 @@ def test_resid_ln_matches_two_launches(gpu, M, d):
     assert rel_err(x2, ref_x) < 1e-6
     ref = F.layer_norm(ref_x, (d,), gam.double(), bet.double(), 1e-5)
     assert rel_err(out2, ref) < 1e-3
+
+
+@pytest.mark.parametrize("M,N", [(64, 4096), (64, 1536), (37, 2304)])
+def test_gemm_layernorm_prologue_bit_identical(gpu, M, N):
+    """A LayerNorm in the GEMM prologue (janus_gemm_ln_f16, the decoder's pre-LN
+    projections) rounds exactly as the LayerNorm launch followed by the plain GEMM."""
+    K = 512
+    g = torch.Generator().manual_seed(M * 3 + N)
+    x = torch.randn(M, K, generator=g) * 2.0 + 0.5
+    gam = torch.randn(K, generator=g) * 0.2 + 1.0
+    bet = torch.randn(K, generator=g) * 0.1
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).half()
+    bias = torch.randn(N, generator=g) * 0.1
+    dx, dg, db, dW, dbias = x.to(gpu), gam.to(gpu), bet.to(gpu), W.to(gpu), bias.to(gpu)
+    out1 = torch.empty(M, N, dtype=torch.float16, device=gpu)
+    nat.call("janus_gemm_ln_f16", 0, dx.data_ptr(), K, dg.data_ptr(), db.data_ptr(), 1e-5,
+             dW.data_ptr(), K, dbias.data_ptr(), out1.data_ptr(), N, M, N, K, stream())
+    a = torch.empty(M, K, dtype=torch.float16, device=gpu)
+    nat.call("janus_layernorm_f16", dx.data_ptr(), dg.data_ptr(), db.data_ptr(), a.data_ptr(), M, K,
+             1e-5, stream())
+    out2 = torch.empty(M, N, dtype=torch.float16, device=gpu)
+    nat.call("janus_gemm_f16", 0, a.data_ptr(), K, dW.data_ptr(), K, dbias.data_ptr(), out2.data_ptr(), N,
+             None, N, M, N, K, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
