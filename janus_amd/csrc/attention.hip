@@ -292,10 +292,16 @@ __global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __res
           pb[n >> 1][4 * (n & 1) + r] = (_Float16)pv_;
         }
       lq[qg] = lq[qg] * alpha + ls;
+      // once no query's running maximum moved (alpha == 1 exactly in every lane, the
+      // common case after the first tiles) the rescale is a multiply by 1: skipped
+      if (!__all(alpha == 1.0f)) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[qg][m][r] *= alpha;
+      }
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[qg][m][r] *= alpha;
         o[qg][m] = mfma16(va[m][0], pb[0], o[qg][m]);
         o[qg][m] = mfma16(va[m][1], pb[1], o[qg][m]);
       }
