@@ -27,6 +27,7 @@
 // tile, far below the L2's rate at the MFMA pace).
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include "mfma.h"
 #include "kernels.h"
@@ -61,6 +62,13 @@ template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4,
 // ring depth 2 (the default, JANUS_WIDE128_CFG=2): 16 fewer VGPRs, three blocks per CU
 template <> struct WideCfg<128, 2> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 2, NP = 2; static constexpr bool EPF = false; };
 template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN = 4, NPB = 4, NP = 1; static constexpr bool EPF = false; };
+// C = 256 on the register ring (JANUS_WIDE256_CFG=ring): 8 waves x 32 columns over all
+// m-tiles, weights from L2 into registers. Per block k-step: A-fragment LDS reads 64 KB
+// (512 clocks at 128 B/clock), weight fragments 16 KB over the L1 path (256 clocks), MFMA
+// 512 clocks per SIMD — against the LDS-staged form's 80 KB of LDS traffic (640 clocks).
+template <> struct WideCfg<256, 3> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 2, NP = 2; static constexpr bool EPF = false; };
+// the same with the weight ring 4 deep (the default; one block per CU either way)
+template <> struct WideCfg<256, 4> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 4, NP = 2; static constexpr bool EPF = false; };
 
 template <int C, int V = 0>
 struct WideGeo {
@@ -82,6 +90,8 @@ struct WideGeo {
   static constexpr int RP = 16 * WM * ((MW2 + NP - 1) / NP);  // rows per epilogue pass
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
   static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)RP * ES * 4);
+  // blocks per CU the register budget is sized for (C = 256: one 8-wave block, 256 VGPRs)
+  static constexpr int MINB = C == 256 ? 1 : 2;
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
 };
 
@@ -154,7 +164,7 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
 }
 
 template <int C, int V>
-__global__ __launch_bounds__((WideGeo<C, V>::NT), 2) void resunit_wide_kernel(ResUnitArgs a,
+__global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void resunit_wide_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt) {
   using G = WideGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, NT = G::NT, LI = G::LI;
@@ -648,7 +658,14 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
     else wide_cfg<128, 2>(a, s);
   }
   else if (a.C == 256) {
-    if (w256 == 16) epf ? lds_cfg<256, true, 1>(a, s) : lds_cfg<256, false, 1>(a, s);
+    // JANUS_WIDE256_CFG: ring4 (default: weights from L2 into a per-wave register ring 4
+    // deep, 8 waves x 32 columns; standalone 64 x 30 s, C = 256 units 27.0 -> 22.3 ms;
+    // overlapped step, vocoder side 289 -> 282 ms), ring (2 deep: 22.8 ms), lds (weights
+    // staged through LDS, the r01 form)
+    static const std::string c256 = std::getenv("JANUS_WIDE256_CFG") ? std::getenv("JANUS_WIDE256_CFG") : "ring4";
+    if (c256 == "ring") wide_cfg<256, 3>(a, s);
+    else if (c256 == "ring4") wide_cfg<256, 4>(a, s);
+    else if (w256 == 16) epf ? lds_cfg<256, true, 1>(a, s) : lds_cfg<256, false, 1>(a, s);
     else epf ? lds_cfg<256, true, 0>(a, s) : lds_cfg<256, false, 0>(a, s);
   }
   else throw Error("resunit (wide): C must be 64, 128 or 256");
