@@ -67,6 +67,12 @@ template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN =
 // (512 clocks at 128 B/clock), weight fragments 16 KB over the L1 path (256 clocks), MFMA
 // 512 clocks per SIMD — against the LDS-staged form's 80 KB of LDS traffic (640 clocks).
 template <> struct WideCfg<256, 3> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 2, NP = 2; static constexpr bool EPF = false; };
+// C = 64 on the register ring (JANUS_WIDE64_CFG=ring): 2 x 2 waves of 32 columns x 6
+// m-tiles; per block k-step A-fragment LDS reads 24 KB and weight fragments 8 KB from L2
+// (three blocks per CU: 576 / 384 clocks against 576 of MFMA), where the LDS-staged form
+// moves 32 KB through LDS (768 clocks). Measured slower all the same (standalone 64 x 30 s,
+// C = 64 units 30.9-31.1 vs 30.2 ms): kept as an A/B switch.
+template <> struct WideCfg<64, 5> { static constexpr int BM = 176, WM = 2, WN = 2, NPB = 2, NP = 1; static constexpr bool EPF = false; };
 // the same with the weight ring 4 deep (the default; one block per CU either way)
 template <> struct WideCfg<256, 4> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 4, NP = 2; static constexpr bool EPF = false; };
 
@@ -91,7 +97,7 @@ struct WideGeo {
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
   static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)RP * ES * 4);
   // blocks per CU the register budget is sized for (C = 256: one 8-wave block, 256 VGPRs)
-  static constexpr int MINB = C == 256 ? 1 : 2;
+  static constexpr int MINB = C == 256 ? 1 : (C == 64 ? 3 : 2);
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
 };
 
@@ -645,7 +651,9 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
   static const int w64 = std::getenv("JANUS_WIDE64_WAVES") ? std::atoi(std::getenv("JANUS_WIDE64_WAVES")) : 4;
   static const int w256 = std::getenv("JANUS_WIDE256_WAVES") ? std::atoi(std::getenv("JANUS_WIDE256_WAVES")) : 8;
   if (a.C == 64) {
-    if (w64 == 8) epf ? lds_cfg<64, true, 1>(a, s) : lds_cfg<64, false, 1>(a, s);
+    static const bool ring64 = std::getenv("JANUS_WIDE64_CFG") && std::string(std::getenv("JANUS_WIDE64_CFG")) == "ring";
+    if (ring64) wide_cfg<64, 5>(a, s);
+    else if (w64 == 8) epf ? lds_cfg<64, true, 1>(a, s) : lds_cfg<64, false, 1>(a, s);
     else epf ? lds_cfg<64, true, 0>(a, s) : lds_cfg<64, false, 0>(a, s);
   }
   else if (a.C == 128) {
