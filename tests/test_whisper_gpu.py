@@ -235,3 +235,22 @@ def test_fused_select_embed_bit_identical(base_engine, gpu, monkeypatch):
     t2, n2, s2 = eng.decode(enc, 37, check_every=8)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
+
+
+@pytest.mark.parametrize("env", [("JANUS_RESID_LN", "1"), ("JANUS_LN_PROLOGUE", "15"), ("JANUS_LN_PROLOGUE", "0")])
+def test_layernorm_placements_bit_identical(base_engine, gpu, monkeypatch, env):
+    """Every LayerNorm placement rounds alike (mfma.h ln_sum4 / ln_sq4 / ln_norm4): the
+    separate launch (mask 0), the GEMM prologues (mask 15: LN1 -> QKV, LN2 -> absorbed query
+    projection, LN3 -> fc1, final -> vocabulary projection), the whole-row residual
+    projection + LayerNorm kernel (JANUS_RESID_LN) and the default (mask 9) decode the same
+    tokens with the same summed log-probabilities."""
+    eng, _ = base_engine
+    utts = [synth_speech(120 + k, 3.0 + 2 * k) for k in range(4)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    t1, n1, s1 = eng.decode(enc, 40)
+    t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
+    monkeypatch.setenv(*env)
+    t2, n2, s2 = eng.decode(enc, 40)
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
