@@ -356,9 +356,15 @@ static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
+#ifndef JANUS_NARROW16_BM
+#define JANUS_NARROW16_BM 240
+#endif
+#ifndef JANUS_NARROW32_BM
+#define JANUS_NARROW32_BM 240
+#endif
 template <int C, int K, int NW>
 static void narrow_dw(const ResUnitArgs& a, hipStream_t s) {
-  constexpr int BM = 240;
+  constexpr int BM = C == 16 ? JANUS_NARROW16_BM : JANUS_NARROW32_BM;  // output rows per tile
   if (a.d == 1) narrow_cfg<C, K, 1, BM, NW>(a, s);
   else if (a.d == 3) narrow_cfg<C, K, 3, BM, NW>(a, s);
   else if (a.d == 5) narrow_cfg<C, K, 5, BM, NW>(a, s);
@@ -373,7 +379,8 @@ template <int C, int K>
 static void narrow_d(const ResUnitArgs& a, hipStream_t s) {
   static const int nw = std::getenv("JANUS_NARROW_WAVES") ? std::atoi(std::getenv("JANUS_NARROW_WAVES"))
                                                           : (C == 32 ? 8 : 4);
-  if (nw == 8) narrow_dw<C, K, 8>(a, s);
+  if constexpr (C == 16 && JANUS_NARROW16_BM != 240) narrow_dw<C, K, 4>(a, s);  // BM A/B builds
+  else if (nw == 8) narrow_dw<C, K, 8>(a, s);
   else narrow_dw<C, K, 4>(a, s);
 }
 
