@@ -7,6 +7,7 @@
 // in so P·V reads 16-byte B fragments); P goes through a per-wave LDS tile to become
 // the A operand. The S = QK^T score matrix is never materialised in HBM.
 #include <cstdlib>
+#include <type_traits>
 #include "mfma.h"
 #include "kernels.h"
 
@@ -166,19 +167,30 @@ constexpr int kSKT = 64;            // keys per tile
 constexpr int kSLK = kHd + 8;       // sK pitch (halves): 36 dwords, conflict-free 16-B reads
 constexpr int kSLV = kSKT + 8;      // sVt pitch (halves): 36 dwords
 
-__global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __restrict__ qkv,
+// Grid: one block per (query block, head, utterance), flattened; with remap the blocks
+// that share one (utterance, head) — and so read the same 384 KB of keys and values — run
+// on one XCD (xcd_remap gives each XCD a contiguous run of work items), so those rows are
+// fetched into one L2 instead of into every XCD's.
+// JANUS_ATTN_MINB: blocks per CU the register budget is sized for (3: 168 VGPRs, no
+// spills; left free the kernel takes 174 and runs 2 blocks per CU; 4 spills)
+#ifndef JANUS_ATTN_MINB
+#define JANUS_ATTN_MINB 3
+#endif
+__global__ __launch_bounds__(256, JANUS_ATTN_MINB) void attention_st_kernel(const _Float16* __restrict__ qkv,
                                                            _Float16* __restrict__ out, int T,
-                                                           int H, float scale_log2) {
+                                                           int H, float scale_log2, int nqb,
+                                                           int remap) {
   __shared__ __attribute__((aligned(16))) _Float16 sK[2][kSKT * kSLK];
   __shared__ __attribute__((aligned(16))) _Float16 sVt[2][kHd * kSLV];
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  const int item = remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qblk = item % nqb, h = (item / nqb) % H, b = item / (nqb * H);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, lr = lane & 15;
   const int d = H * kHd;
   const int64_t ld = 3 * (int64_t)d;
   const _Float16* base = qkv + (int64_t)b * T * ld + h * kHd;
-  const int q0 = blockIdx.x * kSQB + w * kSQW;
+  const int q0 = qblk * kSQB + w * kSQW;
 
   // Q^T B fragments: query q0 + 16 qg + lr, dims 32 ks + 8 g .. +7
   half8 qb[2][2];
@@ -194,11 +206,13 @@ __global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __res
   // staging: thread -> (16-byte dim chunk sc, key pair kp); keys 2kp, 2kp + 1
   const int sc = tid >> 5, kp = tid & 31;
   uint4 pk[2], pv[2];
-  auto load_tile = [&](int k0) {
+  // GUARD: the tile may run past T (the last tile only; full tiles load unguarded)
+  auto load_tile = [&](int k0, auto guard_c) {
+    constexpr bool GUARD = decltype(guard_c)::value;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int kr = k0 + 2 * kp + e;
-      const bool ok = kr < T;
+      const bool ok = !GUARD || kr < T;
       const _Float16* rowp = base + (int64_t)(ok ? kr : 0) * ld + sc * 8;
       pk[e] = ok ? *reinterpret_cast<const uint4*>(rowp + d) : make_uint4(0, 0, 0, 0);
       pv[e] = ok ? *reinterpret_cast<const uint4*>(rowp + 2 * d) : make_uint4(0, 0, 0, 0);
@@ -225,12 +239,21 @@ __global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __res
   float mq[2] = {-INFINITY, -INFINITY}, lq[2] = {0.f, 0.f};
 
   const int ntiles = (T + kSKT - 1) / kSKT;
-  load_tile(0);
+  using False = std::false_type;
+  using True = std::true_type;
+  auto load_any = [&](int k0) {  // block-uniform choice
+    if (k0 + kSKT <= T) load_tile(k0, False{});
+    else load_tile(k0, True{});
+  };
+  load_any(0);
   store_tile(0);
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  // TAIL: the last, partial tile masks the keys past T (peeled, so the full tiles carry no
+  // per-key compares or selects)
+  auto tile_step = [&](int t, auto tail_c) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail_c)::value;
     const int buf = t & 1, k0 = t * kSKT;
-    if (t + 1 < ntiles) load_tile(k0 + kSKT);  // in flight during this tile
+    if (t + 1 < ntiles) load_any(k0 + kSKT);  // in flight during this tile
     const _Float16* K = sK[buf];
     const _Float16* Vt = sVt[buf];
 
@@ -258,8 +281,7 @@ __global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __res
         va[m][c] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 
-    const bool tail = k0 + kSKT > T;  // block-uniform: only the last tile masks keys
-    if (tail) {
+    if constexpr (TAIL) {
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
@@ -308,7 +330,10 @@ __global__ __launch_bounds__(256) void attention_st_kernel(const _Float16* __res
     }
     if (t + 1 < ntiles) store_tile(buf ^ 1);  // its readers finished before the last barrier
     __syncthreads();
-  }
+  };
+  for (int t = 0; t + 1 < ntiles; ++t) tile_step(t, False{});
+  if (ntiles * kSKT > T) tile_step(ntiles - 1, True{});
+  else tile_step(ntiles - 1, False{});
 
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
@@ -337,8 +362,13 @@ void attention_launch(const _Float16* qkv, _Float16* out, int B, int T, int H, f
     dim3 grid((T + kQT - 1) / kQT, H, B);
     attention_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
   } else {
-    dim3 grid((T + kSQB - 1) / kSQB, H, B);
-    attention_st_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
+    // JANUS_ATTN_NO_REMAP: dispatch order (blocks of one head spread over all XCDs)
+    static const int remap = std::getenv("JANUS_ATTN_NO_REMAP") ? 0 : 1;
+    const int nqb = (T + kSQB - 1) / kSQB;
+    const int64_t nblk = (int64_t)nqb * H * B;
+    JANUS_CHECK(nblk < (1ll << 31), "attention: grid too large");
+    attention_st_kernel<<<(unsigned)nblk, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f,
+                                                      nqb, remap);
   }
   JANUS_LAUNCH_CHECK();
 }
