@@ -33,16 +33,25 @@ __device__ __forceinline__ uint32_t ordered_key(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__global__ __launch_bounds__(256) void mel_kernel(const float* __restrict__ pcm,
+// LDS: the sample window (xs) and, once every wave is done with it, the power tile (ps) in
+// the same 53.8 KB, so three blocks fit per CU (the DFT's basis loads come from L2: the
+// other blocks' waves cover their latency)
+constexpr int kMelLds = (kXRows * kXRow > kFT * kPS) ? kXRows * kXRow : kFT * kPS;
+constexpr int kKG = 10;                      // DFT k-steps per basis prefetch group
+constexpr int kNG = kNfft / 4 / kKG;         // 10 groups
+static_assert(kNG * kKG * 4 == kNfft && kNG % 2 == 0, "basis prefetch groups");
+
+__global__ __launch_bounds__(256, 3) void mel_kernel(const float* __restrict__ pcm,
                                                   const int64_t* __restrict__ offsets,
                                                   const float* __restrict__ basis,
                                                   const float* __restrict__ filtT,
                                                   float* __restrict__ logmel,
                                                   uint32_t* __restrict__ maxkey, int n_frames_out,
                                                   int n_frames_max, int decim) {
-  __shared__ float xs[kXRows * kXRow];
-  __shared__ float ps[kFT * kPS];
+  __shared__ float smem[kMelLds];
   __shared__ float redmax[4];
+  float* xs = smem;  // [kXRows][kXRow] samples
+  float* ps = smem;  // [kFT][kPS] power, after the DFT
   const int b = blockIdx.y, f0 = blockIdx.x * kFT;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int64_t base = offsets[b];
@@ -59,32 +68,64 @@ __global__ __launch_bounds__(256) void mel_kernel(const float* __restrict__ pcm,
   }
   __syncthreads();
 
-  // DFT power: wave w owns bin tiles w, w+4, w+8 (and 12 for w == 0)
-  for (int bt = w; bt < kBinPad / 16; bt += 4) {
+  // DFT power: wave w owns bin tiles w, w+4, w+8 (and 12 for w == 0). The basis values
+  // of kKG k-steps are loaded a group ahead (two register sets), and the power values
+  // stay in registers until every wave is done with xs.
+  float pw[4][4][4];  // [tile j][m][r]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bt = w + 4 * j;
+    if (bt >= kBinPad / 16) break;  // wave-uniform
     f32x4 re[4], im[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) { re[m] = zero_f32x4(); im[m] = zero_f32x4(); }
     const int col = bt * 16 + (lane & 15);
-    for (int kk = 0; kk < kNfft / 4; ++kk) {
-      const int n = kk * 4 + (lane >> 4);
-      const float bc = basis[n * kNB + col];
-      const float bs = basis[n * kNB + kBinPad + col];
-      const int hr = n / kHop, hc = n % kHop;
+    const float* bp = basis + (lane >> 4) * kNB + col;  // basis row n = 4 kk + (lane >> 4)
+    float cA[kKG], sA[kKG], cB[kKG], sB[kKG];
+    auto ldg = [&](float (&c)[kKG], float (&sn)[kKG], int g) __attribute__((always_inline)) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int i = m * 16 + (lane & 15);
-        const float av = xs[(i + hr) * kXRow + hc];
-        re[m] = mfma_f32(av, bc, re[m]);
-        im[m] = mfma_f32(av, bs, im[m]);
+      for (int q = 0; q < kKG; ++q) {
+        const int kk = g * kKG + q;
+        c[q] = bp[kk * 4 * kNB];
+        sn[q] = bp[kk * 4 * kNB + kBinPad];
       }
+    };
+    auto run = [&](const float (&c)[kKG], const float (&sn)[kKG], int g) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < kKG; ++q) {
+        const int n = (g * kKG + q) * 4 + (lane >> 4);
+        const int hr = n / kHop, hc = n % kHop;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int i = m * 16 + (lane & 15);
+          const float av = xs[(i + hr) * kXRow + hc];
+          re[m] = mfma_f32(av, c[q], re[m]);
+          im[m] = mfma_f32(av, sn[q], im[m]);
+        }
+      }
+    };
+    ldg(cA, sA, 0);
+    for (int g = 0; g < kNG; g += 2) {
+      ldg(cB, sB, g + 1);
+      run(cA, sA, g);
+      if (g + 2 < kNG) ldg(cA, sA, g + 2);
+      run(cB, sB, g + 1);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int fr = m * 16 + 4 * (lane >> 4) + r;
-        ps[fr * kPS + col] = re[m][r] * re[m][r] + im[m][r] * im[m][r];
-      }
+      for (int r = 0; r < 4; ++r) pw[j][m][r] = re[m][r] * re[m][r] + im[m][r] * im[m][r];
+  }
+  __syncthreads();  // every wave is done with xs: ps over it
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bt = w + 4 * j;
+    if (bt >= kBinPad / 16) break;
+    const int col = bt * 16 + (lane & 15);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ps[(m * 16 + 4 * (lane >> 4) + r) * kPS + col] = pw[j][m][r];
   }
   __syncthreads();
 
