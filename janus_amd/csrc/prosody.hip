@@ -132,25 +132,26 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
     int found = 0x7fffffff;
     for (int chunk = 0; chunk < kYinLen / kTauChunk; ++chunk) {
       const int tau0 = chunk * kTauChunk + 2 * tid;
-      float acc0 = 0.f, acc1 = 0.f;
+      // the lane's two taus as one packed pair: v_pk_add_f32 / v_pk_mul_f32 do the two
+      // taus' sub, square and add in one instruction each (IEEE single ops, no
+      // contraction: this file builds with -ffp-contract=off), half the VALU issue of
+      // scalar code; the same per-tau j order as aubio
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      f32x2 acc = {0.f, 0.f};
 #pragma unroll 4
       for (int j = 0; j < kYinLen; j += 4) {
         const float4 a = *reinterpret_cast<const float4*>(&w[j]);
-        const float2 p0 = *reinterpret_cast<const float2*>(&w[j + tau0]);
-        const float2 p1 = *reinterpret_cast<const float2*>(&w[j + tau0 + 2]);
-        const float p2 = w[j + tau0 + 4];
         const float av[4] = {a.x, a.y, a.z, a.w};
-        const float bv[5] = {p0.x, p0.y, p1.x, p1.y, p2};
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          float t0 = __fsub_rn(av[jj], bv[jj + 0]);
-          float t1 = __fsub_rn(av[jj], bv[jj + 1]);
-          acc0 = __fadd_rn(acc0, __fmul_rn(t0, t0));
-          acc1 = __fadd_rn(acc1, __fmul_rn(t1, t1));
+          const f32x2 bv = {w[j + tau0 + jj], w[j + tau0 + jj + 1]};
+          const f32x2 aa = {av[jj], av[jj]};
+          const f32x2 t = aa - bv;
+          acc = acc + t * t;
         }
       }
-      dd[tau0 + 0] = acc0;
-      dd[tau0 + 1] = acc1;
+      dd[tau0 + 0] = acc.x;
+      dd[tau0 + 1] = acc.y;
       __syncthreads();
       // tmp2 += yin[tau] in tau order (pitchyin.c), one lane. 16 taus per batch through
       // 16-byte LDS reads / writes: the add chain stays sequential (bit-exact), but one LDS

@@ -212,15 +212,17 @@ class JanusPipeline:
                                       max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
-        # the YIN of the first B/8 utterances runs on the decoder side, after the decoder,
-        # to even out the two sides (JANUS_YIN_DEC_UTTS; 64 utterances, r02 v38: 2 / 6 / 8 /
+        # the YIN of the first JANUS_YIN_DEC_UTTS utterances can run on the decoder side,
+        # after the decoder, to even out the two sides (64 utterances, r02 v38: 2 / 6 / 8 /
         # 10 -> 316.7-317.1 / 314.5-315.2 / 313.6-314.3 / 315.2-315.7 ms per step; v40 with
         # the faster decoder: 8 / 12 / 16 -> 302.9-303.4 / 301.5-301.8 / 303.0-304.0; v42
         # with the fused merge + value projection (decoder side -3.4 ms) 16: the vocoder side
         # runs 286-301 ms from box to box, the decoder side 284-295; v46 with the C = 256
         # units on the register ring (vocoder side -7 ms): 16 / 10 / 6 -> 300.8-301.0 /
-        # 298.4-298.9 / 297.4-298.9 ms on one box; 8)
-        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(max(1, B // 8)))))
+        # 298.4-298.9 / 297.4-298.9 ms on one box; 8; v49 with the faster encoder phase and
+        # packed-pair YIN (1.14x): 8 / 4 / 0 -> 299.7-300.3 / 298.6-300.1 / 296.7-297.3 ms,
+        # sides 284.7 / 282.0 ms at 0: all of YIN after the vocoder)
+        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "0")))
                  if yin_side == "voc" else 0)
         ys = self._yin_s.stream if yin_side == "beside" else None
         pres = None
