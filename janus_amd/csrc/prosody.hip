@@ -31,9 +31,9 @@ namespace janus {
 constexpr int kYinBuf = 4096;          // aubio pitch buffer (prosody.py:32)
 constexpr int kYinLen = kYinBuf / 2;   // yin fvec length
 // Block = NT threads, each lane owns 2 consecutive taus, so one pass covers 2·NT taus.
-// NT = 64 (128-tau passes, the default for an uncapped grid): a voiced hop stops within
-// 128 taus of its period (F0 >= 190 Hz at 48 kHz after two passes); NT = 128 / 256 (256- /
-// 512-tau passes) by JANUS_YIN_THREADS; 256 for a grid capped beside the decoder.
+// NT = 128 (256-tau passes, the default for an uncapped grid): a voiced hop stops within
+// 256 taus of its period; NT = 64 / 256 (128- / 512-tau passes) by JANUS_YIN_THREADS; 256
+// for a grid capped beside the decoder.
 
 __device__ __forceinline__ int find_utt(const int64_t* offs, int B, int64_t g) {
   // largest b with offs[b] <= g (offs is non-decreasing, offs[0]=0, offs[B]=total)
@@ -375,12 +375,14 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     // beside the latency-bound decoder with one block per CU, leaving it room to dispatch
     const int64_t cap = max_blocks > 0 ? max_blocks : (1ll << 30);
     const int64_t grid = std::min<int64_t>(total_hops, cap);
-    // one-wave blocks (128-tau passes) for an uncapped grid on its own CUs (overlapped
-    // step, vocoder side: 297.3 vs 298.9 ms against 128-thread blocks, which had measured
-    // 33.5 vs 36 ms against 256); a capped grid beside the greedy decoder keeps the
-    // 256-thread blocks (back-to-back step: 422 vs 449 ms per step with 128)
+    // two-wave blocks (256-tau passes) for an uncapped grid on its own CUs: with the packed
+    // difference loop (LDS-latency-bound at one wave per 24.5 KB block) the second wave
+    // per block pays for the coarser early exit (r02 v49: 56 x 30 s 11.86 vs 12.63 ms
+    // standalone, 302.0-302.2 vs 304.7-305.1 ms per step; with the scalar loop one-wave
+    // blocks had been 1.6 ms per step faster); a capped grid beside the greedy decoder
+    // keeps the 256-thread blocks (back-to-back step: 422 vs 449 ms per step with 128)
     static const int nt_env = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 0;
-    const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 64);
+    const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 128);
     if (nt == 256)
       yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(
           pcm, sample_off, hop_off, B, hop, state_in, tol, silence_db, level_thr, (unsigned)sample_rate,
