@@ -49,10 +49,14 @@ def test_transcriber_wav(gpu, tmp_path):
     assert isinstance(t1, str) and t1 == t2
 
 
-def test_overlapped_step_matches_sequential(gpu):
+@pytest.mark.parametrize("yin_dec", ["0", "1"])
+def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
     """The serving pipeline (encode batch i on the whole GPU, then the greedy decoder of
     batch i and the vocoder of batch i-1 + YIN on disjoint CU-masked streams) produces the
-    same packets and the same waveforms as the back-to-back step."""
+    same packets and the same waveforms as the back-to-back step — with all of YIN on the
+    vocoder side (the default) and with the first utterance's YIN on the decoder side
+    (JANUS_YIN_DEC_UTTS=1: the prosody result comes back in two parts)."""
+    monkeypatch.setenv("JANUS_YIN_DEC_UTTS", yin_dec)
     pipe = JanusPipeline("tiny.en", max_length=12)
     batches = []
     for i in range(2):
