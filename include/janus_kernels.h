@@ -127,6 +127,14 @@ int janus_decode_attention_f16(const uint16_t* q, int64_t q_bs, const uint16_t* 
                                uint16_t* out, int64_t o_bs, int batch, int H, float scale,
                                float* part_o, float* part_ml, void* stream);
 
+/* Per segment b of a flat f32 array (offsets[B+1], int64): the count of values > 0 and
+ * np.mean of those values in order, numpy float32 bit for bit (float32 pairwise sums over
+ * 8192-element buffers, float64 divide by the count, 0 when none). The voiced-f0 mean of
+ * janus_prosody_analyze (backend/services/prosody.py:86-90: pitch_values.append(pitch) for
+ * pitch > 0, np.mean(pitch_values)) exposed for edge tests. */
+int janus_np_voiced_mean_f32(const float* values, const int64_t* offsets, int batch,
+                             float* mean_out, int32_t* count_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,7 @@ SIGNATURES = {
                               _P, _P, _P],
     "janus_prosody_analyze_ex": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
                                  _P, _P, _I32, _P],
+    "janus_np_voiced_mean_f32": [_P, _P, _I32, _P, _P, _P],
     "janus_pack_packet": [ctypes.POINTER(janus_packet), _P, ctypes.c_size_t,
                           ctypes.POINTER(ctypes.c_size_t)],
     "janus_unpack": [_P, ctypes.c_size_t, ctypes.POINTER(janus_mp_node), ctypes.c_size_t,

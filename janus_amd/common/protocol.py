@@ -42,7 +42,9 @@ def _to_value(v, keep) -> nat.janus_value:
     elif isinstance(v, float):
         out.type, out.f = nat.VAL_FLOAT, float(v)
     elif isinstance(v, str):
-        b = str(v).encode("utf-8")
+        # by value, as msgpack packs any str subclass (str(v) of a str-enum member is
+        # "Cls.MEMBER" on Python 3.10; protocol.py:107 packs the member's value)
+        b = str.encode(v, "utf-8")
         keep.append(b)
         out.type, out.s, out.len = nat.VAL_STR, b, len(b)
     else:
@@ -55,7 +57,7 @@ def pack_dict_fields(text, mode, prosody, override, timestamp) -> bytes:
     keep = []
     if not isinstance(text, str):
         raise TypeError("packet text must be str")
-    tb = text.encode("utf-8")
+    tb = str.encode(text, "utf-8")
     items = list((prosody or {}).items()) if prosody is not None else []
     if prosody is not None and not isinstance(prosody, dict):
         raise TypeError("prosody must be a dict")
@@ -76,7 +78,7 @@ def pack_dict_fields(text, mode, prosody, override, timestamp) -> bytes:
     if override is not None:
         if not isinstance(override, str):
             raise TypeError("override_emotion must be str")
-        ob = override.encode("utf-8")
+        ob = str.encode(override, "utf-8")
         keep.append(ob)
         pkt.override_emotion, pkt.override_len = ob, len(ob)
     else:

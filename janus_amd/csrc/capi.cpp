@@ -31,6 +31,8 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
                     float* mean_f0_out, int32_t* n_voiced_out, hipStream_t stream,
                     int max_blocks = 0);
 
+void np_voiced_mean_launch(const float* vals, const int64_t* offsets, int B, float* mean_out,
+                           int32_t* n_out, hipStream_t stream);
 void duck_pcm16_launch(int16_t* pcm, int64_t n, float level, hipStream_t s);
 void vad_energy_launch(const float* pcm, int64_t n_chunks, int chunk_len, int decim,
                        float center_db, float width_db, float* prob, hipStream_t s);
@@ -82,6 +84,14 @@ extern "C" int janus_prosody_analyze_ex(const float* pcm, const int64_t* sample_
     prosody_launch(pcm, sample_offsets, hop_offsets, batch, total_hops, sample_rate, hop_size,
                    tolerance, silence_db, state_in, state_out, f0_out, rms_out, mean_f0_out,
                    n_voiced_out, (hipStream_t)stream, max_blocks);
+  });
+}
+
+extern "C" int janus_np_voiced_mean_f32(const float* values, const int64_t* offsets, int batch,
+                                        float* mean_out, int32_t* count_out, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(batch >= 0 && (batch == 0 || (offsets && mean_out && count_out)), "bad argument");
+    np_voiced_mean_launch(values, offsets, batch, mean_out, count_out, (hipStream_t)stream);
   });
 }
 

@@ -262,63 +262,228 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
   }
 }
 
-// Per-utterance: RMS over the buffer (prosody.py:67), mean and count of voiced f0 (:86-90).
-__global__ __launch_bounds__(1024) void prosody_reduce_kernel(
+// ---- numpy float32 reductions, bit for bit -------------------------------------------
+// rms = np.sqrt(np.mean(x ** 2)) (prosody.py:67) and np.mean(pitch_values) (:90) are float32
+// np.add.reduce followed by a float64 divide by the np.intp count (numpy/_core/_methods.py
+// _mean: ret.dtype.type(ret / rcount)). np.add.reduce over a contiguous float32 array:
+//   * the reduction iterator hands the inner loop buffers of NPY_BUFSIZE = 8192 elements,
+//     whose sums accumulate SEQUENTIALLY into the identity 0.0f (out += pairwise(buffer));
+//   * each buffer is summed by pairwise_sum (numpy/_core/src/umath/loops_utils.h.src):
+//     n < 8 -> sequential from 0; n <= 128 -> 8 accumulators seeded with a[0..7], stepped
+//     by 8, combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), remainder added in order;
+//     else split at n2 = n/2 - (n/2)%8 and return pairwise(a, n2) + pairwise(a+n2, n-n2).
+// Pinned against numpy 2.2 on random sizes (tests/test_oracle_prosody.py).
+// The split tree depends on the buffer length only. A buffer <= 8192 has its leaves at depth
+// <= 7, so it maps onto 128 slots: slot t walks the splits by the bits of t (msb first);
+// a leaf reached at depth l belongs to the slot whose low 7-l bits are zero, the others
+// hold 0.0f. The perfect binary tree over the slots then adds exactly the pairs numpy adds
+// (x + 0.0f == x for every x >= 0 and NaN/inf alike), so a 7-level xor-shuffle tree gives
+// numpy's value bit for bit.
+constexpr int kNpBuf = 8192;    // NPY_BUFSIZE
+constexpr int kPwBlock = 128;   // PW_BLOCKSIZE
+constexpr int kPwDepth = 7;     // slots = 2^7 cover every buffer <= 8192 (host test)
+constexpr int kPwSlots = 1 << kPwDepth;
+
+__device__ __forceinline__ bool pw_slot(int m, int t, int& off, int& len) {
+  off = 0;
+  len = m;
+#pragma unroll
+  for (int l = 0; l < kPwDepth; ++l) {
+    if (len <= kPwBlock) return (t & ((1 << (kPwDepth - l)) - 1)) == 0;
+    int n2 = len >> 1;
+    n2 -= n2 & 7;
+    if ((t >> (kPwDepth - 1 - l)) & 1) { off += n2; len -= n2; }
+    else len = n2;
+  }
+  return true;
+}
+
+// pairwise_sum leaf over ld(off .. off+len), len <= 128
+template <class Ld>
+__device__ __forceinline__ float pw_leaf(const Ld& ld, int off, int len) {
+  if (len < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < len; ++i) r = __fadd_rn(r, ld(off + i));
+    return r;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = ld(off + j);
+  const int end = len - (len & 7);
+  int i = 8;
+  for (; i < end; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], ld(off + i + j));
+  }
+  float res = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                        __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+  for (; i < len; ++i) res = __fadd_rn(res, ld(off + i));
+  return res;
+}
+
+// Tree over the 128 slots of one buffer: slot t lives in lane t & 63 of wave (t >> 6) of a
+// 2-wave group; the root is the two waves' sums added (through LDS by the caller).
+__device__ __forceinline__ float pw_wave_tree(float v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) v = __fadd_rn(v, __shfl_xor(v, off));
+  return v;
+}
+
+// Squares of one 8192-element buffer, slot t = the 128 elements at 128 t (every leaf of a
+// full buffer): 16-byte loads when x is 16-byte aligned.
+__device__ __forceinline__ float sq_leaf_full(const float* x, int t) {
+  const float* a = x + kPwBlock * t;
+  float r[8];
+  if (((uintptr_t)a & 15) == 0) {
+    // two halves of 16 loads in flight (the 8-accumulator order is sequential in i, so
+    // the split changes nothing): 64 VGPRs of loads fit the 1024-thread block's budget
+    const float4* a4 = reinterpret_cast<const float4*>(a);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = a4[16 * h + q];
+      int q0 = 0;
+      if (h == 0) {
+        r[0] = __fmul_rn(v[0].x, v[0].x); r[1] = __fmul_rn(v[0].y, v[0].y);
+        r[2] = __fmul_rn(v[0].z, v[0].z); r[3] = __fmul_rn(v[0].w, v[0].w);
+        r[4] = __fmul_rn(v[1].x, v[1].x); r[5] = __fmul_rn(v[1].y, v[1].y);
+        r[6] = __fmul_rn(v[1].z, v[1].z); r[7] = __fmul_rn(v[1].w, v[1].w);
+        q0 = 2;
+      }
+#pragma unroll
+      for (int q = q0; q < 16; q += 2) {
+        r[0] = __fadd_rn(r[0], __fmul_rn(v[q].x, v[q].x));
+        r[1] = __fadd_rn(r[1], __fmul_rn(v[q].y, v[q].y));
+        r[2] = __fadd_rn(r[2], __fmul_rn(v[q].z, v[q].z));
+        r[3] = __fadd_rn(r[3], __fmul_rn(v[q].w, v[q].w));
+        r[4] = __fadd_rn(r[4], __fmul_rn(v[q + 1].x, v[q + 1].x));
+        r[5] = __fadd_rn(r[5], __fmul_rn(v[q + 1].y, v[q + 1].y));
+        r[6] = __fadd_rn(r[6], __fmul_rn(v[q + 1].z, v[q + 1].z));
+        r[7] = __fadd_rn(r[7], __fmul_rn(v[q + 1].w, v[q + 1].w));
+      }
+    }
+    return __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                     __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+  }
+  auto ld = [&](int i) { return __fmul_rn(a[i], a[i]); };
+  return pw_leaf(ld, 0, kPwBlock);
+}
+
+constexpr int kReduceThreads = 1024;                       // 8 buffers per pass
+constexpr int kReduceGroups = kReduceThreads / kPwSlots;
+
+// Per utterance: rms = np.sqrt(np.mean(x ** 2)) (prosody.py:67) and the count and
+// np.mean of the voiced f0 values in hop order (:86-90), numpy float32 bit for bit.
+// pcm == nullptr skips the energy half (kernel-level janus_np_voiced_mean_f32).
+__global__ __launch_bounds__(kReduceThreads) void prosody_reduce_kernel(
     const float* __restrict__ pcm, const int64_t* __restrict__ sample_off,
     const int64_t* __restrict__ hop_off, const float* __restrict__ f0, float* __restrict__ rms_out,
     float* __restrict__ mean_f0_out, int32_t* __restrict__ n_voiced_out) {
+  __shared__ float s_wave[kReduceThreads / 64];
+  __shared__ int s_cnt[kReduceThreads / 64];
+  __shared__ float s_comp[kNpBuf];   // the voiced values of one numpy buffer, compacted
   const int b = blockIdx.x;
-  const int64_t base = sample_off[b], n = sample_off[b + 1] - base;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid / kPwSlots, slot = tid % kPwSlots;
+
+  if (pcm != nullptr) {
+    const int64_t base = sample_off[b], n = sample_off[b + 1] - base;
+    const float* x = pcm + base;
+    const int64_t nbuf = (n + kNpBuf - 1) / kNpBuf;
+    float total = 0.0f;   // out = identity; out += pairwise(buffer) in buffer order (tid 0)
+    for (int64_t c0 = 0; c0 < nbuf; c0 += kReduceGroups) {
+      const int64_t c = c0 + grp;
+      float v = 0.0f;
+      if (c < nbuf) {
+        const float* xb = x + c * kNpBuf;
+        const int m = (int)min<int64_t>(kNpBuf, n - c * kNpBuf);
+        if (m == kNpBuf) {
+          v = sq_leaf_full(xb, slot);
+        } else {
+          int off, len;
+          if (pw_slot(m, slot, off, len)) {
+            auto ld = [&](int i) { return __fmul_rn(xb[i], xb[i]); };
+            v = pw_leaf(ld, off, len);
+          }
+        }
+      }
+      v = pw_wave_tree(v);
+      if (lane == 0) s_wave[wid] = v;
+      __syncthreads();
+      if (tid == 0) {
+        for (int g = 0; g < kReduceGroups && c0 + g < nbuf; ++g)
+          total = __fadd_rn(total, __fadd_rn(s_wave[2 * g], s_wave[2 * g + 1]));
+      }
+      __syncthreads();
+    }
+    if (tid == 0)
+      rms_out[b] = n > 0 ? __fsqrt_rn((float)((double)total / (double)n))
+                         : __int_as_float(0x7fc00000);  // mean([]) = nan
+  }
+
+  // voiced f0: count, then per numpy buffer of compacted values, gather + pairwise
   const int64_t h0 = hop_off[b], nh = hop_off[b + 1] - h0;
-  double ss = 0.0, fs = 0.0;
   int cnt = 0;
-  const float* x = pcm + base;
-  // vectorised when aligned; pcm offsets are arbitrary, so peel to 16 B.
-  int64_t head = (int64_t)((16 - ((uintptr_t)x & 15)) & 15) / 4;
-  if (head > n) head = n;
-  for (int64_t k = threadIdx.x; k < head; k += blockDim.x) ss += (double)x[k] * x[k];
-  const int64_t nv = (n - head) / 4;
-  const float4* x4 = reinterpret_cast<const float4*>(x + head);
-  // one block streams a whole utterance (5.76 MB at 30 s / 48 kHz): 4 loads per thread in
-  // flight per iteration (1024 threads) instead of one at a time
-  const int64_t step = 4 * (int64_t)blockDim.x;
-  int64_t k = threadIdx.x;
-  for (; k + 3 * (int64_t)blockDim.x < nv; k += step) {
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = x4[k + u * (int64_t)blockDim.x];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      ss += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y + (double)v[u].z * v[u].z +
-            (double)v[u].w * v[u].w;
-  }
-  for (; k < nv; k += blockDim.x) {
-    const float4 v = x4[k];
-    ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-  }
-  for (int64_t k = head + nv * 4 + threadIdx.x; k < n; k += blockDim.x) ss += (double)x[k] * x[k];
-  for (int64_t k = threadIdx.x; k < nh; k += blockDim.x) {
-    const float v = f0[h0 + k];
-    if (v > 0.0f) { fs += v; ++cnt; }
-  }
-  __shared__ double sh_ss[16], sh_fs[16];
-  __shared__ int sh_c[16];
-  for (int off = 32; off > 0; off >>= 1) {
-    ss += __shfl_xor(ss, off);
-    fs += __shfl_xor(fs, off);
-    cnt += __shfl_xor(cnt, off);
-  }
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sh_ss[wid] = ss; sh_fs[wid] = fs; sh_c[wid] = cnt; }
+  for (int64_t k = tid; k < nh; k += kReduceThreads) cnt += f0[h0 + k] > 0.0f;
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (lane == 0) s_cnt[wid] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0, f = 0;
-    int c = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { s += sh_ss[k]; f += sh_fs[k]; c += sh_c[k]; }
-    rms_out[b] = n > 0 ? (float)sqrt(s / (double)n) : __int_as_float(0x7fc00000);  // mean([]) = nan
-    mean_f0_out[b] = c > 0 ? (float)(f / c) : 0.0f;
-    n_voiced_out[b] = c;
+  int nv = 0;
+#pragma unroll
+  for (int w = 0; w < kReduceThreads / 64; ++w) nv += s_cnt[w];
+  __syncthreads();
+  float fsum = 0.0f;
+  for (int64_t cb = 0; cb < nv; cb += kNpBuf) {
+    // compact hops in order: block-wide exclusive scan of the voiced flags per 1024 hops
+    int64_t before = 0;
+    for (int64_t k0 = 0; k0 < nh; k0 += kReduceThreads) {
+      const int64_t k = k0 + tid;
+      const float v = k < nh ? f0[h0 + k] : 0.0f;
+      const bool voiced = v > 0.0f;
+      const unsigned long long m = __ballot(voiced);
+      const int in_wave = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) s_cnt[wid] = __popcll(m);
+      __syncthreads();
+      int64_t pos = before + in_wave;
+      int64_t seg = 0;
+#pragma unroll
+      for (int w = 0; w < kReduceThreads / 64; ++w) {
+        pos += w < wid ? s_cnt[w] : 0;
+        seg += s_cnt[w];
+      }
+      if (voiced && pos >= cb && pos < cb + kNpBuf) s_comp[pos - cb] = v;
+      before += seg;
+      __syncthreads();
+    }
+    const int m = (int)min<int64_t>(kNpBuf, nv - cb);
+    if (tid < kPwSlots) {
+      float v = 0.0f;
+      int off, len;
+      if (pw_slot(m, slot, off, len)) {
+        auto ld = [&](int i) { return s_comp[i]; };
+        v = pw_leaf(ld, off, len);
+      }
+      v = pw_wave_tree(v);
+      if (lane == 0) s_wave[wid] = v;
+    }
+    __syncthreads();
+    if (tid == 0) fsum = __fadd_rn(fsum, __fadd_rn(s_wave[0], s_wave[1]));
+    __syncthreads();
   }
+  if (tid == 0) {
+    mean_f0_out[b] = nv > 0 ? (float)((double)fsum / (double)nv) : 0.0f;
+    n_voiced_out[b] = nv;
+  }
+}
+
+void np_voiced_mean_launch(const float* vals, const int64_t* offsets, int B, float* mean_out,
+                           int32_t* n_out, hipStream_t stream) {
+  JANUS_CHECK(B >= 0, "batch must be >= 0");
+  if (B == 0) return;
+  prosody_reduce_kernel<<<dim3(B), dim3(kReduceThreads), 0, stream>>>(
+      nullptr, nullptr, offsets, vals, nullptr, mean_out, n_out);
+  JANUS_LAUNCH_CHECK();
 }
 
 // Detector state after the call = the aubio buffer after the last hop.
@@ -397,7 +562,7 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
           f0_out, total_hops);
     JANUS_LAUNCH_CHECK();
   }
-  prosody_reduce_kernel<<<dim3(B), dim3(1024), 0, stream>>>(pcm, sample_off, hop_off, f0_out, rms_out,
+  prosody_reduce_kernel<<<dim3(B), dim3(kReduceThreads), 0, stream>>>(pcm, sample_off, hop_off, f0_out, rms_out,
                                                            mean_f0_out, n_voiced_out);
   JANUS_LAUNCH_CHECK();
   if (state_out) {

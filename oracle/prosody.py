@@ -89,6 +89,76 @@ def yin_stream(x, sample_rate=48000, hop=512, tol=DEFAULT_TOLERANCE,
     return f0, st
 
 
+NP_BUFSIZE = 8192   # numpy's reduction buffer (NPY_BUFSIZE)
+PW_BLOCKSIZE = 128  # numpy pairwise_sum leaf size
+PW_DEPTH = 7        # leaves of a buffer <= 8192 lie at depth <= 7 (128 slots on the GPU)
+
+
+def _pw_leaf(a):
+    """numpy/_core/src/umath/loops_utils.h.src pairwise_sum for n <= 128 (float32)."""
+    n = len(a)
+    f = np.float32
+    if n < 8:
+        r = f(0)
+        for v in a:
+            r = f(r + v)
+        return r
+    r = [f(v) for v in a[:8]]
+    i = 8
+    while i < n - (n % 8):
+        for j in range(8):
+            r[j] = f(r[j] + a[i + j])
+        i += 8
+    res = f(f(f(r[0] + r[1]) + f(r[2] + r[3])) + f(f(r[4] + r[5]) + f(r[6] + r[7])))
+    for k in range(i, n):
+        res = f(res + a[k])
+    return res
+
+
+def pairwise_sum_f32(a):
+    """numpy's float32 pairwise_sum over one buffer: split at n/2 rounded down to a
+    multiple of 8 until a block is <= 128."""
+    n = len(a)
+    if n <= PW_BLOCKSIZE:
+        return _pw_leaf(a)
+    n2 = n // 2
+    n2 -= n2 % 8
+    return np.float32(pairwise_sum_f32(a[:n2]) + pairwise_sum_f32(a[n2:]))
+
+
+def np_sum_f32(a):
+    """np.add.reduce of a contiguous float32 array: the reduction iterator feeds buffers of
+    8192 elements, each pairwise-summed, accumulated in order into the identity 0.0f."""
+    a = np.ascontiguousarray(a, np.float32)
+    out = np.float32(0)
+    for i in range(0, len(a), NP_BUFSIZE):
+        out = np.float32(out + pairwise_sum_f32(a[i:i + NP_BUFSIZE]))
+    return out
+
+
+def np_mean_f32(a):
+    """np.mean of a float32 array: float32 sum, float64 divide by the np.intp count
+    (numpy/_core/_methods.py _mean), cast back to float32."""
+    return np.float32(np.float64(np_sum_f32(a)) / np.float64(len(a)))
+
+
+def pw_slot(m, t):
+    """The GPU's slot map (csrc/prosody.hip pw_slot): (offset, length) of the leaf slot t
+    of a buffer of m <= 8192 owns, or None for a zero slot."""
+    off, ln = 0, m
+    for lvl in range(PW_DEPTH):
+        if ln <= PW_BLOCKSIZE:
+            return (off, ln) if t & ((1 << (PW_DEPTH - lvl)) - 1) == 0 else None
+        n2 = ln // 2
+        n2 -= n2 % 8
+        if (t >> (PW_DEPTH - 1 - lvl)) & 1:
+            off, ln = off + n2, ln - n2
+        else:
+            ln = n2
+    assert ln <= PW_BLOCKSIZE, (m, t, ln)
+    return off, ln
+
+
 def energy_tag(rms) -> str:
     """prosody.py:69-74 (NaN from an empty buffer compares False -> 'Loud')."""
     if rms < 0.05:

@@ -4,7 +4,8 @@ reproduces the reference's own known-answer tests
 import numpy as np
 
 from janus_amd.workload import sine, synth_speech
-from oracle.prosody import OracleProsody, yin_stream
+from oracle.prosody import (NP_BUFSIZE, PW_DEPTH, OracleProsody, np_mean_f32, np_sum_f32,
+                            pairwise_sum_f32, pw_slot, yin_stream)
 
 
 def test_kat_energy_quiet():              # test_input_processing.py:461-468
@@ -68,3 +69,55 @@ def test_synthetic_speech_classes():
         r, f0, rms = OracleProsody(48000).analyze_buffer(x)
         assert r['energy'] == 'Normal' and abs(rms - 0.10) < 1e-3
         assert abs(np.median(f0[f0 > 0]) - f0c) < 0.05 * f0c
+
+
+# ---- numpy float32 reductions (prosody.py:67 rms, :90 mean of voiced f0) -----------------
+
+def test_np_sum_restatement_matches_numpy():
+    """The reduction the GPU reproduces — 8192-element buffers, pairwise inside, sequential
+    across — equals numpy's own np.sum / np.mean on float32 bit for bit (sizes around the
+    leaf, split and buffer boundaries and up to a 30 s 48 kHz buffer)."""
+    rng = np.random.default_rng(0)
+    sizes = list(range(0, 300)) + [1000, 1023, 4096, 8191, 8192, 8193, 8199, 16384, 16385,
+                                   24575, 100000, 1440000]
+    sizes += [int(v) for v in rng.integers(1, 400000, 40)]
+    for n in sizes:
+        x = (rng.standard_normal(n) * rng.uniform(0.01, 3.0)).astype(np.float32)
+        sq = x ** 2
+        assert np_sum_f32(sq).view(np.uint32) == np.sum(sq).view(np.uint32), n
+        if n:
+            with np.errstate(all="ignore"):
+                assert np_mean_f32(sq).view(np.uint32) == np.mean(sq).view(np.uint32), n
+    # the mean of a list of np.float32 scalars (pitch_values, prosody.py:87-90)
+    vals = [np.float32(v) for v in rng.uniform(80, 400, 3000)]
+    assert np_mean_f32(np.array(vals, np.float32)) == np.mean(vals)
+
+
+def test_np_sum_is_not_plain_pairwise():
+    """Sanity: the 8192 buffering matters (a whole-array pairwise tree differs)."""
+    rng = np.random.default_rng(1)
+    diff = 0
+    for _ in range(20):
+        sq = (rng.standard_normal(100000).astype(np.float32)) ** 2
+        diff += pairwise_sum_f32(sq) != np.sum(sq)
+    assert diff > 0
+
+
+def test_gpu_slot_map_covers_every_buffer():
+    """The GPU's 128-slot map (zero slots padded into a perfect tree) reaches every leaf of
+    every buffer length <= 8192 within 7 levels and reproduces pairwise_sum exactly."""
+    rng = np.random.default_rng(2)
+    for m in range(0, NP_BUFSIZE + 1):
+        slots = [pw_slot(m, t) for t in range(1 << PW_DEPTH)]   # asserts depth <= 7
+        got = [s for s in slots if s is not None]
+        assert sum(ln for _, ln in got) == m and all(ln <= 128 for _, ln in got)
+        if m % 97 == 0 or m in (8190, 8191, 8192):
+            a = (rng.standard_normal(m).astype(np.float32)) ** 2
+            vals = [np.float32(0)] * (1 << PW_DEPTH)
+            from oracle.prosody import _pw_leaf
+            for t, s in enumerate(slots):
+                if s is not None:
+                    vals[t] = _pw_leaf(a[s[0]:s[0] + s[1]])
+            while len(vals) > 1:
+                vals = [np.float32(vals[2 * i] + vals[2 * i + 1]) for i in range(len(vals) // 2)]
+            assert vals[0] == pairwise_sum_f32(a), m

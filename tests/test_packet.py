@@ -79,3 +79,34 @@ def test_str_enum_override_packs_as_str(native_lib):
 def test_unsupported_type_raises(native_lib):
     with pytest.raises(TypeError):
         JanusPacket("x", 0, {'energy': object()}, timestamp=1.0).serialize()
+
+
+def test_str_subclass_values_pack_by_value(native_lib):
+    """str-enum prosody keys/values, text and override (a caller's `class Tag(str, Enum)`)
+    pack as their string value, byte for byte what msgpack 1.2.1 emits for the reference's
+    to_dict (protocol.py:107); str(member) would be "Tag.NORMAL" on Python 3.10."""
+    import enum
+
+    class Tag(str, enum.Enum):
+        ENERGY = "energy"
+        PITCH = "pitch"
+        NORMAL = "Normal"
+        HIGH = "High"
+
+    class Text(str):
+        def __str__(self):
+            return "not this"
+
+    for override in ("Auto", Text("(joyful)")):
+        pkt = JanusPacket(Text("Hello world"), JanusMode.SEMANTIC_VOICE,
+                          {Tag.ENERGY: Tag.NORMAL, Tag.PITCH: Tag.HIGH}, override, 1234567890.0)
+        ref = {'t': Text("Hello world"), 'm': 0, 'p': {Tag.ENERGY: Tag.NORMAL, Tag.PITCH: Tag.HIGH},
+               'ts': 1234567890.0}
+        if override != "Auto":
+            ref['o'] = override
+        assert pkt.serialize() == msgpack.packb(ref, use_bin_type=True)
+    plain = JanusPacket("Hello world", JanusMode.SEMANTIC_VOICE, {'energy': 'Normal', 'pitch': 'High'},
+                        None, 1234567890.0)
+    tagged = JanusPacket("Hello world", JanusMode.SEMANTIC_VOICE,
+                         {Tag.ENERGY: Tag.NORMAL, Tag.PITCH: Tag.HIGH}, None, 1234567890.0)
+    assert tagged.serialize() == plain.serialize()

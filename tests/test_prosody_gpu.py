@@ -38,11 +38,14 @@ def check_batch(bufs, sr, hop, dev, states=None):
         assert np.array_equal(st[b].view(np.uint32), ref_st.view(np.uint32))
         with np.errstate(all="ignore"):
             ref_rms = np.sqrt(np.mean(x.astype(np.float32) ** 2))
-        if len(x):
-            assert abs(rms[b] - ref_rms) <= 1e-6 * max(ref_rms, 1e-6)
-        else:
-            assert np.isnan(rms[b])
+        # numpy float32 semantics bit for bit (prosody.py:67), NaN for an empty buffer
+        assert np.float32(rms[b]).view(np.uint32) == np.float32(ref_rms).view(np.uint32), \
+            (b, rms[b], ref_rms)
         voiced = [p for p in ref if p > 0]
+        mf = res.mean_f0.cpu().numpy()[b]
+        assert int(res.n_voiced.cpu().numpy()[b]) == len(voiced)
+        if voiced:
+            assert mf.view(np.uint32) == np.mean(voiced).view(np.uint32), (b, mf, np.mean(voiced))
         assert tags[b] == {'energy': energy_tag(ref_rms), 'pitch': pitch_tag(voiced)}
 
 
@@ -203,3 +206,149 @@ def test_grid_cap_identical(gpu, max_blocks):
     torch.cuda.synchronize()
     assert np.array_equal(a.f0.cpu().numpy().view(np.uint32), b.f0.cpu().numpy().view(np.uint32))
     assert a.tags() == b.tags()
+
+
+# ---- numpy-exact energy and voiced-f0 means at the tag edges ---------
+
+def _rms_np(x):
+    return np.sqrt(np.mean(x ** 2))
+
+
+def _buffers_at(target, n, seed):
+    """Buffers whose numpy rms is exactly prev(target), target and next(target) (float32):
+    one random buffer scaled near the target, then its largest sample a set by bisection
+    over the float32 bit patterns (numpy's rms is monotone in a: every float op on the way
+    is) to the smallest a whose rms reaches each wanted value."""
+    for s in range(seed, seed + 1000, 100):   # large sums can step over an rms value
+        out = _try_buffers_at(target, n, s)
+        if out is not None:
+            return out
+    raise AssertionError("no buffer reaches the wanted rms values")
+
+
+def _try_buffers_at(target, n, seed):
+    t = np.float32(target)
+    x = np.random.default_rng(seed).standard_normal(n).astype(np.float32)
+    y = (np.abs(x) * np.float32(float(target) / float(_rms_np(x)))).astype(np.float32)
+    i = int(np.argmax(y))
+    out = []
+    for want in (np.nextafter(t, np.float32(0)), t, np.nextafter(t, np.float32(np.inf))):
+        lo, hi = 0, int(np.float32(4.0 * float(y[i]) + 1.0).view(np.uint32))
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            y[i] = np.array(mid, np.uint32).view(np.float32)
+            if _rms_np(y) >= want:
+                hi = mid
+            else:
+                lo = mid
+        y[i] = np.array(hi, np.uint32).view(np.float32)
+        if _rms_np(y) != want:
+            return None
+        out.append((want, y.copy()))
+    return out
+
+
+@pytest.mark.parametrize("target", [0.05, 0.15])
+def test_energy_tag_edges_bit_exact(gpu, target):
+    """Buffers whose numpy rms is 0.05f / 0.15f and one ulp either side (lengths spanning
+    several 8192-sample numpy buffers plus a ragged tail): GPU rms bit-identical, tags equal
+    to the reference's (Quiet|Normal / Normal|Loud flip exactly where numpy's does)."""
+    cases = _buffers_at(target, 3 * 8192 + 77, 7) + _buffers_at(target, 150001, 8)
+    bufs = [y for _, y in cases]
+    res, _ = run_batch(bufs, 48000, 512, gpu)
+    rms = res.rms.cpu().numpy()
+    tags = res.tags()
+    for b, (r, y) in enumerate(cases):
+        assert rms[b].view(np.uint32) == r.view(np.uint32), (b, rms[b], r)
+        assert tags[b]['energy'] == energy_tag(r)
+    assert {energy_tag(r) for r, _ in cases} == ({'Quiet', 'Normal'} if target == 0.05 else {'Normal', 'Loud'})
+
+
+def test_energy_ragged_offsets_bit_exact(gpu):
+    """64 utterances at arbitrary (unaligned) offsets and lengths 0 .. 3 numpy buffers: rms
+    bit-identical to numpy (the 16-byte and the scalar leaf paths)."""
+    rng = np.random.default_rng(21)
+    lengths = [0, 1, 7, 8, 127, 128, 129, 8191, 8192, 8193] + [int(v) for v in rng.integers(1, 30000, 54)]
+    bufs = [(rng.standard_normal(n) * rng.uniform(0.01, 1)).astype(np.float32) for n in lengths]
+    res, _ = run_batch(bufs, 48000, 512, gpu)
+    rms = res.rms.cpu().numpy()
+    for b, x in enumerate(bufs):
+        with np.errstate(all="ignore"):
+            ref = _rms_np(x)
+        assert rms[b].view(np.uint32) == ref.view(np.uint32), (b, len(x), rms[b], ref)
+
+
+def _voiced_mean_gpu(lists, gpu):
+    from janus_amd import _native as nat
+    offs = np.concatenate([[0], np.cumsum([len(v) for v in lists])]).astype(np.int64)
+    vals = torch.from_numpy(np.concatenate(lists + [np.zeros(1, np.float32)]).astype(np.float32)).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    mean = torch.empty(len(lists), dtype=torch.float32, device=gpu)
+    cnt = torch.empty(len(lists), dtype=torch.int32, device=gpu)
+    nat.call("janus_np_voiced_mean_f32", vals.data_ptr(), o.data_ptr(), len(lists), mean.data_ptr(),
+             cnt.data_ptr(), nat.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    return mean.cpu().numpy(), cnt.cpu().numpy()
+
+
+def _f0_lists_at(target, n, seed):
+    """f0 lists (n a power of two, so the mean is the sum scaled exactly) whose numpy mean of
+    the positive values is prev(target), target, next(target); unvoiced zeros interleaved."""
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(80, 400, n).astype(np.float32)
+    base = (base - base.mean() + np.float32(target)).astype(np.float32)
+    t = np.float32(target)
+    want = {np.nextafter(t, np.float32(0)): None, t: None, np.nextafter(t, np.float32(np.inf)): None}
+    last = float(base[-1])
+    step = float(np.spacing(np.float32(target))) * n / 64
+    for k in range(-20000, 20000):
+        v = base.copy()
+        v[-1] = np.float32(last + k * step)
+        m = np.mean(v)
+        if m in want and want[m] is None:
+            want[m] = v
+        if all(x is not None for x in want.values()):
+            break
+    assert all(x is not None for x in want.values())
+    out = []
+    for m, v in want.items():
+        z = np.zeros(len(v) + len(v) // 3, np.float32)
+        pos = np.sort(rng.choice(len(z), len(v), replace=False))
+        z[pos] = v
+        out.append((m, z))
+    return out
+
+
+@pytest.mark.parametrize("target", [120.0, 200.0])
+def test_pitch_tag_edges_bit_exact(gpu, target):
+    """Voiced-f0 means at 120f / 200f and one ulp either side (np.mean over the positive
+    values in hop order, prosody.py:86-90), with 256 and 16384 voiced values (the latter
+    spans two numpy buffers): GPU mean and count bit-identical, pitch tag flips exactly
+    where the reference's does."""
+    cases = _f0_lists_at(target, 256, 3) + _f0_lists_at(target, 16384, 4)
+    mean, cnt = _voiced_mean_gpu([z for _, z in cases], gpu)
+    for b, (m, z) in enumerate(cases):
+        voiced = [p for p in z if p > 0]
+        assert cnt[b] == len(voiced)
+        assert mean[b].view(np.uint32) == m.view(np.uint32) == np.mean(voiced).view(np.uint32)
+        from janus_amd.services.prosody import pitch_tag as gpu_tag
+        assert gpu_tag(float(mean[b]), int(cnt[b])) == pitch_tag(voiced)
+    tags = {pitch_tag([m]) for m, _ in cases}
+    assert tags == ({'Deep', 'Normal'} if target == 120.0 else {'Normal', 'High'})
+
+
+def test_voiced_mean_random_bit_exact(gpu):
+    rng = np.random.default_rng(9)
+    lists = [np.zeros(0, np.float32), np.zeros(10, np.float32)]
+    for n in (1, 7, 8, 9, 128, 129, 1000, 2813, 8192, 8193, 9000, 20000):
+        v = rng.uniform(50, 1500, n).astype(np.float32)
+        v[rng.random(n) < 0.3] = 0.0
+        lists.append(v)
+    mean, cnt = _voiced_mean_gpu(lists, gpu)
+    for b, v in enumerate(lists):
+        pos = v[v > 0]
+        assert cnt[b] == len(pos)
+        if len(pos):
+            assert mean[b].view(np.uint32) == np.mean(pos).view(np.uint32), (b, len(v))
+        else:
+            assert mean[b] == 0.0
