@@ -90,6 +90,7 @@ class JanusPipeline:
         with torch.cuda.stream(hi):
             mel = w.logmel(pcm, offsets, B, 3)
             enc = w.encode(mel)
+        self.last_encoder_output = enc   # [B][1500][d] fp16, for parity checks
         main.wait_stream(hi)  # YIN after the (compute-bound) encoder, beside the decoder
         try:
             pres = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=256)
@@ -234,6 +235,7 @@ class JanusPipeline:
         with torch.cuda.stream(hi):
             mel = w.logmel(pcm, offsets, B, 3)
             enc = w.encode(mel)
+        self.last_encoder_output = enc   # [B][1500][d] fp16 of batch i, for parity checks
         # batch i-1 on the host while the encoder runs (its tensors were joined into the
         # caller's stream at the end of the previous call)
         prev = getattr(self, "_pending", None)

@@ -172,13 +172,19 @@ def synthetic_weights(cfg: WhisperConfig, seed: int = 0) -> dict:
     return engine_weights(W)
 
 
+# tensors the engine reads in fp32 (whisper.cpp: the decoder's positional table is added
+# to the token embedding in fp32); every other matrix is stored fp16 on the GPU
+FP32_MATRICES = frozenset({"decoder.embed_positions.weight"})
+
+
 def engine_weights(W: dict) -> dict:
-    """The numbers the engine multiplies: every matrix (conv kernels, projections,
-    embeddings, positional tables; ndim >= 2) rounded to fp16, the precision the GPU keeps
-    them in (a CTranslate2 float16 conversion stores them the same way); biases and
-    LayerNorm parameters stay fp32. The oracle is run on these weights, so parity
-    measures arithmetic, not weight rounding."""
-    return {k: (v.astype(np.float16).astype(np.float32) if v.ndim >= 2 else v.astype(np.float32))
+    """The numbers the engine multiplies: every matrix the GPU stores in fp16 (conv
+    kernels, projections, the token embedding, the encoder's positional table; ndim >= 2)
+    rounded to fp16, as a CTranslate2 float16 conversion stores them; biases, LayerNorm
+    parameters and the fp32-consumed tables (FP32_MATRICES) stay fp32. The oracle is run on
+    these weights, so parity measures arithmetic, not weight rounding."""
+    return {k: (v.astype(np.float16).astype(np.float32) if v.ndim >= 2 and k not in FP32_MATRICES
+                else v.astype(np.float32))
             for k, v in W.items()}
 
 

@@ -1,0 +1,105 @@
+"""Parity at the benchmark's own size (VERDICT r2 "next" #1): the bench's workload —
+JanusPipeline("base.en") on 64 x 30 s utterances, seeds 4000 + i (bench.py), run through
+the overlapped serving step exactly as bench.py times it (encoder on the whole GPU at
+M = 64 x 1500 rows and 64 x 8 attention heads; the greedy decoder at B = 64 on its 16
+CUs per XCD; the vocoder on 64 x 2584 frames on the other half) — compared row by row
+with the oracle, as engine.py:510-552 would produce them one utterance at a time:
+
+* rows {0, 21, 42, 63}: encoder output within 1e-3 relative RMS of the fp32 oracle
+  encoder (on the GPU's own log-mel); free-running tokens (447) identical to the oracle's
+  KV-cached greedy decoder on the engine's encoder output, or a first divergence at an
+  oracle near-tie; prosody tags identical to the stateful oracle; packet bytes identical
+  to the oracle packer (oracle transcript, oracle tags);
+* rows {0, 63}: the 30 s waveform (2584 latent frames) within 1e-3 RMS of the fp32
+  Firefly-GAN oracle driven by the oracle front end (prompt from the packet, stock voice),
+  int16 PCM equal to the oracle's rounding.
+Rows are independent, so the oracle runs only those utterances (~40 s of CPU)."""
+import numpy as np
+import pytest
+import torch
+
+from janus_amd import vocoder as jv
+from janus_amd import whisper as jw
+from janus_amd.common.protocol import JanusPacket
+from janus_amd.pipeline import JanusPipeline
+from janus_amd.services.synthesizer import emotion_prompt
+from janus_amd.workload import synth_speech
+from oracle import packet as opk
+from oracle import vocoder as ov
+from oracle import whisper as ow
+from oracle.prosody import OracleProsody
+
+pytestmark = pytest.mark.gpu
+
+B, SECONDS, FRAMES = 64, 30.0, 2584
+ROWS = (0, 21, 42, 63)
+WAV_ROWS = (0, 63)
+NEAR_TIE = 2e-3
+TS = 1700000000.25
+
+
+@pytest.mark.timeout(900)
+def test_bench_workload_rows_match_oracle(gpu):
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    utts = [synth_speech(4000 + i, SECONDS) for i in range(B)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+    pipe = JanusPipeline("base.en", max_length=448)
+    # the bench's step: the batch enters the overlapped pipeline, flush renders it
+    assert pipe.step_overlapped(pcm, offs, lengths, FRAMES, 16, timestamp=TS) == (None, None, None)
+    enc_gpu = pipe.last_encoder_output.float().cpu()
+    res, wav, pcm16 = pipe.flush(FRAMES)
+    mel = pipe.whisper.logmel(pcm, offs, B, 3)
+    torch.cuda.synchronize()
+    assert enc_gpu.shape == (B, 1500, 512) and wav.shape == (B, FRAMES * 512)
+
+    cfg = jw.CONFIGS["base.en"]
+    W = jw.load_weights(cfg, 0)
+    tk = pipe.whisper.tokenizer
+    rows = list(ROWS)
+    # encoder at M = 96 000 rows (the bench's GEMM shapes), oracle on the GPU's log-mel
+    ref_enc = ow.encoder(mel[rows].float().cpu().numpy(), W, cfg)
+    for i, b in enumerate(rows):
+        rel = float((enc_gpu[b] - ref_enc[i]).norm() / ref_enc[i].norm())
+        print(f"row {b}: encoder rel RMS {rel:.2e}")
+        assert rel < 1e-3, (b, rel)
+    # free-running greedy decode at B = 64 vs the oracle on the engine's encoder output
+    ref = ow.greedy_cached(enc_gpu[rows], W, cfg, tk, 448, no_speech=50361)
+    plen = len(tk.sot_sequence)
+    toks = res.tokens.cpu().numpy()
+    ntok = res.n_tokens.cpu().numpy()
+    identical = 0
+    for i, b in enumerate(rows):
+        g = [int(t) for t in toks[b][plen:plen + int(ntok[b])]]
+        r = ref[i]["tokens"]
+        assert len(g) >= 128
+        if g == r:
+            identical += 1
+        else:
+            first = next((k for k in range(min(len(g), len(r))) if g[k] != r[k]), min(len(g), len(r)))
+            margin = ref[i]["margins"][first] if first < len(ref[i]["margins"]) else 0.0
+            assert margin < NEAR_TIE, (b, first, margin)
+        tags = OracleProsody(48000).analyze_buffer(utts[b])[0]
+        assert res.tags[b] == tags, (b, res.tags[b], tags)
+        if g == r:
+            text = tk.transcript(r)
+            assert res.texts[b] == text
+            assert res.packets[b] == opk.serialize(text, 0, tags, "auto", TS), b
+    print(f"bench rows: {identical}/{len(rows)} token sequences identical")
+    assert identical >= len(rows) - 1
+    # the 30 s waveforms of two rows vs the fp32 generator
+    VW = jv.load_weights(jv.FireflyConfig(), 0)
+    vcfg = jv.FireflyConfig()
+    stock = np.asarray(VW["frontend.voice_embed"], np.float32)[jv.voice_id(jv.DEFAULT_REFERENCE_ID)]
+    assert all(p is not None for p in res.packets)   # every row rendered, in order
+    for b in WAV_ROWS:
+        prompt, tag = emotion_prompt(JanusPacket.deserialize(res.packets[b]))
+        lat = ov.frontend([prompt.encode()], [jv.emotion_id(tag, vcfg.n_emotions)], FRAMES, VW,
+                          stock[None])
+        ref_w = ov.generator(lat.half().float(), VW, vcfg)[0]
+        got = wav[b].float().cpu()
+        rms = float(((got - ref_w) ** 2).mean().sqrt())
+        print(f"row {b}: waveform rms {rms:.2e}")
+        assert rms <= 1e-3, (b, rms)
+        assert np.array_equal(pcm16[b].cpu().numpy(), ov.pcm16(got.numpy()))

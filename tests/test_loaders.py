@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from janus_amd import tokenizer as tkz
-from janus_amd.whisper import CONFIGS, WhisperConfig, load_weights, synthetic_weights
+from janus_amd.whisper import CONFIGS, FP32_MATRICES, WhisperConfig, load_weights, synthetic_weights
 
 TINY = WhisperConfig("t", d_model=64, n_heads=1, enc_layers=1, dec_layers=1)
 
@@ -31,7 +31,7 @@ def test_whisper_safetensors_names_and_dtype(tmp_path, monkeypatch, dtype):
     for k, v in got.items():
         assert v.dtype == np.float32 and v.shape == W[k].shape, k
         ref = W[k].astype(dtype).astype(np.float32)
-        if v.ndim >= 2:                       # matrices: fp16, as the engine holds them
+        if v.ndim >= 2 and k not in FP32_MATRICES:   # fp16, as the engine holds them
             ref = ref.astype(np.float16).astype(np.float32)
         assert np.array_equal(v, ref), k
 
