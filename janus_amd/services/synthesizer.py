@@ -19,6 +19,7 @@ suite does (backend/tests/test_synthesis.py:28-312). Morse generation is host nu
 in the reference.
 """
 import dataclasses
+import hashlib
 import logging
 import os
 
@@ -84,6 +85,25 @@ class _TTS:
 
     def __init__(self, engine: VocoderEngine):
         self.engine = engine
+        self._ref_key = None     # (len, blake2b) of the last reference recording
+        self._ref_voice = None   # its voice vector, or None when it could not be used
+
+    def _recording_voice(self, audio: bytes):
+        """Voice vector of a reference recording, computed once per distinct file content
+        (the Synthesizer hands the same hot-reloaded bytes with every packet). A recording
+        this host cannot decode (MP3 / WebM need FFmpeg) or embed is logged and the packet
+        is rendered without the voice term, instead of failing the render: the cloud the
+        reference calls accepts those files (synthesizer.py:179-203)."""
+        key = (len(audio), hashlib.blake2b(audio, digest_size=16).digest())
+        if key != self._ref_key:
+            try:
+                self._ref_voice = self.engine.speaker_embedding([wavio.read_wav_16k(audio)])[0]
+            except Exception as e:
+                logger.warning(f"reference audio not usable for voice cloning ({e}); "
+                               "rendering without it")
+                self._ref_voice = None
+            self._ref_key = key
+        return self._ref_voice
 
     def voice(self, references=None, reference_id=None):
         """[latent] f32 voice vector (device) for the SDK's voice arguments, or None."""
@@ -91,7 +111,7 @@ class _TTS:
         if references:
             ref = references[0]
             audio = ref.audio if isinstance(ref, ReferenceAudio) else ref["audio"]
-            return eng.speaker_embedding([wavio.read_wav_16k(bytes(audio))])[0]
+            return self._recording_voice(bytes(audio))
         if reference_id:
             return eng.voice(reference_id)
         return None

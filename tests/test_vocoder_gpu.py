@@ -149,3 +149,39 @@ def test_fishaudio_convert_matches_oracle(voc, tmp_path):
         assert out == wav_bytes(pcm[0].cpu().numpy()), k
         outs[k] = out
     assert outs["none"] != outs["rec"] and outs["id"] != outs["rec"]
+
+
+def test_reference_recording_formats_and_fallback(gpu, tmp_path):
+    """the hot-reloaded voice-cloning file. A 24-bit WAV is decoded and
+    embedded ONCE for any number of packets (cached on the file content); a file this host
+    cannot decode (an MP3) no longer silences every packet — it is rendered without the
+    voice term, as references=None would be."""
+    import struct
+
+    from janus_amd.services.synthesizer import Synthesizer
+    from janus_amd.workload import synth_speech
+    x = np.clip(synth_speech(91, 1.5) * 8388607, -8388608, 8388607).astype(np.int64)
+    pcm24 = b"".join(int(v).to_bytes(3, "little", signed=True) for v in x)
+    fmt = struct.pack("<HHIIHH", 1, 1, 48000, 48000 * 3, 3, 24)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", 16) + fmt + b"data" + struct.pack("<I", len(pcm24)) + pcm24
+    wav24 = tmp_path / "ref24.wav"
+    wav24.write_bytes(b"RIFF" + struct.pack("<I", len(body)) + body)
+    s = Synthesizer(api_key="unused", reference_audio_path=str(wav24))
+    tts = s.client.tts
+    calls = []
+    orig = tts.engine.speaker_embedding
+    tts.engine.speaker_embedding = lambda clips: (calls.append(len(clips)), orig(clips))[1]
+    pk = [JanusPacket("hello there", JanusMode.SEMANTIC_VOICE, {'energy': 'Normal', 'pitch': 'High'}),
+          JanusPacket("again", JanusMode.TEXT_ONLY, {}, "joyful")]
+    outs = [s.synthesize(p) for p in pk]
+    assert all(o[:4] == b"RIFF" and len(o) > 44 for o in outs)
+    assert calls == [1]
+    no_voice = tts.convert(text="(joyful) again", format="wav", latency="balanced", references=None)
+    assert outs[1] != no_voice                      # the recording shaped the voice
+    mp3 = tmp_path / "ref.mp3"
+    mp3.write_bytes(b"ID3\x04\x00\x00\x00\x00\x00\x21" + bytes(range(256)) * 8)
+    s2 = Synthesizer(api_key="unused", reference_audio_path=str(mp3))
+    out = s2.synthesize(pk[1])
+    assert out == s2.client.tts.convert(text="(joyful) again", format="wav", latency="balanced",
+                                        references=None)
+    assert s2.synthesize(pk[0])[:4] == b"RIFF"
