@@ -329,10 +329,10 @@ __device__ __forceinline__ float pw_wave_tree(float v) {
   return v;
 }
 
-// Squares of one 8192-element buffer, slot t = the 128 elements at 128 t (every leaf of a
-// full buffer): 16-byte loads when x is 16-byte aligned.
-__device__ __forceinline__ float sq_leaf_full(const float* x, int t) {
-  const float* a = x + kPwBlock * t;
+// Squares of leaf i of one full 8192-element buffer (the 128 elements at 128 i): 16-byte
+// loads when x is 16-byte aligned.
+__device__ __forceinline__ float sq_leaf_full(const float* x, int leaf) {
+  const float* a = x + kPwBlock * leaf;
   float r[8];
   if (((uintptr_t)a & 15) == 0) {
     // two halves of 16 loads in flight (the 8-accumulator order is sequential in i, so
@@ -399,7 +399,9 @@ __global__ __launch_bounds__(kReduceThreads) void prosody_reduce_kernel(
         const float* xb = x + c * kNpBuf;
         const int m = (int)min<int64_t>(kNpBuf, n - c * kNpBuf);
         if (m == kNpBuf) {
-          v = sq_leaf_full(xb, slot);
+          // a full buffer's 64 leaves of 128 sit at depth 6: slot 2i owns leaf i
+          // (pw_slot(8192, 2i) = (128 i, 128), tests/test_oracle_prosody.py)
+          if ((slot & 1) == 0) v = sq_leaf_full(xb, slot >> 1);
         } else {
           int off, len;
           if (pw_slot(m, slot, off, len)) {

@@ -109,6 +109,8 @@ def test_gpu_slot_map_covers_every_buffer():
     rng = np.random.default_rng(2)
     for m in range(0, NP_BUFSIZE + 1):
         slots = [pw_slot(m, t) for t in range(1 << PW_DEPTH)]   # asserts depth <= 7
+        if m == NP_BUFSIZE:   # the GPU's full-buffer fast path: slot 2i owns (128 i, 128)
+            assert slots == [(128 * (t // 2), 128) if t % 2 == 0 else None for t in range(128)]
         got = [s for s in slots if s is not None]
         assert sum(ln for _, ln in got) == m and all(ln <= 128 for _, ln in got)
         if m % 97 == 0 or m in (8190, 8191, 8192):

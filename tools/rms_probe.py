@@ -1,6 +1,11 @@
 """GPU probe: janus_prosody_analyze rms vs numpy for a few lengths (debug aid)."""
+import os
+import sys
+
 import numpy as np
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from janus_amd.services.prosody import prosody_launch
 dev = torch.device("cuda", 0)
 for n in (100, 8192, 7616, 16384, 24000, 40000):
