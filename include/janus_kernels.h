@@ -30,6 +30,14 @@ int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, i
                    const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
                    int N, int K, void* stream);
 
+/* The same product on the general 128 x 128-tile kernel (any N, K % 8 == 0). janus_gemm_f16
+ * dispatches M > 64 products with N % 256 == 0 and K % 64 == 0 to the 256 x 256-tile
+ * kernel (gemm_big.hip, the encoder's projections); both accumulate each output over the
+ * same k-steps in the same order, so their results are bit-identical. */
+int janus_gemm_nt128_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                         const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
+                         int N, int K, void* stream);
+
 /* The same product on hipBLASLt (the encoder's large-M projections): epi F16 / F32 /
  * RESID_F32 (C == R in place) / GELU_F16 (bias epilogue, then an exact-erf GELU pass);
  * bias required. Error when the library has no plan for the shape. */

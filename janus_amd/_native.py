@@ -86,6 +86,7 @@ SIGNATURES = {
     "janus_vocoder_family_stats": [_P, _I32, _P, _P, _P, _P, _P, _P, _I32],
     # include/janus_kernels.h
     "janus_gemm_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
+    "janus_gemm_nt128_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
     "janus_gemm_lt_f16": [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P],
     "janus_layernorm_f16": [_P, _P, _P, _P, _I32, _I32, _F32, _P],
     "janus_resid_ln_f16": [_P, _I64, _P, _I64, _P, _P, _P, _P, _F32, _P, _I32, _I32, _I32, _P],

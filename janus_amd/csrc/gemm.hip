@@ -645,7 +645,16 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
                             p.ln_g && p.ln_b && p.ldc == p.N),
               "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 512, ldc == N");
   if (p.M <= 64) launch_skinny(epi, p, s);
+  else if (gemm_big_supported(epi, p)) gemm_big_launch(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
+}
+
+void gemm_nt128_launch(int epi, const GemmArgs& p, hipStream_t s) {
+  JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
+  JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");
+  JANUS_CHECK(epi >= EPI_F16 && epi <= EPI_F32, "gemm_nt128: plain epilogues only");
+  if (p.M <= 0 || p.N <= 0) return;
+  launch_cfg<128, 128, 4, 4>(epi, p, s);
 }
 
 // exact-erf GELU in place, 8 halves per thread (the library GEMM's fc1 epilogue)

@@ -1,0 +1,187 @@
+// Large-M fp16 "NT" GEMM on MFMA for the Whisper encoder's projections (QKV, attention
+// output, fc1, fc2 at M = B x 1500 rows; transcriber.py:53-57 -> the CTranslate2 encoder):
+//   C[M,N] = epi( A[M,K] · W[N,K]^T + bias[N] ),  epi: fp16 | exact-erf GELU -> fp16 |
+//   fp32 residual add (C = R + ..., in place) | fp32.
+//
+// Geometry: 256 x 256 x 64 block tile, 8 waves (2 along M x 4 along N, 128 x 64 outputs
+// each = 8 x 4 tiles of v_mfma_f32_16x16x32_f16), one block per CU (128 KB of staging).
+// Staging: global_load_lds (16 B per lane, LDS-DMA, no VGPR round trip) into two LDS
+// buffers — the next k-tile's loads are issued before the current k-tile's MFMAs, one
+// vmcnt(0) + barrier per 64-deep k-tile.
+// LDS image: rows of 64 halves (128 B = 8 chunks of 16 B), chunk c of row r stored at
+// c ^ ((r >> 1) & 7). The fragment reads (lane l: row l & 15, chunk 4s + (l >> 4)) then put
+// the 16 lanes of every ds_read_b128 lane group ({0-3,12-15,20-27}, ...) on 16 distinct
+// 16-B bank slots: conflict-free. The DMA writes lane-linear, so the swizzle is applied to
+// the per-lane SOURCE address (the chunk a lane fetches), and the same XOR on the read.
+// Tiles are dealt XCD-aware (consecutive tiles of one A row panel on one L2).
+// Epilogue: the accumulators of each half of a wave's rows go through the (free) staging
+// LDS, then 8 consecutive columns per lane: bias, GELU or residual in fp32, 16-B stores.
+//
+// Accumulation order: one fp32 accumulator per output, k-steps of 32 in order — the same
+// MFMA sequence per output as gemm_nt_kernel (gemm.hip), so the two are bit-identical.
+#include "mfma.h"
+#include "kernels.h"
+
+namespace janus {
+
+namespace {
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kThreads = 512;                   // 8 waves
+constexpr int kWMT = 8, kWNT = 4;               // 16x16 tiles per wave (128 x 64)
+constexpr int kStageHalves = (kBM + kBN) * kBK; // one buffer: A tile then B tile
+constexpr int kEP = 68;                         // epilogue fp32 pitch (64 + 4)
+constexpr int kEpWave = 64 * kEP;               // floats per wave in the epilogue image
+constexpr int kSmemBytes = 8 * kEpWave * 4 > 2 * kStageHalves * 2 ? 8 * kEpWave * 4 : 2 * kStageHalves * 2;
+}  // namespace
+
+// DMA one 8-row x 128-B piece per wave-instruction: lane l -> row (l >> 3) of the piece,
+// physical chunk l & 7, fetching logical chunk (l & 7) ^ ((row >> 1) & 7).
+__device__ __forceinline__ void glds_rows8(const _Float16* __restrict__ src, int64_t ld, int row_g,
+                                           int row_l, int max_row, int k0, _Float16* lds_piece, int lane) {
+  const int r = row_l + (lane >> 3);
+  const int c = (lane & 7) ^ ((r >> 1) & 7);
+  const int gr = min(row_g + (lane >> 3), max_row);
+  const _Float16* g = src + (int64_t)gr * ld + k0 + 8 * c;
+  typedef __attribute__((address_space(3))) void lds_void;
+  __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)lds_piece, 16, 0, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int row0 = bm * kBM, col0 = bn * kBN;
+  const int lane = threadIdx.x & 63, wid = wave_id();
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // stage k-tile kt into buffer b: wave w DMAs rows [32w, 32w + 32) of the A tile and of
+  // the B tile, four 8-row pieces each
+  auto stage = [&](int kt, int b) {
+    _Float16* sA = smem + b * kStageHalves;
+    _Float16* sB = sA + kBM * kBK;
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wid * 32 + i * 8;
+      glds_rows8(p.A, p.lda, row0 + rl, rl, M - 1, k0, sA + rl * kBK, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wid * 32 + i * 8;
+      glds_rows8(p.W, p.ldw, col0 + rl, rl, N - 1, k0, sB + rl * kBK, lane);
+    }
+  };
+
+  f32x4 acc[kWMT][kWNT];
+#pragma unroll
+  for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+    for (int n = 0; n < kWNT; ++n) acc[m][n] = zero_f32x4();
+
+  // per-lane fragment offsets (halves): row lane & 15 of each 16-row tile, swizzled chunk
+  const int fr = lane & 15, sw = fr >> 1;
+  const int a_off = (wm * 128 + fr) * kBK, b_off = kBM * kBK + (wn * 64 + fr) * kBK;
+
+  const int nk = K / kBK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const _Float16* buf = smem + cur * kStageHalves;
+#pragma unroll
+    for (int s = 0; s < kBK / 32; ++s) {
+      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
+      half8 a[kWMT], b[kWNT];
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n) b[n] = *reinterpret_cast<const half8*>(buf + b_off + n * 16 * kBK + ch);
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m) a[m] = *reinterpret_cast<const half8*>(buf + a_off + m * 16 * kBK + ch);
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+        for (int n = 0; n < kWNT; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue, two passes of 64 rows per wave through the wave's own LDS image
+  float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
+  const int er = lane >> 3, ec = (lane & 7) * 8;           // 8 rows x 8 lanes per pass step
+  const int gcol = col0 + wn * 64 + ec;
+  float bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = p.bias ? p.bias[gcol + j] : 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sC[(m * 16 + (lane >> 4) * 4 + r) * kEP + n * 16 + fr] = acc[4 * h + m][n][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's stores land before its reads
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + er;
+      const int row = row0 + wm * 128 + h * 64 + lr;
+      const float4 lo = *reinterpret_cast<const float4*>(sC + lr * kEP + ec);
+      const float4 hi = *reinterpret_cast<const float4*>(sC + lr * kEP + ec + 4);
+      float v[8] = {lo.x + bias[0], lo.y + bias[1], lo.z + bias[2], lo.w + bias[3],
+                    hi.x + bias[4], hi.y + bias[5], hi.z + bias[6], hi.w + bias[7]};
+      if (row < M) {
+        if constexpr (EPI == EPI_F16 || EPI == EPI_GELU_F16) {
+          half8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (_Float16)(EPI == EPI_GELU_F16 ? gelu_erf(v[j]) : v[j]);
+          *reinterpret_cast<half8*>(static_cast<_Float16*>(p.C) + (int64_t)row * p.ldc + gcol) = o;
+        } else {
+          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + gcol;
+          if constexpr (EPI == EPI_RESID_F32) {
+            const float4 r0 = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol);
+            const float4 r1 = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol + 4);
+            v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+            v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+          }
+          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();       // the next pass overwrites the image
+  }
+}
+
+bool gemm_big_supported(int epi, const GemmArgs& p) {
+  if (!(epi == EPI_F16 || epi == EPI_GELU_F16 || epi == EPI_RESID_F32 || epi == EPI_F32)) return false;
+  if (p.M < kBM || p.N % kBN != 0 || p.K % kBK != 0 || p.K < kBK) return false;
+  if (p.lda % 8 || p.ldw % 8 || p.ldc % 8) return false;
+  if (((uintptr_t)p.A & 15) || ((uintptr_t)p.W & 15) || ((uintptr_t)p.C & 15)) return false;
+  if (epi == EPI_RESID_F32 && (!p.R || p.ldr % 4 || ((uintptr_t)p.R & 15))) return false;
+  if (p.kc || p.ln_part || p.a_group_cols || p.ln_out || p.lnin_x) return false;
+  return (int64_t)cdiv(p.M, kBM) * (p.N / kBN) < (1ll << 31);
+}
+
+void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
+  JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
+  const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
+  switch (epi) {
+    case EPI_F16: gemm_big_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
+    case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;
+    case EPI_RESID_F32: gemm_big_kernel<EPI_RESID_F32><<<blocks, kThreads, 0, s>>>(p); break;
+    default: gemm_big_kernel<EPI_F32><<<blocks, kThreads, 0, s>>>(p); break;
+  }
+  JANUS_LAUNCH_CHECK();
+}
+
+}  // namespace janus

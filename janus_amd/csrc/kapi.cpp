@@ -48,6 +48,18 @@ extern "C" int janus_gemm_f16(int epi, const uint16_t* A, int64_t lda, const uin
   });
 }
 
+extern "C" int janus_gemm_nt128_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W,
+                                    int64_t ldw, const float* bias, void* C, int64_t ldc,
+                                    const float* R, int64_t ldr, int M, int N, int K, void* stream) {
+  return guarded([&] {
+    GemmArgs g;
+    g.A = reinterpret_cast<const _Float16*>(A); g.lda = lda;
+    g.W = reinterpret_cast<const _Float16*>(W); g.ldw = ldw;
+    g.bias = bias; g.C = C; g.ldc = ldc; g.R = R; g.ldr = ldr; g.M = M; g.N = N; g.K = K;
+    gemm_nt128_launch(epi, g, (hipStream_t)stream);
+  });
+}
+
 extern "C" int janus_gemm_lt_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W,
                                  int64_t ldw, const float* bias, void* C, int64_t ldc,
                                  const float* R, int64_t ldr, int M, int N, int K, void* stream) {

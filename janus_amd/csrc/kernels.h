@@ -40,6 +40,11 @@ struct GemmArgs {
   const float* lnin_g = nullptr; const float* lnin_b = nullptr; float lnin_eps = 1e-5f;
 };
 void gemm_launch(int epi, const GemmArgs& p, hipStream_t s);
+// the general large-M kernel (128 x 128 tiles, any N / K % 8), for shapes gemm_big rejects
+void gemm_nt128_launch(int epi, const GemmArgs& p, hipStream_t s);
+// the encoder-size kernel (gemm_big.hip): 256 x 256 tiles, N % 256 == 0, K % 64 == 0
+bool gemm_big_supported(int epi, const GemmArgs& p);
+void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s);
 // x[M][N] += A W^T + bias (fp32, in place), then out[M][N] = LayerNorm(x) fp16 (gamma g,
 // beta b, eps) — one launch for the decoder's attention output projection + the next
 // LayerNorm (resid_ln_kernel in gemm.hip; bit-identical to the two launches it replaces).

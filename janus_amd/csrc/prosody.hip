@@ -420,7 +420,10 @@ __global__ __launch_bounds__(kReduceThreads) void prosody_reduce_kernel(
       __syncthreads();
     }
     if (tid == 0)
-      rms_out[b] = n > 0 ? __fsqrt_rn((float)((double)total / (double)n))
+      // np.sqrt of the float32 mean, correctly rounded: v_sqrt_f32 (what sqrtf / __fsqrt_rn
+      // compile to here) is 1-ulp approximate, the f64 square root is correctly rounded,
+      // and rounding it to float is the correctly rounded float root (53 >= 2 * 24 + 2)
+      rms_out[b] = n > 0 ? (float)sqrt((double)(float)((double)total / (double)n))
                          : __int_as_float(0x7fc00000);  // mean([]) = nan
   }
 
