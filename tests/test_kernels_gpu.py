@@ -46,6 +46,65 @@ def test_gemm(gpu, M, N, K, epi):
     assert err < (2e-3 if out_dtype == torch.float16 else 1e-4), err
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 1536, 512), (256, 512, 512), (4500, 2048, 512),
+                                   (3000, 512, 2048), (257, 256, 64)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_big(gpu, M, N, K, epi):
+    """The encoder-size kernel (janus_gemm_f16 with N % 256 == 0, K % 64 == 0 -> gemm_big:
+    256 x 256 tiles, LDS-DMA staging) against an fp64 reference, ragged M included, and
+    bit-identical to the 128 x 128-tile kernel (same k-step order per output)."""
+    g = torch.Generator().manual_seed(M + N * 5 + K + epi)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).half()
+    W = ((torch.rand(N, K, generator=g) * 2 - 1) / math.sqrt(K)).half()
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    ref = A.double() @ W.double().T + bias.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = ref + R.double()
+    dA, dW, db = A.to(gpu), W.to(gpu), bias.to(gpu)
+    out_dtype = torch.float16 if epi in (0, 1) else torch.float32
+    outs = []
+    for fn in ("janus_gemm_f16", "janus_gemm_nt128_f16"):
+        C = R.to(gpu).clone() if epi == 2 else torch.full((M, N), float("nan"), dtype=out_dtype, device=gpu)
+        nat.call(fn, epi, dA.data_ptr(), K, dW.data_ptr(), K, db.data_ptr(), C.data_ptr(),
+                 N, C.data_ptr() if epi == 2 else None, N, M, N, K, stream())
+        outs.append(C)
+    torch.cuda.synchronize()
+    err = rel_err(outs[0], ref)
+    assert err < (2e-3 if out_dtype == torch.float16 else 1e-4), err
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("N,K,epi", [(1536, 512, 0), (512, 512, 2), (2048, 512, 1), (512, 2048, 2)])
+def test_gemm_big_bench_shapes(gpu, N, K, epi):
+    """The bench's encoder projections at M = 64 x 1500 = 96 000 rows (QKV, attention output
+    + residual, fc1 + GELU, fc2 + residual): bit-identical to the 128 x 128-tile kernel,
+    and a sampled row block against fp64."""
+    M = 96000
+    g = torch.Generator(device=gpu).manual_seed(N + K)
+    A = (torch.rand(M, K, device=gpu, generator=g) * 2 - 1).half()
+    W = ((torch.rand(N, K, device=gpu, generator=g) * 2 - 1) / math.sqrt(K)).half()
+    b = torch.randn(N, device=gpu, generator=g)
+    R0 = torch.randn(M, N, device=gpu, generator=g)
+    outs = []
+    for fn in ("janus_gemm_f16", "janus_gemm_nt128_f16"):
+        C = R0.clone() if epi == 2 else torch.empty(M, N, dtype=torch.float16, device=gpu)
+        nat.call(fn, epi, A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(), C.data_ptr(), N,
+                 C.data_ptr() if epi == 2 else None, N, M, N, K, stream())
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    rows = torch.arange(95000, 96000, device=gpu)
+    ref = A[rows].double() @ W.double().T + b.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = ref + R0[rows].double()
+    assert rel_err(outs[0][rows], ref) < (2e-3 if epi in (0, 1) else 1e-4)
+
+
 @pytest.mark.parametrize("M,N,K", [(3000, 1536, 512), (3000, 512, 512), (3000, 2048, 512),
                                    (3000, 512, 2048), (1500, 384, 1536)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])

@@ -38,9 +38,12 @@ def check_batch(bufs, sr, hop, dev, states=None):
         assert np.array_equal(st[b].view(np.uint32), ref_st.view(np.uint32))
         with np.errstate(all="ignore"):
             ref_rms = np.sqrt(np.mean(x.astype(np.float32) ** 2))
-        # numpy float32 semantics bit for bit (prosody.py:67), NaN for an empty buffer
-        assert np.float32(rms[b]).view(np.uint32) == np.float32(ref_rms).view(np.uint32), \
-            (b, rms[b], ref_rms)
+        # numpy float32 semantics bit for bit (prosody.py:67); NaN (either sign) when empty
+        if len(x):
+            assert np.float32(rms[b]).view(np.uint32) == np.float32(ref_rms).view(np.uint32), \
+                (b, rms[b], ref_rms)
+        else:
+            assert np.isnan(rms[b]) and np.isnan(ref_rms)
         voiced = [p for p in ref if p > 0]
         mf = res.mean_f0.cpu().numpy()[b]
         assert int(res.n_voiced.cpu().numpy()[b]) == len(voiced)
