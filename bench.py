@@ -71,6 +71,9 @@ def cpu_baseline(model: str, tokens_per_utt: float):
     from oracle import vocoder as ov
     from oracle import whisper as ow
     affinity = len(os.sched_getaffinity(0))
+    # every host CPU this process may use: the affinity set, capped by OMP_NUM_THREADS when
+    # the machine sets it (the GPU boxes allot 16 host CPUs per GPU and export 16 there,
+    # while the affinity mask shows the whole host)
     threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
     torch.set_num_threads(threads)
     cfg = jw.CONFIGS[model]
@@ -109,6 +112,9 @@ def cpu_baseline(model: str, tokens_per_utt: float):
                    f"({FRAMES_30S} frames)"),
         "stage_seconds": {k: round(v, 3) for k, v in t.items()},
         "affinity_cpus": affinity,
+        "cores_note": ("threads = min(affinity, OMP_NUM_THREADS): the host CPU share this GPU's "
+                       "process is given (16 per GPU on the bench boxes, whose affinity mask "
+                       "lists the whole host)"),
         "cpu_model": _cpu_model(),
     }
 
@@ -213,6 +219,17 @@ def main():
     tok_counts = [float(n.float().mean().item()) for n in tok_counts]
     fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
+    # latency of one batch through an IDLE pipeline (encode then decode back to back, nothing
+    # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
+    idle = []
+    if args.overlap > 0:
+        pipe.flush(frames)
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pipe.step(pcm, offs, lengths, frames)
+        torch.cuda.synchronize()
+        idle.append(time.perf_counter() - t0)
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
     total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
     n_packets = sum(p is not None for p in enc.packets)
@@ -274,6 +291,8 @@ def main():
             "p50_latency_ms": round(float(np.median(
                 [a + b for a, b in zip(times[:-1], times[1:])] if args.overlap > 0 and len(times) > 1
                 else times)) * 1000.0, 2),
+            # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
+            "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2),
             "overlap": args.overlap,
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),

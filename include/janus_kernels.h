@@ -38,9 +38,10 @@ int janus_gemm_nt128_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t
                          const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
                          int N, int K, void* stream);
 
-/* The same product on hipBLASLt (the encoder's large-M projections): epi F16 / F32 /
- * RESID_F32 (C == R in place) / GELU_F16 (bias epilogue, then an exact-erf GELU pass);
- * bias required. Error when the library has no plan for the shape. */
+/* The same product on hipBLASLt — a comparison point for the hand-written kernels
+ * (tools/gemm_big_probe.py); no product path calls it. epi F16 / F32 / RESID_F32 (C == R
+ * in place) / GELU_F16 (bias epilogue, then an exact-erf GELU pass); bias required;
+ * workspace-free plans only. Error when the library has no such plan for the shape. */
 int janus_gemm_lt_f16(int epi, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                       const float* bias, void* C, int64_t ldc, const float* R, int64_t ldr, int M,
                       int N, int K, void* stream);

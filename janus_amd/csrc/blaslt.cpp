@@ -1,18 +1,17 @@
-// The encoder's large-M projections (M = B * 1500 rows, K = 512 / 2048) on hipBLASLt.
-//
-// These are plain GEMMs — C = A W^T + bias, or the residual form C += A W^T + bias with
-// an fp32 C — the case the task reserves the vendor library for; the library's tiles for
-// them run ~2x the rate of gemm_nt_kernel at K = 512 (tools/gemm_probe.py). The decoder's
-// M <= 64 projections and every fused epilogue stay hand-written (gemm.hip). The GELU
-// projection (fc1) uses the library's bias epilogue into fp16 followed by an exact-erf
-// GELU pass in place (the library's GELU is not Whisper's erf form).
+// The encoder's large-M projections on hipBLASLt — a COMPARISON point only
+// (janus_gemm_lt_f16, tools/gemm_big_probe.py): the product path runs the hand-written
+// gemm_big kernel (gemm_big.hip), at parity with the library over an encoder layer
+// (954 vs 963 us at 64 x 1500 rows, base.en). The GELU projection uses the
+// library's bias epilogue into fp16 followed by an exact-erf GELU pass in place (the
+// library's GELU is not Whisper's erf form).
+// Plans are restricted to workspace-free solutions and handles are per device, so
+// concurrent callers on different streams or devices share no scratch memory.
 //
 // Row-major C[M][N] = A[M][K] W[N][K]^T is the column-major problem
 // C^T[N x M] = op_T(W as [K x N], ld = ldw) * op_N(A as [K x M], ld = lda), bias per
 // column-major row (= per output column n).
 #include <hipblaslt/hipblaslt.h>
 
-#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -40,24 +39,24 @@ struct Plan {
 
 struct Lt {
   hipblasLtHandle_t h = nullptr;
-  void* ws = nullptr;
-  size_t ws_size = 64u << 20;
   std::map<std::tuple<int, int, int, int, int64_t, int64_t, int64_t>, Plan> plans;
-  std::mutex mu;
 };
 
-Lt& lt() {
-  static Lt* s = [] {
-    auto* l = new Lt;
+std::mutex g_lt_mu;  // guards the per-device map and every plan's descriptor
+
+Lt& lt() {  // the calling thread's current device
+  static std::map<int, Lt*> per_dev;
+  int dev = 0;
+  JANUS_HIP(hipGetDevice(&dev));
+  Lt*& l = per_dev[dev];
+  if (!l) {
+    l = new Lt;
     LT_CHECK(hipblasLtCreate(&l->h));
-    JANUS_HIP(hipMalloc(&l->ws, l->ws_size));
-    return l;
-  }();
-  return *s;
+  }
+  return *l;
 }
 
-Plan& plan_for(int epi, int M, int N, int K, int64_t lda, int64_t ldw, int64_t ldc) {
-  Lt& L = lt();
+Plan& plan_for(Lt& L, int epi, int M, int N, int K, int64_t lda, int64_t ldw, int64_t ldc) {
   const auto key = std::make_tuple(epi, M, N, K, lda, ldw, ldc);
   auto it = L.plans.find(key);
   if (it != L.plans.end()) return it->second;
@@ -77,8 +76,9 @@ Plan& plan_for(int epi, int M, int N, int K, int64_t lda, int64_t ldw, int64_t l
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lc, ct, N, M, ldc));         // C^T as [N x M]
   hipblasLtMatmulPreference_t pref;
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  const size_t no_ws = 0;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
-                                                 &L.ws_size, sizeof(L.ws_size)));
+                                                 &no_ws, sizeof(no_ws)));
   hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
   const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(L.h, p.desc, p.la, p.lb, p.lc, p.lc, pref, 1,
@@ -87,20 +87,12 @@ Plan& plan_for(int epi, int M, int N, int K, int64_t lda, int64_t ldw, int64_t l
   if (st == HIPBLAS_STATUS_SUCCESS && n > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS) {
     p.algo = res[0].algo;
     p.ws = res[0].workspaceSize;
-    p.ok = p.ws <= L.ws_size;
+    p.ok = p.ws == 0;
   }
   return L.plans.emplace(key, p).first->second;
 }
 
 }  // namespace
-
-bool gemm_lt_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("JANUS_ENC_BLASLT");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return on;
-}
 
 // true when the library ran the GEMM; false = no plan for this shape (caller falls back
 // to gemm_launch). Epilogues: EPI_F16 / EPI_F32 (bias), EPI_RESID_F32 (C == R in place,
@@ -109,9 +101,9 @@ bool gemm_lt_launch(int epi, const GemmArgs& g, hipStream_t s) {
   if (!(epi == EPI_F16 || epi == EPI_F32 || epi == EPI_RESID_F32 || epi == EPI_GELU_F16)) return false;
   if (epi == EPI_RESID_F32 && (g.R != g.C || g.ldr != g.ldc)) return false;
   if (g.a_group_cols || g.lnin_x || g.ln_part || g.ln_out || g.kc) return false;
+  std::lock_guard<std::mutex> lock(g_lt_mu);
   Lt& L = lt();
-  std::lock_guard<std::mutex> lock(L.mu);
-  Plan& p = plan_for(epi, g.M, g.N, g.K, g.lda, g.ldw, g.ldc);
+  Plan& p = plan_for(L, epi, g.M, g.N, g.K, g.lda, g.ldw, g.ldc);
   if (!p.ok) return false;
   const float alpha = 1.0f, beta = epi == EPI_RESID_F32 ? 1.0f : 0.0f;
   const void* bias = g.bias;
@@ -120,7 +112,7 @@ bool gemm_lt_launch(int epi, const GemmArgs& g, hipStream_t s) {
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
   (void)zero_bias;
   LT_CHECK(hipblasLtMatmul(L.h, p.desc, &alpha, g.W, p.la, g.A, p.lb, &beta, g.C, p.lc, g.C, p.lc,
-                           &p.algo, L.ws, p.ws, s));
+                           &p.algo, nullptr, 0, s));
   if (epi == EPI_GELU_F16)
     gelu_inplace_f16_launch(static_cast<_Float16*>(g.C), g.ldc, g.M, g.N, s);
   return true;

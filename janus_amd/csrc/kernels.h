@@ -150,10 +150,9 @@ struct ConvArgs {
   int remap = -1;                       // tile order: 0 dispatch, 1 XCD runs of row blocks,
                                         // 2 XCD runs over the whole grid; -1 = default
 };
-// Encoder large-M projections on hipBLASLt (blaslt.cpp): true when the library ran the
-// GEMM (plain and residual epilogues; GELU as bias + an exact-GELU pass), false when it
-// has no plan for the shape (the caller falls back to gemm_launch).
-bool gemm_lt_enabled();
+// The same products on hipBLASLt (blaslt.cpp), a comparison point only (the product path
+// runs gemm_big): true when the library ran the GEMM (plain and residual epilogues; GELU
+// as bias + an exact-GELU pass), false when it has no workspace-free plan for the shape.
 bool gemm_lt_launch(int epi, const GemmArgs& g, hipStream_t s);
 // x = gelu_erf(x) in place on fp16 [M][N] (row stride ld, N % 8 == 0)
 void gelu_inplace_f16_launch(_Float16* x, int64_t ld, int M, int N, hipStream_t s);

@@ -213,12 +213,9 @@ static void prepare(janus_whisper* w, hipStream_t s) {
   w->prepared = true;
 }
 
-// The encoder's projections (M = B * 1500 rows) go to hipBLASLt where it has a plan
-// (blaslt.cpp; JANUS_ENC_BLASLT=0 keeps them on gemm_nt_kernel).
-static void enc_gemm(int epi, const GemmArgs& g, hipStream_t s) {
-  if (gemm_lt_enabled() && gemm_lt_launch(epi, g, s)) return;
-  gemm_launch(epi, g, s);
-}
+// The encoder's projections (M = B * 1500 rows): gemm_launch dispatches them to the
+// 256 x 256-tile LDS-DMA kernel (gemm_big.hip) when N % 256 == 0 (base.en: every one).
+static void enc_gemm(int epi, const GemmArgs& g, hipStream_t s) { gemm_launch(epi, g, s); }
 
 static GemmArgs gargs(const _Float16* A, int64_t lda, const _Float16* W, int64_t ldw,
                       const float* bias, void* C, int64_t ldc, int M, int N, int K,
