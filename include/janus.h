@@ -201,11 +201,23 @@ int janus_whisper_set_tensor(janus_whisper* w, const char* name, const float* ho
 /*
  * Log-mel features (faster-whisper FeatureExtractor, n_fft 400, hop 160, 80 mels,
  * 3000 frames) of x[::decim] for each utterance of pcm [device] (offsets [device]
- * int64[B+1]; <= 30 s after decimation). logmel [device] f32 [B][3000][80] (raw
- * log10 mel, may be NULL), mel [device] fp16 [B][3000][80] (clamped and scaled).
+ * int64[B+1]). logmel [device] f32 [B][3000][80] (raw log10 mel, may be NULL), mel
+ * [device] fp16 [B][3000][80] (clamped and scaled). The first 30 s window of each clip as
+ * faster-whisper's generate_segments feeds it to the encoder: frames from len(x16) // 160
+ * on are 0.0 (pad_or_trim of the content frames), the global max is over the frames that
+ * reach the first 30 s + 2 frames of audio (the whole clip when it is <= 30 s).
  */
 int janus_whisper_logmel(janus_whisper* w, const float* pcm, const int64_t* offsets, int batch,
                          int decim, float* logmel, uint16_t* mel, void* stream);
+/*
+ * The whole-clip log-mel faster-whisper computes once per transcribe() call
+ * (transcriber.py:53-57 -> WhisperModel.transcribe -> FeatureExtractor(audio)): `frames`
+ * frames per utterance, mel [device] fp16 [B][frames][80], normalised with the maximum over
+ * every frame of the clip, frames from len(x16) // 160 on 0.0. Its 30 s windows are the
+ * slices [seek, seek + min(3000, content - seek)) padded with zeros to 3000 frames.
+ */
+int janus_whisper_logmel_frames(janus_whisper* w, const float* pcm, const int64_t* offsets,
+                                int batch, int decim, int frames, uint16_t* mel, void* stream);
 /* Encoder forward: mel [device] fp16 [B][3000][80] -> enc [device] fp16 [B][1500][d]. */
 int janus_whisper_encode(janus_whisper* w, const uint16_t* mel, int batch, uint16_t* enc,
                          void* stream);

@@ -70,6 +70,7 @@ SIGNATURES = {
     "janus_whisper_destroy": [_P],
     "janus_whisper_set_tensor": [_P, ctypes.c_char_p, _P, _I64],
     "janus_whisper_logmel": [_P, _P, _P, _I32, _I32, _P, _P, _P],
+    "janus_whisper_logmel_frames": [_P, _P, _P, _I32, _I32, _I32, _P, _P],
     "janus_whisper_encode": [_P, _P, _I32, _P, _P],
     "janus_whisper_decode_greedy": [_P, _P, _I32, _P, _P, _P, _P, _P],
     "janus_whisper_decode_greedy_ex": [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P],

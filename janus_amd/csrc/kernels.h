@@ -205,7 +205,8 @@ void silero_vad_launch(const float* pcm, int n_streams, int n_chunks, int chunk_
 void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* basis,
                 const float* filters, float* logmel, uint32_t* maxkey, int n_frames_out,
                 int decim, hipStream_t s);
-void mel_normalize_launch(const float* logmel, const uint32_t* maxkey, _Float16* out, int B,
-                          int frames, int n_mels, int out_ld, hipStream_t s);
+void mel_normalize_launch(const float* logmel, const uint32_t* maxkey, _Float16* out,
+                          const int64_t* offsets, int decim, int B, int frames, int n_mels,
+                          int out_ld, hipStream_t s);
 
 }  // namespace janus

@@ -162,18 +162,26 @@ __global__ __launch_bounds__(256, 3) void mel_kernel(const float* __restrict__ p
   }
 }
 
+// max(x, global_max - 8), (x + 4) / 4 for the content frames of each utterance; frames at
+// and beyond content = len(x16) // 160 are 0.0. faster-whisper slices every 30 s window out
+// of the whole clip's log-mel (content frames only: segment_size = min(3000,
+// content_frames - seek)) and pads it to 3000 frames with zeros (pad_or_trim), so a window
+// past the end of the audio holds 0.0 there, not the log-mel of silence.
 __global__ void mel_normalize_kernel(const float* __restrict__ logmel,
                                      const uint32_t* __restrict__ maxkey, _Float16* __restrict__ out,
+                                     const int64_t* __restrict__ offsets, int decim,
                                      int frames, int out_ld, int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int mb = (int)(idx % kMels);
   const int64_t row = idx / kMels;  // b*frames + f
   const int b = (int)(row / frames);
+  const int f = (int)(row - (int64_t)b * frames);
+  const int64_t n16 = (offsets[b + 1] - offsets[b] + decim - 1) / decim;
   const uint32_t k = maxkey[b];
   const float gmax = __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
   float v = fmaxf(logmel[idx], gmax - 8.0f);
-  out[row * out_ld + mb] = (_Float16)((v + 4.0f) / 4.0f);
+  out[row * out_ld + mb] = f < n16 / kHop ? (_Float16)((v + 4.0f) / 4.0f) : (_Float16)0.0f;
 }
 
 void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* basis,
@@ -190,13 +198,14 @@ void mel_launch(const float* pcm, const int64_t* offsets, int B, const float* ba
   JANUS_LAUNCH_CHECK();
 }
 
-void mel_normalize_launch(const float* logmel, const uint32_t* maxkey, _Float16* out, int B,
-                          int frames, int n_mels, int out_ld, hipStream_t s) {
+void mel_normalize_launch(const float* logmel, const uint32_t* maxkey, _Float16* out,
+                          const int64_t* offsets, int decim, int B, int frames, int n_mels,
+                          int out_ld, hipStream_t s) {
   JANUS_CHECK(n_mels == kMels, "mel: 80 bins only");
   const int64_t total = (int64_t)B * frames * kMels;
   if (total == 0) return;
-  mel_normalize_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(logmel, maxkey, out, frames,
-                                                                   out_ld, total);
+  mel_normalize_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(logmel, maxkey, out, offsets,
+                                                                   decim, frames, out_ld, total);
   JANUS_LAUNCH_CHECK();
 }
 

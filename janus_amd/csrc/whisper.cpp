@@ -678,25 +678,40 @@ extern "C" int janus_whisper_set_tensor(janus_whisper* w, const char* name, cons
   });
 }
 
+static void logmel_frames(janus_whisper* w, const float* pcm, const int64_t* offsets, int batch,
+                          int decim, int frames, float* logmel, uint16_t* mel, hipStream_t s) {
+  float* lm = logmel;
+  if (!lm) {
+    w->ws_logmel.ensure(sizeof(float) * (int64_t)batch * frames * 80);
+    lm = w->ws_logmel.as<float>();
+  }
+  w->ws_maxkey.ensure(sizeof(uint32_t) * (batch > 0 ? batch : 1));
+  mel_launch(pcm, offsets, batch, w->params.get("mel.basis", 400 * 416),
+             w->params.get("mel.filters", 208 * 80), lm, w->ws_maxkey.as<uint32_t>(), frames,
+             decim, s);
+  mel_normalize_launch(lm, w->ws_maxkey.as<uint32_t>(), reinterpret_cast<_Float16*>(mel), offsets,
+                       decim, batch, frames, 80, 80, s);
+}
+
 extern "C" int janus_whisper_logmel(janus_whisper* w, const float* pcm, const int64_t* offsets,
                                     int batch, int decim, float* logmel, uint16_t* mel,
                                     void* stream) {
   return guarded([&] {
     JANUS_CHECK(w && pcm && offsets && mel, "null argument");
     std::lock_guard<std::mutex> lk(w->mu);
-    hipStream_t s = (hipStream_t)stream;
-    const int frames = 2 * w->cfg.n_audio_ctx;
-    float* lm = logmel;
-    if (!lm) {
-      w->ws_logmel.ensure(sizeof(float) * (int64_t)batch * frames * 80);
-      lm = w->ws_logmel.as<float>();
-    }
-    w->ws_maxkey.ensure(sizeof(uint32_t) * (batch > 0 ? batch : 1));
-    mel_launch(pcm, offsets, batch, w->params.get("mel.basis", 400 * 416),
-               w->params.get("mel.filters", 208 * 80), lm, w->ws_maxkey.as<uint32_t>(), frames,
-               decim, s);
-    mel_normalize_launch(lm, w->ws_maxkey.as<uint32_t>(), reinterpret_cast<_Float16*>(mel), batch,
-                         frames, 80, 80, s);
+    logmel_frames(w, pcm, offsets, batch, decim, 2 * w->cfg.n_audio_ctx, logmel, mel,
+                  (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_whisper_logmel_frames(janus_whisper* w, const float* pcm,
+                                           const int64_t* offsets, int batch, int decim,
+                                           int frames, uint16_t* mel, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(w && pcm && offsets && mel, "null argument");
+    JANUS_CHECK(frames >= 1 && (int64_t)batch * frames * 80 < (1ll << 40), "bad frame count");
+    std::lock_guard<std::mutex> lk(w->mu);
+    logmel_frames(w, pcm, offsets, batch, decim, frames, nullptr, mel, (hipStream_t)stream);
   });
 }
 

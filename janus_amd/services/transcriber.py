@@ -27,10 +27,13 @@ Deliberate deviations: the temperature FALLBACK is not run — a
 whose gates fail (compression ratio > 2.4 or avg_logprob < -1, outside the no-speech
 case) is flagged (``Segment.needs_fallback``, ``WhisperModel.stats``) and its T = 0
 decode kept, because the T > 0 re-decodes are random samples no offline oracle can pin;
-each window's log-mel is computed from the audio slice at the seek position (faster-
-whisper slices one whole-audio log-mel: the two differ only in the global-max
-normalisation scope); a window that would not advance the seek (a leading
-<|0.00|><|0.00|>) advances by the window size, so the loop always terminates.
+a window that would not advance the seek (a leading <|0.00|><|0.00|>) advances by the
+window size, so the loop always terminates.
+
+Features are faster-whisper's: one log-mel of the whole clip (normalised with the maximum
+over all its frames), from which each window takes the content frames
+[seek, seek + min(3000, content - seek)) and is padded with zeros to 3000 frames
+(``features[:, seek:seek + segment_size]`` + ``pad_or_trim``).
 """
 import dataclasses
 import zlib
@@ -149,10 +152,8 @@ class _Stream:
     def active(self):
         return self.seek < self.content_frames
 
-    def window(self):
-        size = min(N_FRAMES, self.content_frames - self.seek)
-        a = self.audio[self.seek * HOP:self.seek * HOP + size * HOP]
-        return size, np.ascontiguousarray(a, np.float32)
+    def window_size(self):
+        return min(N_FRAMES, self.content_frames - self.seek)
 
     def prompt(self, tk, max_length=448):
         prev = self.all_tokens[self.prompt_reset_since:]
@@ -167,18 +168,29 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
     tk = engine.tokenizer
     dev = engine.device
     streams = [_Stream(np.asarray(a, np.float32)) for a in audios]
+    # the whole clip's features, once per utterance (faster-whisper's FeatureExtractor call)
+    feats = []
+    for st in streams:
+        if st.content_frames <= 0:
+            feats.append(None)
+            continue
+        pcm = torch.from_numpy(np.concatenate([st.audio, np.zeros(1, np.float32)])).to(dev)
+        offs = torch.tensor([0, len(st.audio)], dtype=torch.int64, device=dev)
+        feats.append(engine.logmel_frames(pcm, offs, 1, 1, st.content_frames)[0])
     while True:
-        act = [s for s in streams if s.active]
+        act = [i for i, s in enumerate(streams) if s.active]
         if not act:
             break
         for c0 in range(0, len(act), max_batch):
-            grp = act[c0:c0 + max_batch]
-            wins = [s.window() for s in grp]
-            lengths = [len(a) for _, a in wins]
-            offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
-            pcm = torch.from_numpy(np.concatenate([a for _, a in wins] + [np.zeros(1, np.float32)])).to(dev)
-            enc = engine.encode(engine.logmel(pcm, offs, len(grp), 1))
+            idx = act[c0:c0 + max_batch]
+            grp = [streams[i] for i in idx]
+            sizes = [s.window_size() for s in grp]
+            mel = torch.zeros(len(grp), N_FRAMES, 80, dtype=torch.float16, device=dev)
+            for j, (i, s, size) in enumerate(zip(idx, grp, sizes)):
+                mel[j, :size] = feats[i][s.seek:s.seek + size]      # pad_or_trim: zeros after
+            enc = engine.encode(mel)
             out = engine.decode_ex(enc, prompts=[s.prompt(tk, max_length) for s in grp], max_length=max_length)
+            wins = [(size, None) for size in sizes]
             for s, (size, _), (toks, avg_lp, nsp) in zip(grp, wins, out.rows()):
                 s.windows += 1
                 text = tk.decode(toks).strip()

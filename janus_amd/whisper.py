@@ -256,6 +256,15 @@ class WhisperEngine:
                  raw.data_ptr() if raw is not None else None, mel.data_ptr(), nat.stream_ptr())
         return (mel, raw) if want_raw else mel
 
+    def logmel_frames(self, pcm: torch.Tensor, offsets: torch.Tensor, batch: int, decim: int,
+                      frames: int) -> torch.Tensor:
+        """Whole-clip features (janus_whisper_logmel_frames): fp16 [batch][frames][80],
+        normalised over every frame of each clip, 0.0 from each clip's content end on."""
+        mel = torch.empty(batch, frames, 80, dtype=torch.float16, device=self.device)
+        nat.call("janus_whisper_logmel_frames", self._h, pcm.data_ptr(), offsets.data_ptr(), batch,
+                 decim, frames, mel.data_ptr(), nat.stream_ptr())
+        return mel
+
     def encode(self, mel: torch.Tensor) -> torch.Tensor:
         B = mel.shape[0]
         assert mel.dtype == torch.float16 and mel.is_contiguous()

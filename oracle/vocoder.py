@@ -49,7 +49,7 @@ def speaker(clips16k, W):
     for x in clips16k:
         x = np.asarray(x, np.float32)[:480000]
         nf = min(3000, max(1, -(-len(x) // 160)))
-        m = logmel(x, 1, mel_filters()).astype(np.float64)[:nf].mean(0)
+        m = logmel(x, 1, mel_filters(), zero_pad=False).astype(np.float64)[:nf].mean(0)
         out.append(bias + P @ m)
     return np.stack(out).astype(np.float32)
 

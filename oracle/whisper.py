@@ -21,8 +21,15 @@ import torch
 import torch.nn.functional as F
 
 
-def logmel(x, decim=3, filters=None, n_frames=3000):
-    """float32 [n_frames][80]; ``filters`` is [201][80] (janus_amd.whisper.mel_filters)."""
+def logmel(x, decim=3, filters=None, n_frames=3000, zero_pad=True):
+    """float32 [n_frames][80]; ``filters`` is [201][80] (janus_amd.whisper.mel_filters).
+    faster-whisper's features: the log-mel of the clip padded with 30 s of zeros,
+    normalised with the maximum over every frame, of which only the content frames
+    (len(x16) // 160) are used — a window is sliced from them and padded with ZEROS to 3000
+    frames (generate_segments: features[:, seek:seek + segment_size], pad_or_trim). So rows
+    from len(x16) // 160 on are 0.0 here. n_frames=None returns the content frames alone
+    (the whole-clip features a seek loop slices). zero_pad=False keeps the log-mel of the
+    zero padding instead (the build-defined voice embedding, janus_vocoder_speaker)."""
     x16 = np.asarray(x, np.float32)[::decim].astype(np.float64)
     n_samples = 480000
     padded = np.pad(x16, (0, n_samples))               # faster-whisper: padding=30 s
@@ -36,7 +43,24 @@ def logmel(x, decim=3, filters=None, n_frames=3000):
     lg = np.log10(np.maximum(mel, 1e-10))
     lg = np.maximum(lg, lg.max() - 8.0)
     lg = (lg + 4.0) / 4.0
-    return lg[:n_frames].astype(np.float32)
+    content = len(x16) // 160
+    if not zero_pad:
+        return lg[:n_frames].astype(np.float32)
+    if n_frames is None:
+        return lg[:content].astype(np.float32)
+    out = np.zeros((n_frames, lg.shape[1]), np.float32)
+    k = min(n_frames, content)
+    out[:k] = lg[:k]
+    return out
+
+
+def window(features, seek, n_frames=3000):
+    """generate_segments' window: features[seek:seek + min(3000, content - seek)] padded
+    with zeros to 3000 frames (pad_or_trim)."""
+    size = min(n_frames, len(features) - seek)
+    out = np.zeros((n_frames, features.shape[1]), np.float32)
+    out[:size] = features[seek:seek + size]
+    return out
 
 
 def _t(W, name):
@@ -244,11 +268,12 @@ def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=
     audio16k = np.asarray(audio16k, np.float32)
     tb = tk.timestamp_begin
     content = len(audio16k) // 160
+    features = logmel(audio16k, 1, filters, n_frames=None)   # the whole clip, once
     seek, all_tokens, segs = 0, [], []
     cnt = dict(windows=0, needs_fallback=0, skips=0)
     while seek < content:
         size = min(3000, content - seek)
-        mel = logmel(audio16k[seek * 160:(seek + size) * 160], 1, filters)[None]
+        mel = window(features, seek)[None]
         enc = encoder(mel, W, cfg)
         if enc_fp16:
             enc = enc.half().float()

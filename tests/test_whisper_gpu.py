@@ -62,6 +62,31 @@ def test_logmel(engine, gpu):
         assert err < 2e-3, (b, err)
 
 
+def test_whole_clip_features(engine, gpu):
+    """faster-whisper's features for the seek loop (janus_whisper_logmel_frames): one
+    log-mel of the whole clip normalised over all of its frames (here a 47 s clip whose loud
+    part lies beyond the first 30 s, so the first window's clamp differs from a per-window
+    log-mel), 0.0 from the content end on; and the single-window call pads with zeros."""
+    eng, _ = engine
+    x = np.concatenate([0.05 * synth_speech(40, 30.0, sr=16000), synth_speech(41, 17.0, sr=16000)])
+    x = x.astype(np.float32)
+    c = len(x) // 160
+    pcm, offs = pack([x], gpu)
+    full = eng.logmel_frames(pcm, offs, 1, 1, c + 7)
+    torch.cuda.synchronize()
+    ref = ow.logmel(x, 1, mel_filters(), n_frames=None)
+    got = full[0].float().cpu().numpy()
+    assert np.abs(got[:c] - ref).max() < 2e-3
+    assert not got[c:].any()
+    win0 = ow.logmel(x[:480000], 1, mel_filters())           # per-window scope: different
+    assert np.abs(ow.window(ref, 0) - win0).max() > 0.05
+    short = synth_speech(42, 3.3, sr=16000)
+    pcm2, offs2 = pack([short], gpu)
+    m = eng.logmel(pcm2, offs2, 1, 1)[0].float().cpu().numpy()
+    cs = len(short) // 160
+    assert not m[cs:].any() and np.abs(m[:cs] - ow.logmel(short, 1, mel_filters())[:cs]).max() < 2e-3
+
+
 @pytest.mark.parametrize("which", ["tiny.en", "base.en"])
 def test_encoder(engine, base_engine, gpu, which):
     eng, W = engine if which == "tiny.en" else base_engine
