@@ -36,6 +36,7 @@ PRE_ROLL_CHUNKS = 10          # engine.py:439
 SILENCE_THRESHOLD_CHUNKS = 15  # engine.py:441
 MIN_PHRASE_SAMPLES = CHUNK * 6  # engine.py:504
 CAPTURE_RATE = 48000
+WINDOW_16K = 480000           # one 30 s Whisper window at 16 kHz
 
 class PhraseSegmenter:
     """engine.py:438-506 for one channel: feed every chunk with its gate decision; returns
@@ -125,6 +126,7 @@ class StreamingEncoder:
         self.receiver = receiver    # JanusPipeline-like .decode(packets, frames), or None
         self.asynchronous = asynchronous
         self.max_queue = 0
+        self.long_phrases = 0       # phrases over one 30 s window (full seek loop)
         if asynchronous:
             self._jobs = queue.Queue()
             self._results = queue.Queue()
@@ -271,6 +273,16 @@ class StreamingEncoder:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
         from .pipeline import _texts_and_gates
         texts, _ = _texts_and_gates(w, dec)
+        # a phrase longer than one 30 s window (continuous speech with no 0.5 s pause) gets
+        # the whole seek loop, as the engine's transcribe_buffer call does
+        # (engine.py:514 -> transcriber.py:53-64), instead of its first window only
+        long = [i for i, n in enumerate(lengths) if (n + 2) // 3 > WINDOW_16K]
+        if long:
+            from .services.transcriber import generate_segments
+            auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in long]
+            for i, st in zip(long, generate_segments(w, auds, max_length=self.max_length)):
+                texts[i] = ' '.join(sg.text.strip() for sg in st.segments).strip()
+            self.long_phrases += len(long)
         ts = time.time() if timestamp is None else timestamp
         res = []
         for s, t, g in zip(streams, texts, tags):

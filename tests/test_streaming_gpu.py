@@ -120,6 +120,32 @@ def test_streaming_two_phrases_one_push(gpu, tiny):
     assert max(per.values()) >= 2
 
 
+def test_streaming_long_phrase_full_seek_loop(gpu, tiny):
+    """a phrase longer than one 30 s window (continuous speech, no 0.5 s pause)
+    is transcribed by the whole seek loop, as transcribe_buffer does for the engine
+    (engine.py:514), not truncated to its first window."""
+    from janus_amd.services.transcriber import generate_segments
+    enc = StreamingEncoder(1, tiny, max_length=8)
+    x = synth_speech(880, 33.0)
+    total = (len(x) + 5000 + 48000 + 10 * CHUNK - 1) // (10 * CHUNK) * (10 * CHUNK)
+    audio = np.zeros((1, total), np.float32)
+    audio[0, 5000:5000 + len(x)] = x
+    vad = VoiceActivityDetector()
+    dec = vad.is_speech_batch(torch.from_numpy(audio.reshape(-1, CHUNK)).to(gpu)).reshape(1, -1)
+    got = []
+    for t in range(total // (10 * CHUNK)):
+        got += enc.push(audio[:, t * 10 * CHUNK:(t + 1) * 10 * CHUNK])
+    chunks = [audio[0, i * CHUNK:(i + 1) * CHUNK] for i in range(total // CHUNK)]
+    ref = segment(chunks, list(dec[0]), non_vad=[False] * len(chunks))
+    long_refs = [ph for _, ph in ref if (len(ph) + 2) // 3 > 480000]
+    assert len(long_refs) == 1 and enc.long_phrases == 1
+    st = generate_segments(tiny, [np.ascontiguousarray(long_refs[0][::3])], max_length=8)[0]
+    assert st.windows >= 2
+    want = ' '.join(sg.text.strip() for sg in st.segments).strip()
+    mine = [r for r in got if r["text"] == want]
+    assert len(mine) == 1
+
+
 def test_streaming_text_only_bypasses_gate(gpu, tiny):
     """TEXT_ONLY / MORSE skip the speech gate (engine.py:473-474): every chunk counts as
     speech, so the whole run is one phrase that never closes on silence."""
