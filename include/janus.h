@@ -282,6 +282,23 @@ int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* enc, int ba
                                    int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
                                    float* no_speech_prob, void* stream);
 
+/*
+ * janus_whisper_decode_greedy_ex at temperature > 0: faster-whisper's fallback re-decode
+ * (generate_with_fallback, temperatures 0.2 ... 1.0 with best_of 5: CTranslate2
+ * generate(sampling_temperature=T, sampling_topk=0, num_hypotheses=5); the caller
+ * replicates a window's row per hypothesis). Every token is drawn from softmax(l / T)
+ * over the rule-filtered logits l by Gumbel-max; the noise is a counter-based hash of
+ * (seeds[b], position, token), seeds [host] uint32 [B], so a row's draws are independent
+ * of its batch neighbours and reproducible on the CPU. sum_logprob accumulates the chosen
+ * tokens' log-probabilities under the untempered filtered distribution (the scores
+ * CTranslate2 gathers from its log-softmax). temperature <= 0 or null seeds: error.
+ */
+int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                   const janus_decode_options* opt, const janus_decode_rows* rows,
+                                   float temperature, const uint32_t* seeds, int32_t* tokens,
+                                   int32_t* n_tokens, float* sum_logprob, float* no_speech_prob,
+                                   void* stream);
+
 /* ------------------------------------------------------------ vocoder --- */
 /*
  * Local Firefly-GAN decoder (fish-speech HiFiGANGenerator architecture) replacing the

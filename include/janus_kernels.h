@@ -144,6 +144,15 @@ int janus_decode_attention_f16(const uint16_t* q, int64_t q_bs, const uint16_t* 
 int janus_np_voiced_mean_f32(const float* values, const int64_t* offsets, int batch,
                              float* mean_out, int32_t* count_out, void* stream);
 
+/*
+ * The decoder's sampling noise (janus_whisper_decode_sample_ex): out [batch][V] f32 =
+ * Gumbel(0, 1) draw of token t for row b at position pos, -log(-log u) with u an odd
+ * multiple of 2^-24 from a murmur3-finalised hash of (seeds[b] [device uint32], pos, t).
+ * Lets tests pin the CPU oracle's noise to the device's.
+ */
+int janus_sample_gumbel_f32(const uint32_t* seeds, int batch, int pos, int V, float* out,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,7 @@ SIGNATURES = {
     "janus_prosody_analyze_ex": [_P, _P, _P, _I32, _I64, _I32, _I32, _F32, _F32, _P, _P, _P, _P,
                                  _P, _P, _I32, _P],
     "janus_np_voiced_mean_f32": [_P, _P, _I32, _P, _P, _P],
+    "janus_sample_gumbel_f32": [_P, _I32, _I32, _I32, _P, _P],
     "janus_pack_packet": [ctypes.POINTER(janus_packet), _P, ctypes.c_size_t,
                           ctypes.POINTER(ctypes.c_size_t)],
     "janus_unpack": [_P, ctypes.c_size_t, ctypes.POINTER(janus_mp_node), ctypes.c_size_t,
@@ -74,6 +75,7 @@ SIGNATURES = {
     "janus_whisper_encode": [_P, _P, _I32, _P, _P],
     "janus_whisper_decode_greedy": [_P, _P, _I32, _P, _P, _P, _P, _P],
     "janus_whisper_decode_greedy_ex": [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P],
+    "janus_whisper_decode_sample_ex": [_P, _P, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P],
     "janus_vocoder_create": [_P, _P],
     "janus_vocoder_destroy": [_P],
     "janus_vocoder_set_tensor": [_P, ctypes.c_char_p, _P, _I64],

@@ -11,6 +11,9 @@ struct DecodeRules {
   int no_timestamps;             // <|notimestamps|> (always suppressed in timestamp mode)
   int max_initial_ts;            // max_initial_timestamp index (-1: none)
   int target;                    // token whose raw softmax probability is tracked (no-speech), -1: none
+  float inv_temp;                // 0: greedy (argmax); > 0: sample at temperature 1 / inv_temp
+                                 // (Gumbel-max over the rule-filtered logits, noise from
+                                 // sample_noise(seed of the row, position, token))
 };
 
 // Per-row rule state carried across steps (computed by the selector for the next step).
@@ -28,12 +31,30 @@ struct LogitPart {
   float m_all, s_all;     // max / sum exp(v - m_all) over allowed tokens
   float m_text;           // max over allowed text tokens (< ts_begin)
   float m_ts, s_ts;       // max / sum exp over allowed timestamp tokens
-  float b_all_v; int b_all_i;  // argmax over allowed (first index on ties)
-  float b_ts_v; int b_ts_i;    // argmax over allowed timestamps
+  float b_all_v; int b_all_i;  // argmax over allowed (first index on ties); sampling: of the
+                               // perturbed key logit * inv_temp + gumbel
+  float b_ts_v; int b_ts_i;    // the same over allowed timestamps
   float t_v;              // raw logit of DecodeRules::target (-inf if not in this block)
   float m_raw, s_raw;     // max / sum exp over ALL tokens (unfiltered softmax)
-  float pad;
+  float b_all_r, b_ts_r;  // the logits of b_all_i / b_ts_i (= b_*_v when greedy)
 };
+
+// Sampling noise (decode at temperature > 0): a counter-based hash of (row seed, position,
+// token), so a row's draws do not depend on its batch neighbours or the tile schedule and
+// the CPU oracle can regenerate them (oracle/whisper.py sample_noise).
+__host__ __device__ inline uint32_t noise_mix(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__host__ __device__ inline uint32_t noise_base(uint32_t seed, int pos) {
+  return noise_mix(seed ^ noise_mix((uint32_t)pos * 0x9e3779b9u + 0x7f4a7c15u));
+}
+// uniform u = an odd multiple of 2^-24 in (0, 1), exact in f32; Gumbel(0, 1) = -log(-log u)
+__device__ inline float sample_gumbel(uint32_t base, int token) {
+  const uint32_t h = noise_mix(base ^ ((uint32_t)token * 0x27d4eb2fu));
+  const float u = (float)((h >> 8) | 1u) * 0x1p-24f;
+  return -logf(-logf(u));
+}
 
 void cast_f16_f32_launch(const _Float16* in, float* out, int64_t n, hipStream_t s);
 void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t s);
@@ -65,7 +86,10 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s,
                            const float* lnx = nullptr, int ldx = 0, const float* ln_g = nullptr,
-                           const float* ln_b = nullptr, int max_blocks = 256);
+                           const float* ln_b = nullptr, int max_blocks = 256,
+                           const uint32_t* seeds = nullptr, int pos = 0);
+// R.inv_temp > 0: seeds [B] (device) per-row noise seeds, pos = the position whose logits
+// these are (the sampled token goes to pos + 1)
 // plen [B] (device, nullable = all rows sample from pos + 1 >= 1): rows with pos + 1 <
 // plen[b] are still inside their own prompt and keep the forced token. At a row's first
 // sampled step (pos + 1 == plen[b]) nsp[b] (nullable) gets the raw softmax probability of
@@ -81,5 +105,7 @@ void select_embed_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                          const _Float16* tok_emb, const float* pos_emb, int d, float* x,
                          float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out);
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s);
+// out [B][V] = sample_gumbel(noise_base(seeds[b], pos), t)
+void sample_gumbel_launch(const uint32_t* seeds, int B, int pos, int V, float* out, hipStream_t s);
 
 }  // namespace janus

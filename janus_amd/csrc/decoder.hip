@@ -382,12 +382,17 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
 
 // NB: weight tiles in flight per wave (2: two register sets, the tile two strides ahead is
 // issued after this tile's MFMAs, so each load has two tile-times to land)
-template <int NKS, int NB>  // K / 32
+// SAMPLE (decode at temperature > 0, faster-whisper's fallback): the argmaxes are taken
+// over the perturbed keys logit * inv_temp + Gumbel noise (Gumbel-max: a draw from
+// softmax(logits / T) over the same rule-filtered set), the chosen logit carried beside
+// the key for the log-probability; everything else as in the greedy kernel.
+template <int NKS, int NB, bool SAMPLE>  // K / 32
 __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int V, int B,
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
     LogitPart* __restrict__ parts, int ntiles, const float* __restrict__ lnx, int ldx,
-    const float* __restrict__ ln_g, const float* __restrict__ ln_b, int rot) {
+    const float* __restrict__ ln_g, const float* __restrict__ ln_b, int rot,
+    const uint32_t* __restrict__ seeds, int pos) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   constexpr int K = NKS * 32;
   constexpr int kLgWaves = lg_waves(K);
@@ -450,6 +455,9 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   float ba_v = -INFINITY, bt_v = -INFINITY;
   int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
   float m_raw = -INFINITY, s_raw = 0.f, t_v = -INFINITY;  // unfiltered softmax, target logit
+  float ba_r = -INFINITY, bt_r = -INFINITY;                // logits of the sampled argmaxes
+  uint32_t nb = 0;                                         // row's noise base at this position
+  if constexpr (SAMPLE) nb = noise_base(lane < B ? seeds[lane] : 0u, pos);
   for (int tb = tile0; tb < ntiles; tb += NB * stride) {
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
@@ -524,9 +532,17 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
         for (int c = 0; c < 16; ++c)
           if ((okm >> c) & 1u) u_all += __expf(vals[c] - t_all);
       }
+      if constexpr (SAMPLE) {
+        for (int c = 0; c < 16; ++c) {
+          if (!((okm >> c) & 1u)) continue;
+          const float key = vals[c] * R.inv_temp + sample_gumbel(nb, col0 + c);
+          if (better(key, col0 + c, ba_v, ba_i)) { ba_v = key; ba_i = col0 + c; ba_r = vals[c]; }
+        }
+      } else {
 #pragma unroll
-      for (int c = 0; c < 16; ++c)
-        if (((okm >> c) & 1u) && better(vals[c], col0 + c, ba_v, ba_i)) { ba_v = vals[c]; ba_i = col0 + c; }
+        for (int c = 0; c < 16; ++c)
+          if (((okm >> c) & 1u) && better(vals[c], col0 + c, ba_v, ba_i)) { ba_v = vals[c]; ba_i = col0 + c; }
+      }
     } else {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -553,10 +569,12 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
         const int t = col0 + c;
         const float v = vals[c];
         u_all += __expf(v - t_all);
-        if (better(v, t, ba_v, ba_i)) { ba_v = v; ba_i = t; }
+        // sampling: the key (perturbed logit) is compared, the logit kept beside it
+        const float key = SAMPLE ? v * R.inv_temp + sample_gumbel(nb, t) : v;
+        if (better(key, t, ba_v, ba_i)) { ba_v = key; ba_i = t; ba_r = v; }
         if (R.ts_begin >= 0 && t >= R.ts_begin) {
           u_ts += __expf(v - t_ts);
-          if (better(v, t, bt_v, bt_i)) { bt_v = v; bt_i = t; }
+          if (better(key, t, bt_v, bt_i)) { bt_v = key; bt_i = t; bt_r = v; }
         }
       }
     }
@@ -573,7 +591,8 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   {
     LogitPart p;
     p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
-    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i; p.pad = 0.f;
+    p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i;
+    p.b_all_r = SAMPLE ? ba_r : ba_v; p.b_ts_r = SAMPLE ? bt_r : bt_v;
     p.t_v = t_v; p.m_raw = m_raw; p.s_raw = s_raw;
     wp[w * 64 + lane] = p;
   }
@@ -586,8 +605,8 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
       q.s_all = lse_merge(q.m_all, q.s_all, p.m_all, p.s_all, &mo); q.m_all = mo;
       q.s_ts = lse_merge(q.m_ts, q.s_ts, p.m_ts, p.s_ts, &mo); q.m_ts = mo;
       q.m_text = fmaxf(q.m_text, p.m_text);
-      if (better(p.b_all_v, p.b_all_i, q.b_all_v, q.b_all_i)) { q.b_all_v = p.b_all_v; q.b_all_i = p.b_all_i; }
-      if (better(p.b_ts_v, p.b_ts_i, q.b_ts_v, q.b_ts_i)) { q.b_ts_v = p.b_ts_v; q.b_ts_i = p.b_ts_i; }
+      if (better(p.b_all_v, p.b_all_i, q.b_all_v, q.b_all_i)) { q.b_all_v = p.b_all_v; q.b_all_i = p.b_all_i; q.b_all_r = p.b_all_r; }
+      if (better(p.b_ts_v, p.b_ts_i, q.b_ts_v, q.b_ts_i)) { q.b_ts_v = p.b_ts_v; q.b_ts_i = p.b_ts_i; q.b_ts_r = p.b_ts_r; }
       q.s_raw = lse_merge(q.m_raw, q.s_raw, p.m_raw, p.s_raw, &mo); q.m_raw = mo;
       q.t_v = fmaxf(q.t_v, p.t_v);
     }
@@ -600,19 +619,24 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
 void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K, int V, int B,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s, const float* lnx, int ldx,
-                           const float* ln_g, const float* ln_b, int max_blocks) {
+                           const float* ln_g, const float* ln_b, int max_blocks,
+                           const uint32_t* seeds, int pos) {
   JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
+  const bool sample = R.inv_temp > 0.f;
+  JANUS_CHECK(!sample || seeds, "logits: sampling needs per-row seeds");
   const int ntiles = (V + 15) / 16;
   const int nw = lg_waves(K);
   const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)nw * 64 * 17 * 4 + 64 * sizeof(RowRules);
   // weight tiles in flight per wave (JANUS_LG_DEPTH=2: two)
   static const int depth = std::getenv("JANUS_LG_DEPTH") ? std::atoi(std::getenv("JANUS_LG_DEPTH")) : 1;
-  auto kern = depth > 1 ? (K == 384 ? logits_partial_kernel<12, 2> : K == 512 ? logits_partial_kernel<16, 2>
-                                                                            : logits_partial_kernel<24, 1>)
-                        : (K == 384 ? logits_partial_kernel<12, 1> : K == 512 ? logits_partial_kernel<16, 1>
-                                                                            : logits_partial_kernel<24, 1>);
-  static bool attr[6] = {false, false, false, false, false, false};
-  const int ai = (K == 384 ? 0 : K == 512 ? 1 : 2) + (depth > 1 ? 3 : 0);
+  auto kern = sample ? (K == 384 ? logits_partial_kernel<12, 1, true> : K == 512 ? logits_partial_kernel<16, 1, true>
+                                                                          : logits_partial_kernel<24, 1, true>)
+              : depth > 1 ? (K == 384 ? logits_partial_kernel<12, 2, false> : K == 512 ? logits_partial_kernel<16, 2, false>
+                                                                            : logits_partial_kernel<24, 1, false>)
+                        : (K == 384 ? logits_partial_kernel<12, 1, false> : K == 512 ? logits_partial_kernel<16, 1, false>
+                                                                            : logits_partial_kernel<24, 1, false>);
+  static bool attr[9] = {false, false, false, false, false, false, false, false, false};
+  const int ai = (K == 384 ? 0 : K == 512 ? 1 : 2) + (sample ? 6 : depth > 1 ? 3 : 0);
   if (!attr[ai]) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
@@ -639,7 +663,8 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
     kern<<<grid, nw * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
                                           smask, rules + r0, parts + (int64_t)r0 * grid, ntiles,
-                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b, rot);
+                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b, rot,
+                                          seeds ? seeds + r0 : nullptr, pos);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -666,6 +691,7 @@ __device__ __forceinline__ int select_row(
   float ba_v = -INFINITY, bt_v = -INFINITY;
   int ba_i = 0x7fffffff, bt_i = 0x7fffffff;
   float m_raw = -INFINITY, s_raw = 0.f, t_v = -INFINITY;
+  float ba_r = -INFINITY, bt_r = -INFINITY;
   const LogitPart* pr = parts + (int64_t)b * nblk;
   for (int i = tid; i < nblk; i += 256) {
     const LogitPart p = pr[i];
@@ -675,8 +701,8 @@ __device__ __forceinline__ int select_row(
     s_raw = lse_merge(m_raw, s_raw, p.m_raw, p.s_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, p.m_text);
     t_v = fmaxf(t_v, p.t_v);
-    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
-    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
+    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; ba_r = p.b_all_r; }
+    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; bt_r = p.b_ts_r; }
   }
   for (int o = 32; o > 0; o >>= 1) {
     float mo;
@@ -689,15 +715,17 @@ __device__ __forceinline__ int select_row(
     m_text = fmaxf(m_text, __shfl_xor(m_text, o));
     t_v = fmaxf(t_v, __shfl_xor(t_v, o));
     const float av = __shfl_xor(ba_v, o); const int ai = __shfl_xor(ba_i, o);
-    if (better(av, ai, ba_v, ba_i)) { ba_v = av; ba_i = ai; }
+    const float ar = __shfl_xor(ba_r, o);
+    if (better(av, ai, ba_v, ba_i)) { ba_v = av; ba_i = ai; ba_r = ar; }
     const float tv = __shfl_xor(bt_v, o); const int ti = __shfl_xor(bt_i, o);
-    if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; }
+    const float tr = __shfl_xor(bt_r, o);
+    if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; bt_r = tr; }
   }
   if (lane == 0) {
     LogitPart p;
     p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;
     p.b_all_v = ba_v; p.b_all_i = ba_i; p.b_ts_v = bt_v; p.b_ts_i = bt_i;
-    p.t_v = t_v; p.m_raw = m_raw; p.s_raw = s_raw; p.pad = 0.f;
+    p.t_v = t_v; p.m_raw = m_raw; p.s_raw = s_raw; p.b_all_r = ba_r; p.b_ts_r = bt_r;
     sh[w] = p;
   }
   __syncthreads();
@@ -710,20 +738,21 @@ __device__ __forceinline__ int select_row(
     s_raw = lse_merge(m_raw, s_raw, p.m_raw, p.s_raw, &mo); m_raw = mo;
     m_text = fmaxf(m_text, p.m_text);
     t_v = fmaxf(t_v, p.t_v);
-    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; }
-    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; }
+    if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; ba_r = p.b_all_r; }
+    if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; bt_r = p.b_ts_r; }
   }
   // no_speech_prob: the raw softmax probability of the target token at the row's first
   // sampled step (logits at the <|startoftranscript|> position, before any filter)
   if (nsp && pos + 1 == pl) nsp[b] = R.target >= 0 ? __expf(t_v - (m_raw + __logf(s_raw))) : 0.f;
   const float lse_all = m_all + __logf(s_all);
+  // the chosen token's log-probability uses its logit (b_*_r; = the key when greedy)
   int next = ba_i;
-  float lp = ba_v - lse_all;
+  float lp = ba_r - lse_all;
   if (R.ts_begin >= 0 && m_ts > -INFINITY) {
     const float lse_ts = m_ts + __logf(s_ts);
     if (lse_ts - lse_all > m_text - lse_all) {  // timestamp mass beats every text token
       next = bt_i;
-      lp = bt_v - lse_ts;
+      lp = bt_r - lse_ts;
     }
   }
   row_tok[pos + 1] = next;
@@ -786,6 +815,20 @@ void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules&
                             const int32_t* plen, float* nsp) {
   select_partials_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp,
                                            n_tok, plen, nsp);
+  JANUS_LAUNCH_CHECK();
+}
+
+// The sampling noise the SAMPLE logits kernel adds, written out (kernel-level ABI
+// janus_sample_gumbel_f32: the CPU oracle's restatement is checked against it)
+__global__ void sample_gumbel_kernel(const uint32_t* __restrict__ seeds, int pos, int V,
+                                     float* __restrict__ out) {
+  const int b = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < V) out[(int64_t)b * V + t] = sample_gumbel(noise_base(seeds[b], pos), t);
+}
+
+void sample_gumbel_launch(const uint32_t* seeds, int B, int pos, int V, float* out, hipStream_t s) {
+  JANUS_CHECK(B >= 1 && V >= 1, "sample_gumbel: empty shape");
+  sample_gumbel_kernel<<<dim3((unsigned)cdiv(V, 256), (unsigned)B), 256, 0, s>>>(seeds, pos, V, out);
   JANUS_LAUNCH_CHECK();
 }
 

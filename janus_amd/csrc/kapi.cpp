@@ -1,5 +1,6 @@
 // Kernel-level C-ABI (include/janus_kernels.h): thin wrappers over the launchers.
 #include "kernels.h"
+#include "decoder.h"
 #include "../../include/janus_kernels.h"
 
 namespace janus {
@@ -192,5 +193,13 @@ extern "C" int janus_decode_attention_f16(const uint16_t* q, int64_t q_bs, const
                                   reinterpret_cast<const _Float16*>(v), kv_bs, kv_rs, Tkv,
                                   reinterpret_cast<_Float16*>(out), o_bs, batch, H, scale, part_o,
                                   part_ml, (hipStream_t)stream);
+  });
+}
+
+extern "C" int janus_sample_gumbel_f32(const uint32_t* seeds, int batch, int pos, int V, float* out,
+                                       void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(seeds && out, "null argument");
+    sample_gumbel_launch(seeds, batch, pos, V, out, (hipStream_t)stream);
   });
 }

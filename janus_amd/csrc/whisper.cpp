@@ -64,7 +64,7 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   hipStream_t stream = nullptr;  // graph capture needs a non-null stream
   std::vector<uint32_t> stream_mask;  // CU mask the lane stream was created with (empty: none)
@@ -275,9 +275,24 @@ static void encode(janus_whisper* w, const _Float16* mel, int B, _Float16* out, 
                    w->params.get("encoder.layer_norm.bias", d), out, (int)M, d, 1e-5f, s);
 }
 
+static uint32_t float_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, sizeof(u));
+  return u;
+}
+
+// Sampling (faster-whisper's temperature fallback, CTranslate2 generate(sampling_temperature=
+// T, sampling_topk=0)): temperature > 0 draws each token from softmax(filtered logits / T)
+// by Gumbel-max with per-row counter-based noise (seeds [host] uint32 [B]); null = greedy.
+struct DecodeSampling {
+  float temperature;
+  const uint32_t* seeds;
+};
+
 static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, int B, const janus_decode_options* opt,
                           const janus_decode_rows* rows, int32_t* tokens_out, int32_t* n_tokens_out,
-                          float* sum_lp_out, float* nsp_out, hipStream_t s, LaneLatch* latch) {
+                          float* sum_lp_out, float* nsp_out, hipStream_t s, LaneLatch* latch,
+                          const DecodeSampling* smp = nullptr) {
   LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
@@ -361,6 +376,12 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // synchronous uploads: the host vectors die with this call
   JANUS_HIP(hipMemcpyAsync(Z.d_prompt.p, h_plen.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
   JANUS_HIP(hipMemcpyAsync(tokens, h_init.data(), sizeof(int32_t) * h_init.size(), hipMemcpyHostToDevice, s));
+  const bool sampling = smp && smp->temperature > 0.f;
+  Z.d_seed.ensure(sizeof(uint32_t) * B);
+  if (sampling) {
+    JANUS_CHECK(smp->seeds, "decode: sampling needs per-row seeds");
+    JANUS_HIP(hipMemcpyAsync(Z.d_seed.p, smp->seeds, sizeof(uint32_t) * B, hipMemcpyHostToDevice, s));
+  }
   if (opt->n_suppress > 0)
     JANUS_HIP(hipMemcpyAsync(Z.d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
                              hipMemcpyHostToDevice, s));
@@ -400,6 +421,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   R.no_timestamps = opt->no_timestamps;
   R.max_initial_ts = opt->max_initial_timestamp_index;
   R.target = rows ? rows->no_speech_token : -1;
+  R.inv_temp = sampling ? 1.0f / smp->temperature : 0.f;
   const float scale = 0.125f;
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
@@ -571,7 +593,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     if (!ln_fuse && !lnp_fin) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
-                          lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap);
+                          lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap,
+                          sampling ? Z.d_seed.as<uint32_t>() : nullptr, pos);
     if (fuse_se && pos + 1 < maxlen - 1)
       select_embed_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
@@ -593,7 +616,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)Z.d_rules.p, (int64_t)Z.d_lnp.p, (int64_t)fused_ln, (int64_t)ln_fuse, (int64_t)ln_pro_mask, (int64_t)embed_ln, (int64_t)rln, (int64_t)cvp, (int64_t)fuse_se, (int64_t)nblk, (int64_t)msplit_n, (int64_t)Z.d_lncnt.p, (int64_t)xabs, (int64_t)xsplit, (int64_t)Z.d_xqk.p,
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
-      R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p};
+      R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
+      (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -733,11 +757,39 @@ extern "C" int janus_whisper_decode_greedy(janus_whisper* w, const uint16_t* enc
                                         nullptr, stream);
 }
 
+static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
+                        const janus_decode_options* opt, const janus_decode_rows* rows,
+                        int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
+                        float* no_speech_prob, void* stream, const DecodeSampling* smp);
+
 extern "C" int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* enc, int batch,
                                               const janus_decode_options* opt,
                                               const janus_decode_rows* rows, int32_t* tokens,
                                               int32_t* n_tokens, float* sum_logprob,
                                               float* no_speech_prob, void* stream) {
+  return decode_entry(w, enc, batch, opt, rows, tokens, n_tokens, sum_logprob, no_speech_prob, stream,
+                      nullptr);
+}
+
+extern "C" int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                              const janus_decode_options* opt,
+                                              const janus_decode_rows* rows, float temperature,
+                                              const uint32_t* seeds, int32_t* tokens,
+                                              int32_t* n_tokens, float* sum_logprob,
+                                              float* no_speech_prob, void* stream) {
+  if (!(temperature > 0.f) || !seeds) {
+    set_error("decode_sample: temperature must be > 0 and seeds non-null");
+    return -1;
+  }
+  const DecodeSampling smp{temperature, seeds};
+  return decode_entry(w, enc, batch, opt, rows, tokens, n_tokens, sum_logprob, no_speech_prob, stream,
+                      &smp);
+}
+
+static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
+                        const janus_decode_options* opt, const janus_decode_rows* rows,
+                        int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
+                        float* no_speech_prob, void* stream, const DecodeSampling* smp) {
   return guarded([&] {
     JANUS_CHECK(w && enc && opt && tokens && n_tokens && sum_logprob, "null argument");
     JANUS_CHECK(batch >= 1, "decode: batch must be >= 1");
@@ -755,7 +807,7 @@ extern "C" int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* 
     while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
     if (nlanes == 1 && s != nullptr) {
       decode_greedy(w, *w->lanes[0], e, batch, opt, rows, tokens, n_tokens, sum_logprob,
-                    no_speech_prob, s, nullptr);
+                    no_speech_prob, s, nullptr, smp);
       return;
     }
     // the null stream cannot be captured, and lanes run concurrently: each lane gets its
@@ -812,10 +864,12 @@ extern "C" int janus_whisper_decode_greedy_ex(janus_whisper* w, const uint16_t* 
             sub.prompt_lens = rows->prompt_lens + b0;
           }
         }
+        DecodeSampling ssub{};
+        if (smp) ssub = DecodeSampling{smp->temperature, smp->seeds + b0};
         decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, opt,
                       rows ? &sub : nullptr, tokens + (int64_t)b0 * maxlen, n_tokens + b0,
                       sum_logprob + b0, no_speech_prob ? no_speech_prob + b0 : nullptr, Z.stream,
-                      nlanes > 1 ? &latch : nullptr);
+                      nlanes > 1 ? &latch : nullptr, smp ? &ssub : nullptr);
       } catch (const std::exception& ex) {
         errs[i] = ex.what();
       } catch (...) {

@@ -23,11 +23,20 @@ call (beam_size=1, language='en', every other option at its default):
   no-speech skip when no_speech_prob > 0.6 and avg_logprob <= -1;
 * segments whose start equals their end or whose text is blank are dropped.
 
-Deliberate deviations: the temperature FALLBACK is not run — a window
-whose gates fail (compression ratio > 2.4 or avg_logprob < -1, outside the no-speech
-case) is flagged (``Segment.needs_fallback``, ``WhisperModel.stats``) and its T = 0
-decode kept, because the T > 0 re-decodes are random samples no offline oracle can pin;
-a window that would not advance the seek (a leading <|0.00|><|0.00|>) advances by the
+* the temperature FALLBACK (``generate_with_fallback``): a window whose gates fail
+  (compression ratio > 2.4 or avg_logprob < -1, outside the no-speech case) is re-decoded
+  at T = 0.2, 0.4, ... 1.0 with best_of = 5 sampled hypotheses (the best by
+  sum-log-prob / length kept, as CTranslate2 orders them) until one passes; when none
+  does, the result with the highest avg_logprob among those under the compression
+  threshold (else among all) is kept and reported at T = 1.0; a final temperature above
+  ``prompt_reset_on_temperature`` (0.5) resets the conditioning prompt. The hypotheses of
+  all failing windows of a round are decoded as one GPU batch (``janus_whisper_decode_
+  sample_ex``: Gumbel-max over the rule-filtered logits / T). Sampling noise comes from
+  a counter-based hash seeded per (utterance, window, temperature, hypothesis)
+  (``fallback_seed``), so a run is reproducible and the CPU oracle draws the same noise —
+  CTranslate2's own random draws cannot be reproduced offline.
+
+A window that would not advance the seek (a leading <|0.00|><|0.00|>) advances by the
 window size, so the loop always terminates.
 
 Features are faster-whisper's: one log-mel of the whole clip (normalised with the maximum
@@ -54,6 +63,28 @@ INPUT_STRIDE = 2         # mel frames per timestamp step
 COMPRESSION_RATIO_THRESHOLD = 2.4
 LOG_PROB_THRESHOLD = -1.0
 NO_SPEECH_THRESHOLD = 0.6
+TEMPERATURES = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0)   # faster-whisper transcribe(temperature=...)
+BEST_OF = 5
+PROMPT_RESET_ON_TEMPERATURE = 0.5
+FALLBACK_ROWS = 60       # hypotheses per sampling decode (12 windows x 5; B <= 64 keeps
+                         # the absorbed cross-attention path)
+
+
+def _mix32(h: int) -> int:
+    h &= 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def fallback_seed(utt: int, window: int, temp_index: int, hyp: int) -> int:
+    """uint32 noise seed of one sampled hypothesis: utterance (index in the call), window
+    (counter within the utterance), temperature index (1..5), hypothesis (0..best_of-1)."""
+    return _mix32(0x4A414E55 ^ _mix32(utt * 0x01000193 + window * 0x9E3779B1 +
+                                      temp_index * 0x85EBCA77 + hyp))
 
 
 @dataclasses.dataclass
@@ -68,7 +99,58 @@ class Segment:
     avg_logprob: float
     compression_ratio: float
     no_speech_prob: float
-    needs_fallback: bool = False
+    needs_fallback: bool = False   # the T = 0 decode failed its gates (fallback entered)
+
+
+@dataclasses.dataclass
+class Candidate:
+    """One decode result of a window (generate_with_fallback's decode_result)."""
+    tokens: list
+    avg_logprob: float
+    no_speech_prob: float
+    temperature: float
+    text: str
+    compression_ratio: float
+    needs_fallback: bool
+
+
+def candidate(tk, toks, avg_lp, nsp, temperature) -> Candidate:
+    text = tk.decode(toks).strip()
+    return Candidate(list(toks), float(avg_lp), float(nsp), float(temperature), text,
+                     compression_ratio(text), gates(text, avg_lp, nsp)[0])
+
+
+def best_hypothesis(rows):
+    """CTranslate2's first hypothesis of a sampled best_of group: the highest score
+    sum-log-prob / length (length_penalty 1; sequences without <|endoftext|>), the first on
+    ties. rows: [(tokens, avg_logprob, nsp)] as DecodeOut.rows() gives them."""
+    def score(r):
+        toks, avg, _ = r
+        return avg * (len(toks) + 1) / max(len(toks), 1)
+    best = 0
+    for i in range(1, len(rows)):
+        if score(rows[i]) > score(rows[best]):
+            best = i
+    return rows[best]
+
+
+def settle(results, temperatures=TEMPERATURES):
+    """generate_with_fallback's choice over a window's results in temperature order: the
+    first that passes its gates; if none does (every temperature tried), the highest
+    avg_logprob among those under the compression-ratio threshold (else among all),
+    reported at the last temperature. None while the fallback is still running."""
+    for r in results:
+        if not r.needs_fallback:
+            return r
+    if len(results) < len(temperatures):
+        return None
+    below = [r for r in results if not r.compression_ratio > COMPRESSION_RATIO_THRESHOLD]
+    pool = below or results
+    best = pool[0]
+    for r in pool[1:]:
+        if r.avg_logprob > best.avg_logprob:
+            best = r
+    return dataclasses.replace(best, temperature=float(temperatures[-1]))
 
 
 @dataclasses.dataclass
@@ -147,6 +229,7 @@ class _Stream:
         self.prompt_reset_since = 0
         self.segments = []
         self.windows = self.fallbacks = self.skips = 0
+        self.fallback_decodes = 0      # sampled decodes (temperature steps) run
 
     @property
     def active(self):
@@ -161,10 +244,46 @@ class _Stream:
         return p + list(tk.sot_sequence)
 
 
-def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448):
+def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of):
+    """Run the temperature fallback for the windows of one round: first [Candidate] (T = 0
+    results), keys [(utt, window)]; returns each window's settled Candidate. The
+    hypotheses of every window still failing at a temperature go out as one sampled batch
+    (chunks of FALLBACK_ROWS rows)."""
+    results = [[c] for c in first]
+    final = [settle(r, temperatures) if not r[0].needs_fallback else None for r in results]
+    per = max(1, FALLBACK_ROWS // best_of)
+    for ti in range(1, len(temperatures)):
+        T = float(temperatures[ti])
+        pend = [j for j in range(len(first)) if final[j] is None]
+        if not pend:
+            break
+        for c0 in range(0, len(pend), per):
+            js = pend[c0:c0 + per]
+            idx = torch.tensor(js, device=enc.device).repeat_interleave(best_of)
+            rows_enc = enc.index_select(0, idx).contiguous()
+            rows_prompts = [prompts[j] for j in js for _ in range(best_of)]
+            seeds = [fallback_seed(keys[j][0], keys[j][1], ti, h) for j in js for h in range(best_of)]
+            out = engine.decode_ex(rows_enc, prompts=rows_prompts, max_length=max_length,
+                                   temperature=T, seeds=seeds).rows()
+            for k, j in enumerate(js):
+                toks, avg_lp, nsp = best_hypothesis(out[k * best_of:(k + 1) * best_of])
+                results[j].append(candidate(tk, toks, avg_lp, nsp, T))
+        for j in pend:
+            if not results[j][-1].needs_fallback or ti == len(temperatures) - 1:
+                final[j] = settle(results[j], temperatures)
+    return final, [len(r) - 1 for r in results]
+
+
+def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448,
+                      temperatures=TEMPERATURES, best_of: int = BEST_OF):
     """faster-whisper's seek loop for several 16 kHz utterances at once: every round
     decodes the current window of each unfinished utterance as one GPU batch (per-row
-    prompts). Returns one _Stream (segments + gate counters) per utterance."""
+    prompts), then the temperature fallback of the windows whose gates failed
+    (``temperatures`` = (0.0,) disables it). Returns one _Stream (segments + gate counters)
+    per utterance."""
+    temperatures = tuple(float(t) for t in temperatures)
+    if not temperatures or temperatures[0] != 0.0:
+        raise NotImplementedError("the first temperature must be 0 (faster-whisper's default)")
     tk = engine.tokenizer
     dev = engine.device
     streams = [_Stream(np.asarray(a, np.float32)) for a in audios]
@@ -189,29 +308,38 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
             for j, (i, s, size) in enumerate(zip(idx, grp, sizes)):
                 mel[j, :size] = feats[i][s.seek:s.seek + size]      # pad_or_trim: zeros after
             enc = engine.encode(mel)
-            out = engine.decode_ex(enc, prompts=[s.prompt(tk, max_length) for s in grp], max_length=max_length)
-            wins = [(size, None) for size in sizes]
-            for s, (size, _), (toks, avg_lp, nsp) in zip(grp, wins, out.rows()):
+            prompts = [s.prompt(tk, max_length) for s in grp]
+            out = engine.decode_ex(enc, prompts=prompts, max_length=max_length)
+            first = [candidate(tk, toks, avg_lp, nsp, 0.0) for (toks, avg_lp, nsp) in out.rows()]
+            keys = [(i, s.windows) for i, s in zip(idx, grp)]
+            if len(temperatures) > 1:
+                final, ndec = _fallback(engine, tk, enc, prompts, first, keys, max_length,
+                                        temperatures, best_of)
+            else:
+                final, ndec = first, [0] * len(first)
+            for s, size, c0r, r, nd in zip(grp, sizes, first, final, ndec):
                 s.windows += 1
-                text = tk.decode(toks).strip()
-                cr = compression_ratio(text)
-                needs, skip = gates(text, avg_lp, nsp)
-                s.fallbacks += int(needs)
-                if skip:
+                s.fallbacks += int(c0r.needs_fallback)
+                s.fallback_decodes += nd
+                # no-speech skip on the settled result (generate_segments after the fallback)
+                if r.no_speech_prob > NO_SPEECH_THRESHOLD and not r.avg_logprob > LOG_PROB_THRESHOLD:
                     s.skips += 1
                     s.seek += size
                     continue
-                segs, nseek = split_window(tk, toks, s.seek, size)
+                segs, nseek = split_window(tk, r.tokens, s.seek, size)
                 for (st, en, part) in segs:
                     txt = tk.decode(part)
                     if st == en or not txt.strip():
                         continue
                     s.all_tokens.extend(part)
-                    s.segments.append(Segment(len(s.segments), s.seek, st, en, txt, part, 0.0,
-                                              avg_lp, cr, nsp, needs))
+                    s.segments.append(Segment(len(s.segments), s.seek, st, en, txt, part,
+                                              r.temperature, r.avg_logprob, r.compression_ratio,
+                                              r.no_speech_prob, c0r.needs_fallback))
                 s.seek = nseek
-                # condition_on_previous_text at temperature 0 <= prompt_reset_on_temperature:
-                # the prompt is never reset
+                # condition_on_previous_text: a result settled above
+                # prompt_reset_on_temperature restarts the prompt after these segments
+                if r.temperature > PROMPT_RESET_ON_TEMPERATURE:
+                    s.prompt_reset_since = len(s.all_tokens)
     return streams
 
 
@@ -236,9 +364,10 @@ class WhisperModel:
         self.model_size = model_size
         self.requested_device, self.requested_compute_type = device, compute_type
         self.engine = WhisperEngine(CONFIGS[model_size])
-        self.stats = {"windows": 0, "needs_fallback": 0, "no_speech_skips": 0}
+        self.stats = {"windows": 0, "needs_fallback": 0, "no_speech_skips": 0, "fallback_decodes": 0}
 
-    def transcribe(self, audio, beam_size: int = 1, language: str = "en", **_ignored):
+    def transcribe(self, audio, beam_size: int = 1, language: str = "en",
+                   temperature=TEMPERATURES, best_of: int = BEST_OF, **_ignored):
         if beam_size != 1:
             raise NotImplementedError("janus_amd decodes greedily (beam_size=1, transcriber.py:55)")
         if language not in (None, "en"):
@@ -246,7 +375,8 @@ class WhisperModel:
         if isinstance(audio, str):
             audio = read_wav_16k(audio)
         audio = np.ascontiguousarray(audio, dtype=np.float32)
-        st = generate_segments(self.engine, [audio])[0]
+        temps = (float(temperature),) if np.isscalar(temperature) else tuple(temperature)
+        st = generate_segments(self.engine, [audio], temperatures=temps, best_of=best_of)[0]
         self._count(st)
         info = TranscriptionInfo("en", 1.0, len(audio) / 16000.0)
         return iter(st.segments), info
@@ -255,6 +385,7 @@ class WhisperModel:
         self.stats["windows"] += st.windows
         self.stats["needs_fallback"] += st.fallbacks
         self.stats["no_speech_skips"] += st.skips
+        self.stats["fallback_decodes"] += st.fallback_decodes
 
 
 class Transcriber:
@@ -302,4 +433,6 @@ class Transcriber:
 
 
 __all__ = ["Transcriber", "WhisperModel", "Segment", "TranscriptionInfo", "read_wav_16k",
-           "generate_segments", "split_window", "compression_ratio", "gates", "nat"]
+           "generate_segments", "split_window", "compression_ratio", "gates", "nat",
+           "Candidate", "candidate", "best_hypothesis", "settle", "fallback_seed", "TEMPERATURES",
+           "BEST_OF"]

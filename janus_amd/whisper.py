@@ -310,10 +310,16 @@ class WhisperEngine:
 
     def decode_ex(self, enc: torch.Tensor, prompts=None, max_length: int = 448,
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
-                  cu_count: int = 0):
+                  cu_count: int = 0, temperature: float = 0.0, seeds=None):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
-        SOT sequence for every row) and the no-speech probability. Returns a DecodeOut."""
+        SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
+        temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
+        rule-filtered logits / T with per-row uint32 ``seeds``)."""
         B = enc.shape[0]
+        if temperature > 0:
+            if seeds is None or len(seeds) != B:
+                raise ValueError("sampling needs one uint32 seed per row")
+            sd = np.ascontiguousarray(np.asarray(seeds, np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
@@ -333,9 +339,15 @@ class WhisperEngine:
         ntok = torch.empty(B, dtype=torch.int32, device=self.device)
         slp = torch.empty(B, dtype=torch.float32, device=self.device)
         nsp = torch.empty(B, dtype=torch.float32, device=self.device)
-        nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
-                 ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
-                 nsp.data_ptr(), nat.stream_ptr())
+        if temperature > 0:
+            nat.call("janus_whisper_decode_sample_ex", self._h, enc.data_ptr(), B,
+                     ctypes.addressof(opt), ctypes.addressof(rows), ctypes.c_float(temperature),
+                     sd.ctypes.data, tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
+                     nsp.data_ptr(), nat.stream_ptr())
+        else:
+            nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
+                     ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
+                     nsp.data_ptr(), nat.stream_ptr())
         del keep, pr
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 

@@ -11,8 +11,17 @@ faster-whisper WhisperModel.transcribe(audio[::3], beam_size=1, language='en')):
   pinned against transformers' WhisperModel loaded with the same weights.
 * ``greedy``: temperature-0 decoding with OpenAI's SuppressBlank, SuppressTokens and
   ApplyTimestampRules (incl. max_initial_timestamp 1.0 s) that CTranslate2 applies for
-  faster-whisper; parity unpinned against faster-whisper itself (not installed, no
-  weights offline) — its rule code is restated from openai/whisper decoding.py.
+  faster-whisper; the rules are pinned to transformers' logits processors
+  (tests/test_oracle_whisper.py).
+* ``greedy_cached(temperature > 0, seeds)``: sampling as the build defines it for
+  faster-whisper's temperature fallback (generate_with_fallback): Gumbel-max over the
+  rule-filtered logits / T with the counter-based noise of ``sample_noise`` (the same hash
+  as decoder.h noise_base / sample_gumbel). CTranslate2's own random draws cannot be
+  reproduced offline, so the draws are build-defined; the distribution is softmax(l / T)
+  over the filtered set either way.
+* ``transcribe_segments``: generate_segments with the fallback loop
+  (generate_with_fallback: temperatures 0.2 ... 1.0, best_of 5, settle rules,
+  prompt_reset_on_temperature 0.5), restated from faster-whisper 1.x transcribe.py.
 """
 import math
 
@@ -130,6 +139,27 @@ def decoder_logits(tokens, enc, W, cfg):
     return x @ _t(W, "decoder.embed_tokens.weight").T
 
 
+def _mix32(h):
+    """murmur3 finaliser on uint32 numpy arrays (decoder.h noise_mix)."""
+    h = np.asarray(h, np.uint32).copy()
+    h ^= h >> np.uint32(16)
+    h *= np.uint32(0x85EBCA6B)
+    h ^= h >> np.uint32(13)
+    h *= np.uint32(0xC2B2AE35)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def sample_noise(seed, pos, V):
+    """Gumbel(0, 1) noise [V] (float64) of one row at one position: decoder.h
+    noise_base(seed, pos) mixed with each token id, u = odd multiple of 2^-24."""
+    with np.errstate(over="ignore"):
+        base = _mix32(np.uint32(seed) ^ _mix32(np.uint32((pos * 0x9E3779B9 + 0x7F4A7C15) & 0xFFFFFFFF)))
+        h = _mix32(base ^ (np.arange(V, dtype=np.uint32) * np.uint32(0x27D4EB2F)))
+    u = ((h >> np.uint32(8)) | np.uint32(1)).astype(np.float64) * 2.0 ** -24
+    return -np.log(-np.log(u))
+
+
 def apply_rules(logits, sampled, tk, suppress, max_initial=50, timestamps=True):
     """OpenAI decoding filters on one row of logits (numpy f64, modified copy) given the
     tokens sampled so far (after the prompt). Returns (filtered logits, log-probs)."""
@@ -167,14 +197,18 @@ def apply_rules(logits, sampled, tk, suppress, max_initial=50, timestamps=True):
 
 
 @torch.no_grad()
-def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True, prompts=None, no_speech=None):
+def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True, prompts=None, no_speech=None,
+                  temperature=0.0, seeds=None):
     """Batched greedy decode with per-layer K/V caches (fp32), the same algorithm as
     ``greedy`` (one full forward per step) at O(T) per step instead of O(T^2):
     enc [B][1500][d] -> per row a dict(tokens=[sampled incl. eot], margins=[top-2 gap
     of the rule-filtered logits per step], sum_lp=float, nsp=float). Rows that emitted
     eot stop. ``prompts``: per-row prompt token lists (default the SOT sequence); row b
     samples from position len(prompts[b]) on. ``no_speech``: token whose raw softmax
-    probability at the row's first sampled step is reported as nsp."""
+    probability at the row's first sampled step is reported as nsp. ``temperature`` > 0:
+    sample (Gumbel-max, key = filtered logit * f32(1/T) + sample_noise(seeds[b], pos));
+    margins are then the top-2 gaps of the keys and sum_lp the untempered log-probs."""
+    inv_t = float(np.float32(1.0) / np.float32(temperature)) if temperature > 0 else 0.0
     enc = torch.as_tensor(enc, dtype=torch.float32)
     B, Te, d = enc.shape
     H, hd = cfg.n_heads, d // cfg.n_heads
@@ -227,6 +261,8 @@ def greedy_cached(enc, W, cfg, tk, max_length=448, timestamps=True, prompts=None
                 raw = logits[b].astype(np.float64)
                 out[b]["nsp"] = float(np.exp(raw[no_speech] - raw.max()) / np.exp(raw - raw.max()).sum())
             L, lp = apply_rules(logits[b], out[b]["tokens"], tk, suppress, timestamps=timestamps)
+            if inv_t > 0:
+                L = np.where(np.isfinite(L), L * inv_t + sample_noise(seeds[b], pos, len(L)), -np.inf)
             nxt = int(np.argmax(L))
             top2 = np.partition(L[np.isfinite(L)], -2)[-2:] if np.isfinite(L).sum() >= 2 else [L.max(), -np.inf]
             out[b]["margins"].append(float(top2[-1] - top2[-2]))
@@ -258,39 +294,79 @@ def greedy(enc, W, cfg, tk, max_length=448, timestamps=True):
     return sampled
 
 
-def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=True):
-    """faster-whisper generate_segments (beam_size=1, temperature 0, every other option
-    at its default; the T > 0 fallback is not run — janus_amd flags instead) over one
-    16 kHz utterance, restated with this module's log-mel / encoder / greedy:
-    returns (segments [(start, end, text, tokens)], dict(windows, needs_fallback, skips)).
-    The encoder output is rounded to fp16 (``enc_fp16``), as the engine stores it."""
+def fallback_seed(utt, window, temp_index, hyp):
+    """Per-hypothesis noise seed (janus_amd transcriber.fallback_seed, restated)."""
+    m = lambda h: int(_mix32(np.uint32(h & 0xFFFFFFFF)))
+    return m(0x4A414E55 ^ m(utt * 0x01000193 + window * 0x9E3779B1 + temp_index * 0x85EBCA77 + hyp))
+
+
+def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=True,
+                        temperatures=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0), best_of=5, utt=0):
+    """faster-whisper generate_segments (beam_size=1, every other option at its default)
+    over one 16 kHz utterance, restated with this module's log-mel / encoder / decoder,
+    including generate_with_fallback: a window failing its gates (compression ratio > 2.4
+    or avg_logprob < -1, unless no_speech_prob > 0.6) is re-decoded at each further
+    temperature with best_of sampled hypotheses (the best by sum_lp / len first), the
+    first passing result kept, else the best avg_logprob among those with compression
+    ratio <= 2.4 (else all) reported at the last temperature; a settled temperature above
+    0.5 resets the prompt. ``utt``: the utterance index the noise seeds are keyed on.
+    Returns (segments [(start, end, text, tokens)], dict(windows, needs_fallback, skips,
+    fallback_decodes)). The encoder output is rounded to fp16 (``enc_fp16``)."""
     import zlib
     audio16k = np.asarray(audio16k, np.float32)
     tb = tk.timestamp_begin
     content = len(audio16k) // 160
     features = logmel(audio16k, 1, filters, n_frames=None)   # the whole clip, once
-    seek, all_tokens, segs = 0, [], []
-    cnt = dict(windows=0, needs_fallback=0, skips=0)
+    seek, all_tokens, segs, reset_since = 0, [], [], 0
+    cnt = dict(windows=0, needs_fallback=0, skips=0, fallback_decodes=0)
+
+    def judge(r, temp):
+        toks = [t for t in r["tokens"] if t != tk.eot]
+        avg = r["sum_lp"] / (len(toks) + 1)
+        text = tk.decode(toks).strip()
+        b = text.encode()
+        cr = len(b) / len(zlib.compress(b))
+        needs = cr > 2.4 or avg < -1.0
+        if r["nsp"] > 0.6 and avg < -1.0:
+            needs = False
+        return dict(toks=toks, avg=avg, cr=cr, nsp=r["nsp"], needs=needs, temp=temp)
+
     while seek < content:
         size = min(3000, content - seek)
         mel = window(features, seek)[None]
         enc = encoder(mel, W, cfg)
         if enc_fp16:
             enc = enc.half().float()
+        prev = all_tokens[reset_since:]
         prompt = ([tk.sot_prev if hasattr(tk, "sot_prev") else 50360] +
-                  all_tokens[-(max_length // 2 - 1):] if all_tokens else []) + list(tk.sot_sequence)
-        r = greedy_cached(enc, W, cfg, tk, max_length, prompts=[prompt], no_speech=50361)[0]
-        toks = [t for t in r["tokens"] if t != tk.eot]
-        avg = r["sum_lp"] / (len(toks) + 1)
-        text = tk.decode(toks).strip()
-        b = text.encode()
-        cr = len(b) / len(zlib.compress(b))
+                  prev[-(max_length // 2 - 1):] if prev else []) + list(tk.sot_sequence)
+        r0 = judge(greedy_cached(enc, W, cfg, tk, max_length, prompts=[prompt], no_speech=50361)[0], 0.0)
+        results, final = [r0], (r0 if not r0["needs"] else None)
+        for ti in range(1, len(temperatures)):
+            if final is not None:
+                break
+            T = temperatures[ti]
+            seeds = [fallback_seed(utt, cnt["windows"], ti, h) for h in range(best_of)]
+            hyps = greedy_cached(enc.expand(best_of, -1, -1), W, cfg, tk, max_length,
+                                 prompts=[prompt] * best_of, no_speech=50361, temperature=T,
+                                 seeds=seeds)
+            cnt["fallback_decodes"] += 1
+            js = [judge(h, T) for h in hyps]
+            score = [j["avg"] * (len(j["toks"]) + 1) / max(len(j["toks"]), 1) for j in js]
+            best = js[int(np.argmax(score))]
+            results.append(best)
+            if not best["needs"]:
+                final = best
+        if final is None:
+            if len(results) == 1:
+                final = r0          # fallback disabled (temperatures = (0.0,))
+            else:
+                pool = [r for r in results if not r["cr"] > 2.4] or results
+                final = dict(pool[int(np.argmax([r["avg"] for r in pool]))], temp=temperatures[-1])
         cnt["windows"] += 1
-        needs = cr > 2.4 or avg < -1.0
-        if r["nsp"] > 0.6 and avg < -1.0:
-            needs = False
-        cnt["needs_fallback"] += int(needs)
-        if r["nsp"] > 0.6 and not avg > -1.0:
+        cnt["needs_fallback"] += int(r0["needs"])
+        toks, avg = final["toks"], final["avg"]
+        if final["nsp"] > 0.6 and not avg > -1.0:
             cnt["skips"] += 1
             seek += size
             continue
@@ -318,4 +394,6 @@ def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=
                 continue
             all_tokens.extend(part)
             segs.append((s0, s1, txt, part))
+        if final["temp"] > 0.5:           # prompt_reset_on_temperature
+            reset_since = len(all_tokens)
     return segs, cnt

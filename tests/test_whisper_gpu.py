@@ -205,25 +205,113 @@ def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
 
 
-def test_seek_loop_matches_oracle(engine, gpu):
+@pytest.mark.parametrize("temps", [(0.0,), (0.0, 0.2, 0.4, 0.6, 0.8, 1.0)], ids=["t0", "fallback"])
+def test_seek_loop_matches_oracle(engine, gpu, temps):
     """faster-whisper's generate_segments loop (seek by the last timestamp pair, previous
     text as the <|startofprev|> prompt, gates, no-speech skip, blank-segment drop) on the
     GPU (per-row prompts, batched over utterances) vs the oracle's restatement of the same
-    loop, for a 40 s (several windows) and a 7 s utterance. max_length 64 bounds the
-    oracle's time; the prompt keeps max_length // 2 - 1 previous tokens as at 448."""
+    loop, for a 40 s (several windows) and a 7 s utterance — at temperature 0 alone and with
+    generate_with_fallback (every window of the seeded synthetic model fails the log-prob
+    gate, so each runs all five sampled temperatures x best_of 5 and settles on the best
+    avg_logprob at T = 1.0, resetting the prompt). max_length 64 bounds the oracle's time;
+    the prompt keeps max_length // 2 - 1 previous tokens as at 448."""
     from janus_amd.services.transcriber import generate_segments
     eng, W = engine
     auds = [synth_speech(160, 40.0, sr=16000), synth_speech(161, 7.0, sr=16000)]
-    streams = generate_segments(eng, auds, max_length=64)
+    streams = generate_segments(eng, auds, max_length=64, temperatures=temps)
     tk = eng.tokenizer
-    for a, st in zip(auds, streams):
-        ref, cnt = ow.transcribe_segments(a, W, CFG, tk, mel_filters(), max_length=64)
+    for i, (a, st) in enumerate(zip(auds, streams)):
+        ref, cnt = ow.transcribe_segments(a, W, CFG, tk, mel_filters(), max_length=64,
+                                          temperatures=temps, utt=i)
         got = [(s.start, s.end, s.text, list(s.tokens)) for s in st.segments]
         assert st.windows == cnt["windows"] and st.fallbacks == cnt["needs_fallback"] and st.skips == cnt["skips"]
+        assert st.fallback_decodes == cnt["fallback_decodes"]
         assert [g[3] for g in got] == [r[3] for r in ref]
         assert [g[2] for g in got] == [r[2] for r in ref]
         assert np.allclose([g[:2] for g in got], [r[:2] for r in ref])
-        print(f"seek loop: {st.windows} windows, {len(got)} segments, {st.fallbacks} flagged for fallback")
+        if len(temps) > 1:
+            assert st.fallbacks == st.windows and st.fallback_decodes == 5 * st.windows
+            assert all(s.temperature == 1.0 for s in st.segments)
+        print(f"seek loop {temps}: {st.windows} windows, {len(got)} segments, "
+              f"{st.fallbacks} failed at T=0, {st.fallback_decodes} sampled decodes")
+
+
+def test_sample_noise_matches_oracle(gpu):
+    """The decoder's Gumbel noise (janus_sample_gumbel_f32: the hash and -log(-log u) the
+    sampling logits kernel adds) equals the oracle's restatement (float64 logs) to f32
+    rounding, over a whole vocabulary for several seeds and positions."""
+    from janus_amd import _native as nat
+    V = 51864
+    seeds = np.array([0, 1, 0xDEADBEEF, 123456789], np.uint32)
+    sd = torch.from_numpy(seeds.view(np.int32).copy()).to(gpu)
+    out = torch.empty(len(seeds), V, dtype=torch.float32, device=gpu)
+    for pos in (0, 3, 447):
+        nat.call("janus_sample_gumbel_f32", sd.data_ptr(), len(seeds), pos, V, out.data_ptr(),
+                 nat.stream_ptr())
+        got = out.cpu().numpy().astype(np.float64)
+        for b, sdv in enumerate(seeds):
+            ref = ow.sample_noise(int(sdv), pos, V)
+            err = np.abs(got[b] - ref) / np.maximum(1.0, np.abs(ref))
+            assert err.max() < 4e-7, (pos, b, err.max())
+    # the noise is a Gumbel(0, 1) sample: mean 0.5772, variance pi^2 / 6
+    assert abs(got.mean() - 0.5772) < 0.01 and abs(got.var() - np.pi ** 2 / 6) < 0.03
+
+
+@pytest.mark.parametrize("which,T", [("tiny", 0.2), ("tiny", 1.0), ("base", 0.6)])
+def test_sampled_decode_matches_oracle(engine, base_engine, gpu, which, T):
+    """Decode at temperature T (faster-whisper's fallback re-decode,
+    janus_whisper_decode_sample_ex: Gumbel-max over the rule-filtered logits / T with
+    per-row counter-based noise) vs the oracle's sampler with the same seeds on the same
+    encoder output: each row identical, or its first divergence at a step where the
+    oracle's top-2 keys (logit / T + noise) are closer than NEAR_TIE / T (the fp16 path's
+    logit error scaled by 1 / T); sum of log-probs within 0.1 % for identical rows.
+    Rows of one window share the encoder output (best_of replication) and differ only in
+    their seeds."""
+    eng, W = engine if which == "tiny" else base_engine
+    cfg = CFG if which == "tiny" else BASE
+    utts = [synth_speech(300 + k, 6.0 + 7 * k) for k in range(3)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    enc = enc.repeat_interleave(2, 0).contiguous()          # two hypotheses per utterance
+    seeds = [1000 + 17 * b for b in range(enc.shape[0])]
+    ml = 48
+    out = eng.decode_ex(enc, max_length=ml, temperature=T, seeds=seeds)
+    rows = out.rows()
+    toks = out.tokens.cpu().numpy()
+    ref = ow.greedy_cached(enc.float().cpu(), W, cfg, eng.tokenizer, ml, no_speech=50361,
+                           temperature=T, seeds=seeds)
+    plen = len(eng.tokenizer.sot_sequence)
+    same = 0
+    for b, r in enumerate(ref):
+        g = [int(t) for t in toks[b][plen:plen + int(out.n_tokens[b])]]
+        if g == r["tokens"]:
+            same += 1
+            assert abs(float(out.sum_logprob[b]) - r["sum_lp"]) <= 1e-3 * abs(r["sum_lp"]) + 1e-3
+        else:
+            first = next((i for i in range(min(len(g), len(r["tokens"]))) if g[i] != r["tokens"][i]),
+                         min(len(g), len(r["tokens"])))
+            margin = r["margins"][first] if first < len(r["margins"]) else 0.0
+            assert margin < NEAR_TIE / T, (b, first, margin)
+        assert abs(rows[b][2] - r["nsp"]) <= 5e-3 * max(r["nsp"], 1e-6) + 1e-7
+    # the two hypotheses of one window share logits but not draws: they differ
+    assert any(rows[2 * k][0] != rows[2 * k + 1][0] for k in range(len(utts)))
+    assert same >= len(ref) - 1, same
+    print(f"{which} T={T}: {same}/{len(ref)} sampled rows identical")
+
+
+def test_sampling_leaves_greedy_unchanged(engine, gpu):
+    """A sampled decode between two greedy decodes on the same context (the sampling
+    logits kernel is a separate instantiation, its graphs keyed on the temperature) leaves
+    the greedy result bit-identical."""
+    eng, _ = engine
+    utts = [synth_speech(320 + k, 5.0 + 3 * k) for k in range(4)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    t1, n1, s1 = eng.decode(enc, 40)
+    t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
+    eng.decode_ex(enc, max_length=40, temperature=0.4, seeds=[7, 8, 9, 10])
+    t2, n2, s2 = eng.decode(enc, 40)
+    assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
 
 
 @pytest.mark.parametrize("which", ["tiny", "base"])
