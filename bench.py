@@ -54,6 +54,10 @@ def parse():
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--fallback", action="store_true",
+                    help="run faster-whisper's temperature fallback on windows failing their gates "
+                         "(generate_with_fallback: 5 temperatures x best_of 5 sampled re-decodes); "
+                         "off by default: the seeded synthetic weights fail every window (DESIGN.md §0)")
     return ap.parse_args()
 
 
@@ -174,7 +178,9 @@ def main():
     offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
     frames = int(np.ceil(args.seconds * 44100 / 512))
-    pipe = JanusPipeline(args.model, max_length=args.max_length)
+    from janus_amd.services.transcriber import TEMPERATURES
+    pipe = JanusPipeline(args.model, max_length=args.max_length,
+                         temperatures=TEMPERATURES if args.fallback else (0.0,))
     torch.cuda.synchronize()
 
     last = {}
@@ -297,13 +303,15 @@ def main():
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
             "packets_gathered": n_packets,
-            # faster-whisper's gates on each T = 0 window (the fallback re-decode is not
-            # run: synthetic weights give avg_logprob far below -1, so every window would
-            # fall back)
+            # faster-whisper's gates on each T = 0 window; the fallback re-decodes run only
+            # with --fallback (synthetic weights give avg_logprob far below -1, so every
+            # window falls back)
             "gates": {"needs_fallback": int(sum(g[0] for g in enc.gates or [])),
                       "no_speech_skip": int(sum(g[1] for g in enc.gates or [])),
                       "mean_avg_logprob": round(float(np.mean([g[2] for g in enc.gates])), 3)
-                      if enc.gates else None},
+                      if enc.gates else None,
+                      "fallback_run": bool(args.fallback),
+                      "sampled_decodes": int(sum(g[6] for g in enc.gates or []))},
             "stats_gathered": n_stats,
             "host_edges_ms": {"pcm_upload": round(t_up * 1000.0, 1),
                               "wav_download_and_framing": round(t_down * 1000.0, 1)},

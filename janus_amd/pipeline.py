@@ -38,21 +38,38 @@ class EncodeResult:
         self.texts, self.tags, self.packets = texts, tags, packets
         self.tokens, self.n_tokens = tokens, n_tokens
         self.stats = stats
-        self.gates = gates   # per utterance (needs_fallback, no_speech_skip, avg_logprob, cr, nsp)
+        # per utterance: (needs_fallback at T = 0, no_speech_skip, avg_logprob, cr, nsp,
+        # settled temperature, sampled fallback decodes)
+        self.gates = gates
 
 
-def _texts_and_gates(w, dec):
+def _texts_and_gates(w, dec, temperatures=(0.0,), enc=None, **dec_kw):
     """Transcripts of one 30 s window per utterance plus faster-whisper's gates; a
     no-speech skip (no_speech_prob > 0.6 and avg_logprob <= -1) yields no text, as the
-    reference's generate_segments skips the window (transcriber.py:53-64)."""
-    from .services.transcriber import compression_ratio, gates
-    texts = w.texts(dec.tokens, dec.prompt_lens)
+    reference's generate_segments skips the window (transcriber.py:53-64).
+    ``temperatures`` beyond (0.0,): windows failing their gates go through
+    generate_with_fallback (transcriber._fallback: sampled best_of-5 re-decodes of the
+    encoder output ``enc``, on the caller's stream, ``dec_kw`` to decode_ex) and the
+    settled result gives the text. Gates per utterance: (needs_fallback at T = 0,
+    no_speech_skip, avg_logprob, compression_ratio, no_speech_prob, temperature, sampled
+    decodes) of the settled result."""
+    from .services.transcriber import BEST_OF, _fallback, candidate
+    tk = w.tokenizer
+    first = [candidate(tk, toks, avg, nsp, 0.0) for (toks, avg, nsp) in dec.rows()]
+    if len(temperatures) > 1:
+        prompts = [list(tk.sot_sequence)] * len(first)
+        final, ndec = _fallback(w, tk, enc, prompts, first, [(i, 0) for i in range(len(first))],
+                                dec.tokens.shape[1], tuple(temperatures), BEST_OF, **dec_kw)
+        texts = [tk.transcript(c.tokens) for c in final]
+    else:
+        final, ndec = first, [0] * len(first)
+        texts = w.texts(dec.tokens, dec.prompt_lens)
     out_t, out_g = [], []
-    for t, (toks, avg, nsp) in zip(texts, dec.rows()):
-        text = w.tokenizer.decode(toks).strip()
-        needs, skip = gates(text, avg, nsp)
+    for t, c0, c, nd in zip(texts, first, final, ndec):
+        skip = c.no_speech_prob > 0.6 and not c.avg_logprob > -1.0
         out_t.append("" if skip else t)
-        out_g.append((needs, skip, avg, compression_ratio(text), nsp))
+        out_g.append((c0.needs_fallback, skip, c.avg_logprob, c.compression_ratio, c.no_speech_prob,
+                      c.temperature, nd))
     return out_t, out_g
 
 
@@ -68,11 +85,15 @@ def _prosody_stats(parts, B, device):
 
 class JanusPipeline:
     def __init__(self, model: str = "base.en", whisper_seed: int = 0, vocoder_seed: int = 0,
-                 max_length: int = 448, vocoder_cfg: FireflyConfig = FireflyConfig()):
+                 max_length: int = 448, vocoder_cfg: FireflyConfig = FireflyConfig(),
+                 temperatures=(0.0,)):
+        """temperatures: (0.0,) decodes each window once at T = 0 and reports the gates;
+        services.transcriber.TEMPERATURES runs faster-whisper's fallback as well."""
         self.device = nat.require_gpu()
         self.whisper = WhisperEngine(CONFIGS[model], seed=whisper_seed)
         self.vocoder = VocoderEngine(vocoder_cfg, seed=vocoder_seed)
         self.max_length = max_length
+        self.temperatures = tuple(float(t) for t in temperatures)
 
     # ------------------------------------------------------------------ encode
     def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
@@ -98,6 +119,7 @@ class JanusPipeline:
             pres = None
         with torch.cuda.stream(hi):
             dec = w.decode_ex(enc, max_length=self.max_length)
+            texts, gts = _texts_and_gates(w, dec, self.temperatures, enc)
         main.wait_stream(hi)
         try:
             parts = pres if isinstance(pres, tuple) else (pres,)
@@ -106,7 +128,6 @@ class JanusPipeline:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts, gts = _texts_and_gates(w, dec)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
@@ -270,9 +291,13 @@ class JanusPipeline:
             # ms); cu_count: the vocabulary projection at one block per CU of the partition
             # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms) and row-split skinny
             # projections from N <= 1024 (vs 2048: 310.5 -> 306.3 ms)
-            dec = w.decode_ex(enc, max_length=self.max_length,
-                              xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
-                              cu_count=self._dec_s.n_cus)
+            dec_kw = dict(xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+                          cu_count=self._dec_s.n_cus)
+            dec = w.decode_ex(enc, max_length=self.max_length, **dec_kw)
+            # the fallback's sampled re-decodes on the decoder's CUs (host-driven: reads
+            # the T = 0 gates); the settled texts go to _finish
+            dec.settled = (_texts_and_gates(w, dec, self.temperatures, enc, **dec_kw)
+                           if len(self.temperatures) > 1 else None)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
         if timing:
@@ -298,7 +323,8 @@ class JanusPipeline:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        texts, gts = _texts_and_gates(self.whisper, dec)
+        settled = getattr(dec, "settled", None)
+        texts, gts = settled if settled is not None else _texts_and_gates(self.whisper, dec)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]

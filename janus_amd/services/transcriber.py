@@ -244,7 +244,7 @@ class _Stream:
         return p + list(tk.sot_sequence)
 
 
-def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of):
+def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of, **dec_kw):
     """Run the temperature fallback for the windows of one round: first [Candidate] (T = 0
     results), keys [(utt, window)]; returns each window's settled Candidate. The
     hypotheses of every window still failing at a temperature go out as one sampled batch
@@ -264,7 +264,7 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
             rows_prompts = [prompts[j] for j in js for _ in range(best_of)]
             seeds = [fallback_seed(keys[j][0], keys[j][1], ti, h) for j in js for h in range(best_of)]
             out = engine.decode_ex(rows_enc, prompts=rows_prompts, max_length=max_length,
-                                   temperature=T, seeds=seeds).rows()
+                                   temperature=T, seeds=seeds, **dec_kw).rows()
             for k, j in enumerate(js):
                 toks, avg_lp, nsp = best_hypothesis(out[k * best_of:(k + 1) * best_of])
                 results[j].append(candidate(tk, toks, avg_lp, nsp, T))

@@ -111,8 +111,12 @@ class StreamingEncoder:
     def __init__(self, n_streams: int, whisper, max_length: int = 448,
                  mode: JanusMode = JanusMode.SEMANTIC_VOICE, override="auto",
                  vad_threshold: float = 0.5, hop: int = 512, asynchronous: bool = False,
-                 receiver=None, vad_weights: dict = None):
+                 receiver=None, vad_weights: dict = None, temperatures=(0.0,)):
+        """temperatures: (0.0,) decodes each phrase window at T = 0 (gates reported, not
+        acted on); services.transcriber.TEMPERATURES adds faster-whisper's fallback, as
+        the reference's transcribe_buffer runs it."""
         self.device = nat.require_gpu()
+        self.temperatures = tuple(float(t) for t in temperatures)
         self.S = n_streams
         self.whisper = whisper
         self.max_length = max_length
@@ -239,7 +243,8 @@ class StreamingEncoder:
         B = len(done)
         w = self.whisper
         mel = w.logmel(pcm, offs, B, 3)                 # transcriber.py:51 [::3]
-        dec = w.decode_ex(w.encode(mel), max_length=self.max_length)
+        enc = w.encode(mel)
+        dec = w.decode_ex(enc, max_length=self.max_length)
         # prosody in rounds: round r takes every channel's r-th phrase of this tick, so a
         # channel that completed two phrases runs them in order, the second from the first's
         # end state (one aubio object per channel, prosody.py:32)
@@ -272,7 +277,7 @@ class StreamingEncoder:
         except Exception:                               # engine.py:520-525
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
         from .pipeline import _texts_and_gates
-        texts, _ = _texts_and_gates(w, dec)
+        texts, _ = _texts_and_gates(w, dec, self.temperatures, enc)
         # a phrase longer than one 30 s window (continuous speech with no 0.5 s pause) gets
         # the whole seek loop, as the engine's transcribe_buffer call does
         # (engine.py:514 -> transcriber.py:53-64), instead of its first window only
@@ -280,7 +285,8 @@ class StreamingEncoder:
         if long:
             from .services.transcriber import generate_segments
             auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in long]
-            for i, st in zip(long, generate_segments(w, auds, max_length=self.max_length)):
+            for i, st in zip(long, generate_segments(w, auds, max_length=self.max_length,
+                                                     temperatures=self.temperatures)):
                 texts[i] = ' '.join(sg.text.strip() for sg in st.segments).strip()
             self.long_phrases += len(long)
         ts = time.time() if timestamp is None else timestamp

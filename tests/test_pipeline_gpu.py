@@ -83,3 +83,33 @@ def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
             continue
         torch.testing.assert_close(wav, seq[i][1], rtol=0, atol=0)
         assert torch.equal(pcm16, seq[i][2])
+
+
+def test_pipeline_fallback_matches_seek_loop(gpu):
+    """The batched pipeline with faster-whisper's fallback (temperatures 0 ... 1.0, best_of
+    5: every window of the seeded synthetic model fails at T = 0) settles each utterance
+    exactly as the drop-in seek loop (generate_segments) does on the same 16 kHz audio:
+    same avg_logprob, temperature and number of sampled decodes; the overlapped serving
+    step, whose re-decodes run on the decoder's CU partition, gives the same packets."""
+    from janus_amd.services.transcriber import TEMPERATURES, generate_segments
+    pipe = JanusPipeline("tiny.en", max_length=12, temperatures=TEMPERATURES)
+    utts = [synth_speech(500 + k, 2.0 + 3 * k) for k in range(3)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+    res = pipe.encode(pcm, offs, lengths, timestamp=5.0)
+    streams = generate_segments(pipe.whisper, [np.ascontiguousarray(u[::3]) for u in utts],
+                                max_length=12)
+    for b, st in enumerate(streams):
+        needs0, skip, avg, cr, nsp, temp, ndec = res.gates[b]
+        assert st.windows == 1 and needs0 and ndec == st.fallback_decodes == 5
+        if st.segments:
+            assert st.segments[0].avg_logprob == avg and st.segments[0].temperature == temp == 1.0
+    outs = [pipe.step_overlapped(pcm, offs, lengths, 16, 16, timestamp=5.0)]
+    outs.append(pipe.flush(16))
+    assert outs[1][0].packets == res.packets
+    # flags, settled temperature and decode counts identical; the log-prob sums differ in
+    # the last bits (the overlapped decoder runs 4 cross-attention key splits on 128 CUs)
+    for g, r in zip(outs[1][0].gates, res.gates):
+        assert (g[0], g[1], g[3], g[5], g[6]) == (r[0], r[1], r[3], r[5], r[6])
+        assert abs(g[2] - r[2]) <= 1e-4 * abs(r[2]) and abs(g[4] - r[4]) <= 5e-3 * r[4] + 1e-9

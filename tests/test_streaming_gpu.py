@@ -139,7 +139,8 @@ def test_streaming_long_phrase_full_seek_loop(gpu, tiny):
     ref = segment(chunks, list(dec[0]), non_vad=[False] * len(chunks))
     long_refs = [ph for _, ph in ref if (len(ph) + 2) // 3 > 480000]
     assert len(long_refs) == 1 and enc.long_phrases == 1
-    st = generate_segments(tiny, [np.ascontiguousarray(long_refs[0][::3])], max_length=8)[0]
+    st = generate_segments(tiny, [np.ascontiguousarray(long_refs[0][::3])], max_length=8,
+                           temperatures=enc.temperatures)[0]
     assert st.windows >= 2
     want = ' '.join(sg.text.strip() for sg in st.segments).strip()
     mine = [r for r in got if r["text"] == want]
