@@ -54,27 +54,27 @@ template <int C, int V = 0> struct WideCfg;
 // EPF: residual / accumulator rows loaded before c2 (in flight during it) where the
 // registers allow, else after it.
 // NP: epilogue passes (the fp32 tile in NP row slices so the block fits 3 per CU)
-template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 4, NP = 2; static constexpr bool EPF = false; };
+template <> struct WideCfg<128> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 4, NP = 2; static constexpr bool EPF = false, AROT = false; };
 // 8 waves (2 x 4): half the m-tiles per wave, so fewer registers per wave and two 8-wave
 // blocks per CU (16 waves) instead of three 4-wave blocks (JANUS_WIDE128_CFG=1).
 // Measured slower (64 x 30 s, whole GPU: C = 128 units 47.5 -> 59.6 ms): each weight
 // fragment is now fetched by two waves; kept as an A/B switch.
 // ring depth 2 (the default, JANUS_WIDE128_CFG=2): 16 fewer VGPRs, three blocks per CU
-template <> struct WideCfg<128, 2> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 2, NP = 2; static constexpr bool EPF = false; };
-template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN = 4, NPB = 4, NP = 1; static constexpr bool EPF = false; };
+template <> struct WideCfg<128, 2> { static constexpr int BM = 112, WM = 1, WN = 4, NPB = 2, NP = 2; static constexpr bool EPF = false, AROT = true; };
+template <> struct WideCfg<128, 1> { static constexpr int BM = 112, WM = 2, WN = 4, NPB = 4, NP = 1; static constexpr bool EPF = false, AROT = false; };
 // C = 256 on the register ring (JANUS_WIDE256_CFG=ring): 8 waves x 32 columns over all
 // m-tiles, weights from L2 into registers. Per block k-step: A-fragment LDS reads 64 KB
 // (512 clocks at 128 B/clock), weight fragments 16 KB over the L1 path (256 clocks), MFMA
 // 512 clocks per SIMD — against the LDS-staged form's 80 KB of LDS traffic (640 clocks).
-template <> struct WideCfg<256, 3> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 2, NP = 2; static constexpr bool EPF = false; };
+template <> struct WideCfg<256, 3> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 2, NP = 2; static constexpr bool EPF = false, AROT = false; };
 // C = 64 on the register ring (JANUS_WIDE64_CFG=ring): 2 x 2 waves of 32 columns x 6
 // m-tiles; per block k-step A-fragment LDS reads 24 KB and weight fragments 8 KB from L2
 // (three blocks per CU: 576 / 384 clocks against 576 of MFMA), where the LDS-staged form
 // moves 32 KB through LDS (768 clocks). Measured slower all the same (standalone 64 x 30 s,
 // C = 64 units 30.9-31.1 vs 30.2 ms): kept as an A/B switch.
-template <> struct WideCfg<64, 5> { static constexpr int BM = 176, WM = 2, WN = 2, NPB = 2, NP = 1; static constexpr bool EPF = false; };
+template <> struct WideCfg<64, 5> { static constexpr int BM = 176, WM = 2, WN = 2, NPB = 2, NP = 1; static constexpr bool EPF = false, AROT = false; };
 // the same with the weight ring 4 deep (the default; one block per CU either way)
-template <> struct WideCfg<256, 4> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 4, NP = 2; static constexpr bool EPF = false; };
+template <> struct WideCfg<256, 4> { static constexpr int BM = 112, WM = 1, WN = 8, NPB = 4, NP = 2; static constexpr bool EPF = false, AROT = false; };
 
 template <int C, int V = 0>
 struct WideGeo {
@@ -97,7 +97,7 @@ struct WideGeo {
   static constexpr int ACT = std::max(R0MAX * LI, MT1 * 16 * LI);
   static constexpr size_t LDS = std::max((size_t)ACT * 2, (size_t)RP * ES * 4);
   // blocks per CU the register budget is sized for (C = 256: one 8-wave block, 256 VGPRs)
-  static constexpr int MINB = C == 256 ? 1 : (C == 64 ? 3 : 2);
+  static constexpr int MINB = C == 256 ? 1 : (C == 64 || Cfg::NPB == 2 ? 3 : 2);
   static_assert(BM % 16 == 0 && C % (16 * WN) == 0 && C % 32 == 0, "tiling");
 };
 
@@ -110,11 +110,65 @@ __device__ __forceinline__ int own_tile(int j, int wm) {
   return wm + j * WM < MT ? j : (MT - 1 - wm) / WM;
 }
 
-template <int C, int MW, int MT, class G>
+template <int C, int MW, int MT, class G, bool AROT = false>
 __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float16* __restrict__ wp,
                                           const _Float16* src, int dil, int nks, int wm,
                                           int a_lane, int b_lane) {
   constexpr int NTW = G::NTW, NPB = G::NPB, LI = G::LI, WM = G::WM;
+  if constexpr (AROT) {
+    // A fragments in ONE register set, refilled per m-tile: m-tile j's fragment for step
+    // ks+1 is read as soon as step ks's MFMAs on it are issued, so it has the other MW-1
+    // m-tiles' MFMAs to land (half the A registers of the double-buffered form below).
+#pragma unroll
+    for (int j = 0; j < MW; ++j)
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) acc[j][n] = zero_f32x4();
+    half8 bq[NPB][NTW];
+    const _Float16* wl = wp + b_lane;
+    // slots issued in ring order (the loop's vmcnt for slot s counts on it: loaded out of
+    // order, the merged loop-header state made every k-step wait for the whole ring)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < NPB; ++s) {
+#pragma unroll
+      for (int n = 0; n < NTW; ++n)
+        bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)s * C + n * 16) * 32);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    auto a_addr = [&](int ks) __attribute__((always_inline)) {
+      const int kk = ks * 32;  // wave-uniform: one tap
+      return src + a_lane + (kk / C) * dil * LI + kk % C;
+    };
+    half8 av[MW];
+    {
+      const _Float16* ap = a_addr(0);
+#pragma unroll
+      for (int j = 0; j < MW; ++j)
+        av[j] = *reinterpret_cast<const half8*>(ap + own_tile<MT, WM>(j, wm) * WM * 16 * LI);
+    }
+#pragma nounroll
+    for (int ks0 = 0; ks0 < nks; ks0 += NPB) {
+#pragma unroll
+      for (int s = 0; s < NPB; ++s) {
+        const int ks = ks0 + s;
+        const _Float16* ap = a_addr(min(ks + 1, nks - 1));
+#pragma unroll
+        for (int j = 0; j < MW; ++j) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int n = 0; n < NTW; ++n) acc[j][n] = mfma16(av[j], bq[s][n], acc[j][n]);
+          av[j] = *reinterpret_cast<const half8*>(ap + own_tile<MT, WM>(j, wm) * WM * 16 * LI);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int nx = min(ks + NPB, nks - 1);
+#pragma unroll
+        for (int n = 0; n < NTW; ++n)
+          bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)nx * C + n * 16) * 32);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < MW; ++j)
 #pragma unroll
@@ -123,11 +177,14 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
   // compiler's vmcnt for a slot never has to cover younger slots' loads
   half8 bq[NPB][NTW];
   const _Float16* wl = wp + b_lane;
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int s = 0; s < NPB; ++s)
+  for (int s = 0; s < NPB; ++s) {
 #pragma unroll
     for (int n = 0; n < NTW; ++n)
       bq[s][n] = *reinterpret_cast<const half8*>(wl + ((int64_t)s * C + n * 16) * 32);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // A fragments double-buffered across k-steps: step ks+1's LDS reads are issued before
   // step ks's MFMAs (NPB even keeps the buffer index static)
   static_assert(NPB % 2 == 0, "even ring depth");
@@ -169,19 +226,34 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
   }
 }
 
-template <int C, int V>
+// KC, DC > 0: the unit's kernel size and dilation at compile time. The stage loop then
+// walks rows relative to the tile's first output row, so stage slots [0, BM*CPR/NT) of
+// every thread are exactly the residual rows [t0, t0 + BM) in the epilogue's thread
+// mapping: those slots stay in registers through c1 and c2 (raw x; the LDS tile holds
+// silu(x)) instead of being re-read from HBM after c2 (the 1.4-1.6x traffic of the
+// re-reading form). KC = 0: (k, d) at run time, residual re-read after c2.
+template <int C, int V, int KC = 0, int DC = 0>
 __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void resunit_wide_kernel(ResUnitArgs a,
-                                                                         int tiles_per_utt) {
+                                                                         int tiles_per_utt,
+                                                                         int stagger, int slot_blocks) {
   using G = WideGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, NT = G::NT, LI = G::LI;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
   constexpr int NTW = G::NTW, ES = G::ES;
+  constexpr bool RES = KC > 0;
+  constexpr bool AROT = RES && G::Cfg::AROT;
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   _Float16* sX = smem;                         // [R0][LI] silu(x)
   _Float16* sS = smem;                         // [MT1*16][LI] silu(c1 + b1) (over sX)
   float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS)
 
-  const int k = a.k, d = a.d, T = a.T;
+  // first round of blocks: the j-th block of each CU starts j * stagger sleeps late, so
+  // co-resident blocks do not reach their staging / epilogue bursts together
+  if (stagger > 0 && (int)blockIdx.x < 4 * slot_blocks) {
+    const int n = (int)blockIdx.x / slot_blocks * stagger;
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  const int k = RES ? KC : a.k, d = RES ? DC : a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
   const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
@@ -195,8 +267,47 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
   _Float16* ob = a.out + (int64_t)b * T * C;
   const int nks = k * C / 32;
 
+  // residual rows x[t0 + r] of this thread's epilogue chunks (RES: kept from the stage)
+  constexpr int NR = RES ? BM * CPR / NT : 1;
+  static_assert(!RES || (NT % CPR == 0 && (BM * CPR) % NT == 0 && NR == G::NE),
+                "resident residual: stage slots = epilogue chunks");
+  uint4 rx[NR];
   // ---- 1. stage silu(x): all loads in flight, then convert + store
-  {
+  if constexpr (RES) {
+    constexpr int P = (KC - 1) / 2 + DC * (KC - 1) / 2;  // rows left of t0: p2 + p1
+    constexpr int RPI = NT / CPR;                        // rows per stage slot
+    constexpr int ILO = -((P + RPI - 1) / RPI);          // first slot (left halo)
+    constexpr int R0C = MT1 * 16 + (KC - 1) * DC;        // staged rows
+    constexpr int IHI = (R0C - P + RPI - 1) / RPI;       // one past the last slot
+    constexpr int NS = IHI - ILO;
+    static_assert(ILO <= 0 && IHI >= NR, "stage slots cover the residual rows");
+    uint4 pf[NS];
+    const int rr0 = tid / CPR, cc = tid % CPR;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int rl = (ILO + i) * RPI + rr0;  // row relative to t0
+      const int t = t0 + rl;
+      const int tc = min(max(t, 0), T - 1);
+#ifdef JANUS_ABL_NOSTAGE  // timing ablation only (wrong results)
+      pf[i] = make_uint4(tc, 0, 0, 0);
+#else
+      pf[i] = ld_act(xb + (int64_t)tc * C + cc * 8);
+#endif
+      if (!(rl >= -P && rl < R0C - P && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int rl = (ILO + i) * RPI + rr0;
+      if (rl >= -P && rl < R0C - P) {
+        half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        *reinterpret_cast<half8*>(sX + (rl + P) * LI + cc * 8) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) rx[i] = pf[i - ILO];
+  } else {
     const int xbase = t0 - p2 - p1;
     uint4 pf[G::NLD];
 #pragma unroll
@@ -206,7 +317,11 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       const int t = xbase + r;
       // unconditional load of a clamped row, zeroed below (no branch per load)
       const int tc = min(max(t, 0), T - 1);
+#ifdef JANUS_ABL_NOSTAGE  // timing ablation only (wrong results)
+      pf[i] = make_uint4(tc, 0, 0, 0);
+#else
       pf[i] = ld_act(xb + (int64_t)tc * C + cc * 8);
+#endif
       if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -230,7 +345,7 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
   // ---- 2. c1 over MT1*16 rows (row r <-> time t0 - p2 + r): A = sX[r + tap*d]
   {
     f32x4 acc[MW1][NTW];
-    wide_conv<C, MW1, MT1, G>(acc, a.w1, sX, d, nks, wm, a_lane, b_lane);
+    wide_conv<C, MW1, MT1, G, AROT>(acc, a.w1, sX, d, nks, wm, a_lane, b_lane);
     __syncthreads();  // every wave is done reading sX: write silu(c1 + b1) over it
 #pragma unroll
     for (int n = 0; n < NTW; ++n) {
@@ -263,15 +378,21 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       const int r = idx / CPR, cg = (idx % CPR) * 8;
       const bool ok = r < BM && t0 + r < T;
       const int64_t o = (int64_t)(t0 + r) * C + cg;
-      rq[i] = ok ? ld_res(xb + o) : make_uint4(0, 0, 0, 0);
+#ifdef JANUS_ABL_NORES  // timing ablation only (wrong results)
+      rq[i] = make_uint4(o, 0, 0, 0);
+      pq[i] = make_uint4(ok, 0, 0, 0);
+#else
+      if constexpr (RES) rq[i] = rx[i];
+      else rq[i] = ok ? ld_res(xb + o) : make_uint4(0, 0, 0, 0);
       pq[i] = (ok && a.accumulate) ? ld_res(ob + o) : make_uint4(0, 0, 0, 0);
+#endif
     }
   };
   if constexpr (G::Cfg::EPF) epi_load();
 
   // ---- 3. c2 over BM rows (row r <-> time t0 + r): A = sS[r + tap]
   f32x4 acc2[MW2][NTW];
-  wide_conv<C, MW2, MT2, G>(acc2, a.w2, sS, 1, nks, wm, a_lane, b_lane);
+  wide_conv<C, MW2, MT2, G, AROT>(acc2, a.w2, sS, 1, nks, wm, a_lane, b_lane);
   if constexpr (!G::Cfg::EPF) epi_load();
   __syncthreads();  // sS dead: the fp32 epilogue tile takes its place
 
@@ -320,13 +441,20 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
   }
 }
 
-template <int C, int V>
-static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
+// A/B switches: JANUS_WIDE_STAGGER = sleeps (s_sleep 127 each) per block slot,
+// JANUS_WIDE_SLOT = blocks per slot round (the CUs the stream runs on)
+static void wide_stagger(int& st, int& slot) {
+  static const int st_ = std::getenv("JANUS_WIDE_STAGGER") ? std::atoi(std::getenv("JANUS_WIDE_STAGGER")) : 0;
+  static const int slot_ = std::getenv("JANUS_WIDE_SLOT") ? std::atoi(std::getenv("JANUS_WIDE_SLOT")) : 256;
+  st = st_;
+  slot = std::max(slot_, 1);
+}
+
+template <int C, int V, int KC, int DC>
+static void wide_go(const ResUnitArgs& a, hipStream_t s) {
   using G = WideGeo<C, V>;
-  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
-  JANUS_CHECK((a.k * C / 32) % G::NPB == 0, "resunit (wide): k-step count vs ring depth");
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_wide_kernel<C, V>;
+  auto kern = resunit_wide_kernel<C, V, KC, DC>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -334,8 +462,33 @@ static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
     attr = true;
   }
   const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
-  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
+  int st = 0, slot = 256;
+  wide_stagger(st, slot);
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt, st, slot);
   JANUS_LAUNCH_CHECK();
+}
+
+template <int C, int V>
+static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
+  using G = WideGeo<C, V>;
+  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
+  JANUS_CHECK((a.k * C / 32) % G::NPB == 0, "resunit (wide): k-step count vs ring depth");
+  // Firefly-GAN's ResBlock1 geometry (k in {3, 7, 11} x d in {1, 3, 5}) at compile time with
+  // the residual kept resident; JANUS_WIDE_RES=0 (A/B) or any other (k, d): run-time form
+  static const bool res = [] { const char* e = std::getenv("JANUS_WIDE_RES"); return e ? std::atoi(e) != 0 : true; }();
+  constexpr bool fits = G::NT % G::CPR == 0 && (G::BM * G::CPR) % G::NT == 0 &&
+                        G::BM * G::CPR / G::NT == G::NE;
+  if constexpr (fits) {
+    if (res) {
+#define JANUS_WIDE_KD(K_, D_) \
+    if (a.k == K_ && a.d == D_) return wide_go<C, V, K_, D_>(a, s);
+    JANUS_WIDE_KD(3, 1) JANUS_WIDE_KD(3, 3) JANUS_WIDE_KD(3, 5)
+    JANUS_WIDE_KD(7, 1) JANUS_WIDE_KD(7, 3) JANUS_WIDE_KD(7, 5)
+    JANUS_WIDE_KD(11, 1) JANUS_WIDE_KD(11, 3) JANUS_WIDE_KD(11, 5)
+#undef JANUS_WIDE_KD
+    }
+  }
+  wide_go<C, V, 0, 0>(a, s);
 }
 
 template <int C, int V = 0> struct LdsCfg;
@@ -392,7 +545,8 @@ struct LdsGeo {
 // instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
 template <int C, bool EPF, int V>
 __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel(ResUnitArgs a,
-                                                                         int tiles_per_utt) {
+                                                                         int tiles_per_utt,
+                                                                         int stagger, int slot_blocks) {
   using G = LdsGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
@@ -403,6 +557,10 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
   float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS and sW)
   _Float16* sW = smem + G::ACT_H;              // [2][C][LW]
 
+  if (stagger > 0 && (int)blockIdx.x < 4 * slot_blocks) {
+    const int n = (int)blockIdx.x / slot_blocks * stagger;
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int k = a.k, d = a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
@@ -504,13 +662,18 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
   // (nkb = k*C/KB is even: two k-blocks per trip keep the register slots static; the
   // loads are unconditional (clamped index) so the compiler's vmcnt for slot B never
   // has to cover slot A's younger loads)
+// (sched barriers pin each weight load ahead of the MFMAs it is meant to overlap: left
+// free, the scheduler sank the loads past the next k-block's MFMAs, one k-block of cover
+// instead of two)
 #define WIDE_KLOOP(ACC, MWT, MTT, WP, SRC, DIL)                                         \
   for (int kb = 0; kb < nkb; kb += 2) {                                                 \
     WIDE_WLOAD(rwA0, rwA1, WP, min(kb + 2, nkb - 1));                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
     mma(ACC, MWT{}, MTT{}, SRC, DIL, kb, 0);                                            \
     WIDE_WSTORE(rwB0, rwB1, 1);                                                         \
     __syncthreads();                                                                    \
     WIDE_WLOAD(rwB0, rwB1, WP, min(kb + 3, nkb - 1));                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
     mma(ACC, MWT{}, MTT{}, SRC, DIL, kb + 1, 1);                                        \
     if (kb + 2 < nkb) WIDE_WSTORE(rwA0, rwA1, 0);                                       \
     __syncthreads();                                                                    \
@@ -630,7 +793,9 @@ static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
     attr = true;
   }
   const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
-  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
+  int st = 0, slot = 256;
+  wide_stagger(st, slot);
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt, st, slot);
   JANUS_LAUNCH_CHECK();
 }
 
