@@ -26,6 +26,7 @@
 // (WN) or distinct m-tiles (WM); weights are re-read per tile from L2 (~C*k*C*4 B per
 // tile, far below the L2's rate at the MFMA pace).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -47,6 +48,24 @@ __global__ void resunit_wide_pack_kernel(const float* __restrict__ w, _Float16* 
   const int tap = kk / C, ci = kk % C;
   out[idx] = (_Float16)w[((int64_t)co * C + ci) * k + tap];
 }
+
+// Phase profile (JANUS_PHASE_PROF builds only, tools/phase_prof.py): thread 0 of every
+// block of one chosen unit launch records the shader clock at each phase boundary plus the
+// real-time clock and its hardware slot (HW_ID, XCC_ID), 16 values per block.
+#ifdef JANUS_PHASE_PROF
+#define JANUS_PROF(I)                                                                    \
+  do {                                                                                  \
+    if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 16 + (I)] = (long long)clock64(); \
+  } while (0)
+#else
+#define JANUS_PROF(I) do { } while (0)
+#endif
+
+#ifdef JANUS_ABL_NOSILU  // timing ablation only (wrong results)
+#define WSILU(x) (x)
+#else
+#define WSILU(x) silu(x)
+#endif
 
 template <int C, int V = 0> struct WideCfg;
 // BM output rows per block, WM x WN waves (wave tile: every WM-th m-tile x C/WN columns),
@@ -235,7 +254,7 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
 template <int C, int V, int KC = 0, int DC = 0>
 __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void resunit_wide_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt,
-                                                                         int stagger, int slot_blocks) {
+                                                                         long long* prof) {
   using G = WideGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, NT = G::NT, LI = G::LI;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
@@ -247,12 +266,14 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
   _Float16* sS = smem;                         // [MT1*16][LI] silu(c1 + b1) (over sX)
   float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS)
 
-  // first round of blocks: the j-th block of each CU starts j * stagger sleeps late, so
-  // co-resident blocks do not reach their staging / epilogue bursts together
-  if (stagger > 0 && (int)blockIdx.x < 4 * slot_blocks) {
-    const int n = (int)blockIdx.x / slot_blocks * stagger;
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+#ifdef JANUS_PHASE_PROF
+  if (prof && threadIdx.x == 0) {
+    prof[(int64_t)blockIdx.x * 16 + 8] = (long long)wall_clock64();
+    prof[(int64_t)blockIdx.x * 16 + 10] = (long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+    prof[(int64_t)blockIdx.x * 16 + 11] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
   }
+#endif
+  JANUS_PROF(0);
   const int k = RES ? KC : a.k, d = RES ? DC : a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
@@ -301,7 +322,7 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       if (rl >= -P && rl < R0C - P) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
         *reinterpret_cast<half8*>(sX + (rl + P) * LI + cc * 8) = v;
       }
     }
@@ -331,13 +352,14 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
       }
     }
   }
   __syncthreads();
 
+  JANUS_PROF(1);
   const int arow = lane & 15, kq = 8 * (lane >> 4);
   const int a_lane = (wm * 16 + arow) * LI + kq;                 // A: row, k chunk
   const int b_lane = ((wn * NTW) * 16 + arow) * 32 + kq;         // B: column, k chunk
@@ -346,7 +368,9 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
   {
     f32x4 acc[MW1][NTW];
     wide_conv<C, MW1, MT1, G, AROT>(acc, a.w1, sX, d, nks, wm, a_lane, b_lane);
+    JANUS_PROF(2);
     __syncthreads();  // every wave is done reading sX: write silu(c1 + b1) over it
+    JANUS_PROF(3);
 #pragma unroll
     for (int n = 0; n < NTW; ++n) {
       const int co = (wn * NTW + n) * 16 + arow;
@@ -361,7 +385,7 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
           // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
-          v[rr] = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
+          v[rr] = WSILU(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
         }
         st_frag_f16_pairs(sS, LI, m * 16 + 4 * (lane >> 4), co, v, lane);
       }
@@ -388,13 +412,16 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
 #endif
     }
   };
+  JANUS_PROF(4);
   if constexpr (G::Cfg::EPF) epi_load();
 
   // ---- 3. c2 over BM rows (row r <-> time t0 + r): A = sS[r + tap]
   f32x4 acc2[MW2][NTW];
   wide_conv<C, MW2, MT2, G, AROT>(acc2, a.w2, sS, 1, nks, wm, a_lane, b_lane);
+  JANUS_PROF(5);
   if constexpr (!G::Cfg::EPF) epi_load();
   __syncthreads();  // sS dead: the fp32 epilogue tile takes its place
+  JANUS_PROF(6);
 
   // ---- 4. epilogue in NP row passes (WM == 1: every wave owns all m-tiles): c2 + b2 ->
   // fp32 LDS tile of RP rows, then 16-byte row chunks
@@ -439,16 +466,37 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       st_act(ob + (int64_t)(t0 + r) * C + cg, hv);
     }
   }
+  JANUS_PROF(7);
+#ifdef JANUS_PHASE_PROF
+  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 16 + 9] = (long long)wall_clock64();
+#endif
 }
 
-// A/B switches: JANUS_WIDE_STAGGER = sleeps (s_sleep 127 each) per block slot,
-// JANUS_WIDE_SLOT = blocks per slot round (the CUs the stream runs on)
-static void wide_stagger(int& st, int& slot) {
-  static const int st_ = std::getenv("JANUS_WIDE_STAGGER") ? std::atoi(std::getenv("JANUS_WIDE_STAGGER")) : 0;
-  static const int slot_ = std::getenv("JANUS_WIDE_SLOT") ? std::atoi(std::getenv("JANUS_WIDE_SLOT")) : 256;
-  st = st_;
-  slot = std::max(slot_, 1);
+#ifdef JANUS_PHASE_PROF
+// JANUS_PHASE_PROF=C,k,d: the first launch of that unit records into a device buffer
+static long long* g_prof = nullptr;
+static int g_prof_blocks = 0;
+static bool g_prof_done = false;
+static long long* phase_prof_target(int C, int k, int d, int blocks) {
+  const char* e = std::getenv("JANUS_PHASE_PROF");
+  if (!e || g_prof_done) return nullptr;
+  int pc = 0, pk = 0, pd = 0;
+  if (std::sscanf(e, "%d,%d,%d", &pc, &pk, &pd) != 3 || pc != C || pk != k || pd != d) return nullptr;
+  g_prof_done = true;
+  g_prof_blocks = blocks;
+  JANUS_HIP(hipMalloc(&g_prof, sizeof(long long) * 16 * (size_t)blocks));
+  JANUS_HIP(hipMemset(g_prof, 0, sizeof(long long) * 16 * (size_t)blocks));
+  return g_prof;
 }
+}  // namespace janus
+extern "C" int janus_debug_phase_read(long long* dst, int cap) {
+  if (!janus::g_prof) return 0;
+  const int n = std::min(cap, janus::g_prof_blocks);
+  if (hipMemcpy(dst, janus::g_prof, sizeof(long long) * 16 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
+}
+namespace janus {
+#endif
 
 template <int C, int V, int KC, int DC>
 static void wide_go(const ResUnitArgs& a, hipStream_t s) {
@@ -462,9 +510,11 @@ static void wide_go(const ResUnitArgs& a, hipStream_t s) {
     attr = true;
   }
   const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
-  int st = 0, slot = 256;
-  wide_stagger(st, slot);
-  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt, st, slot);
+  long long* prof = nullptr;
+#ifdef JANUS_PHASE_PROF
+  prof = phase_prof_target(C, a.k, a.d, tiles_per_utt * a.B);
+#endif
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt, prof);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -545,8 +595,7 @@ struct LdsGeo {
 // instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
 template <int C, bool EPF, int V>
 __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel(ResUnitArgs a,
-                                                                         int tiles_per_utt,
-                                                                         int stagger, int slot_blocks) {
+                                                                         int tiles_per_utt) {
   using G = LdsGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
   constexpr int CPR = G::CPR, MT1 = G::MT1, MT2 = G::MT2, MW1 = G::MW1, MW2 = G::MW2;
@@ -557,10 +606,6 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
   float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS and sW)
   _Float16* sW = smem + G::ACT_H;              // [2][C][LW]
 
-  if (stagger > 0 && (int)blockIdx.x < 4 * slot_blocks) {
-    const int n = (int)blockIdx.x / slot_blocks * stagger;
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   const int k = a.k, d = a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
@@ -622,7 +667,7 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
       }
     }
@@ -708,7 +753,7 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
           const int r = m * 16 + 4 * (lane >> 4) + rr;
           const int t = t0 - p2 + r;
           // c2 zero-pads its input outside [0, T): a 0/1 factor, not a branch per element
-          v[rr] = silu(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
+          v[rr] = WSILU(acc[j][n][rr] + bias) * ((r < R1 && t >= 0 && t < T) ? 1.0f : 0.0f);
         }
         st_frag_f16_pairs(sS, LI, m * 16 + 4 * (lane >> 4), co, v, lane);
       }
@@ -793,9 +838,7 @@ static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
     attr = true;
   }
   const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
-  int st = 0, slot = 256;
-  wide_stagger(st, slot);
-  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt, st, slot);
+  kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
   JANUS_LAUNCH_CHECK();
 }
 

@@ -826,31 +826,8 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
       for (int c = 0; c < ncu && c < 32 * (int)mask.size(); ++c)
         if (!((mask[c / 32] >> (c % 32)) & 1u)) masked = true;
     }
-    // JANUS_DEC_LANE_SPLIT (default on): lane i runs on its own share of the partition's CUs
-    // (every XCD's enabled CUs dealt to the lanes in turn: balanced per XCD and shader
-    // engine), so the lanes' latency-bound launch chains run side by side instead of
-    // queueing for the same CUs; each lane sizes its launches to its share
-    static const bool split = [] { const char* v = std::getenv("JANUS_DEC_LANE_SPLIT"); return v ? std::atoi(v) != 0 : true; }();
-    std::vector<std::vector<uint32_t>> lane_mask(nlanes, masked ? mask : std::vector<uint32_t>());
-    if (split && nlanes > 1) {
-      int ncu = 0;
-      JANUS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-      std::vector<uint32_t> all = mask;
-      if (!masked) std::fill(all.begin(), all.end(), 0xffffffffu);
-      for (auto& m : lane_mask) m.assign(mask.size(), 0u);
-      for (int x = 0; x < 8; ++x) {
-        int j = 0;
-        for (int c = x; c < ncu && c < 32 * (int)all.size(); c += 8)
-          if ((all[c / 32] >> (c % 32)) & 1u) {
-            lane_mask[j % nlanes][c / 32] |= 1u << (c % 32);
-            ++j;
-          }
-      }
-      masked = true;
-    }
     for (int i = 0; i < nlanes; ++i) {
       DecLane& Z = *w->lanes[i];
-      const std::vector<uint32_t>& mask = lane_mask[i];
       if (Z.stream && Z.stream_mask != (masked ? mask : std::vector<uint32_t>())) {
         JANUS_HIP(hipStreamSynchronize(Z.stream));
         JANUS_HIP(hipStreamDestroy(Z.stream));
@@ -889,9 +866,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
         }
         DecodeSampling ssub{};
         if (smp) ssub = DecodeSampling{smp->temperature, smp->seeds + b0};
-        janus_decode_options lopt = *opt;
-        if (split) lopt.cu_count = 0;  // read from the lane stream's CU mask
-        decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, &lopt,
+        decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, opt,
                       rows ? &sub : nullptr, tokens + (int64_t)b0 * maxlen, n_tokens + b0,
                       sum_logprob + b0, no_speech_prob ? no_speech_prob + b0 : nullptr, Z.stream,
                       nlanes > 1 ? &latch : nullptr, smp ? &ssub : nullptr);
