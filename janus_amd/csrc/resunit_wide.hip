@@ -134,6 +134,9 @@ __device__ __forceinline__ void wide_conv(f32x4 (&acc)[MW][G::NTW], const _Float
                                           const _Float16* src, int dil, int nks, int wm,
                                           int a_lane, int b_lane) {
   constexpr int NTW = G::NTW, NPB = G::NPB, LI = G::LI, WM = G::WM;
+  // at least one ring turn (k*C/32 >= NPB, checked at launch): without it the compiler
+  // guards the loop and sinks the ring preload into the guard, out of ring order
+  __builtin_assume(nks >= NPB);
   if constexpr (AROT) {
     // A fragments in ONE register set, refilled per m-tile: m-tile j's fragment for step
     // ks+1 is read as soon as step ks's MFMAs on it are issued, so it has the other MW-1
@@ -859,8 +862,8 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
   static const int w64 = std::getenv("JANUS_WIDE64_WAVES") ? std::atoi(std::getenv("JANUS_WIDE64_WAVES")) : 4;
   static const int w256 = std::getenv("JANUS_WIDE256_WAVES") ? std::atoi(std::getenv("JANUS_WIDE256_WAVES")) : 8;
   if (a.C == 64) {
-    static const bool ring64 = std::getenv("JANUS_WIDE64_CFG") && std::string(std::getenv("JANUS_WIDE64_CFG")) == "ring";
-    if (ring64) wide_cfg<64, 5>(a, s);
+    static const std::string c64 = std::getenv("JANUS_WIDE64_CFG") ? std::getenv("JANUS_WIDE64_CFG") : "lds";
+    if (c64 == "ring") wide_cfg<64, 5>(a, s);
     else if (w64 == 8) epf ? lds_cfg<64, true, 1>(a, s) : lds_cfg<64, false, 1>(a, s);
     else epf ? lds_cfg<64, true, 0>(a, s) : lds_cfg<64, false, 0>(a, s);
   }

@@ -9,7 +9,7 @@ for v in "$@"; do
   unset JANUS_LIB
   case "$v" in
     default) envs="" ;;
-    env:*) envs="${v#env:}" ;;
+    env:*) envs="${v#env:}"; envs="${envs//,/ }" ;;
     *) export JANUS_LIB=$v; envs="" ;;
   esac
   env $envs timeout -k 10 200 python -u tools/vocoder_ab.py --reps 3 2> gpurun_out/voc_ab.err | tail -1 || { tail -5 gpurun_out/voc_ab.err; exit 1; }
