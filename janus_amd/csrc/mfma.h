@@ -47,15 +47,24 @@ __device__ __forceinline__ float silu(float x) {
 // once): with JANUS_ACT_NT the accesses carry the non-temporal hint, so the multi-GB
 // vocoder stream does not displace what the concurrently running decoder re-reads
 // (encoder output, weights) from the caches.
-// Measured (overlapped bench step, r02): non-temporal OUTPUT stores are the default —
-// 324.3 -> 319.3 ms, both sides faster (decoder -5.5 ms: its re-read encoder output and
-// weights survive in the caches; vocoder -3 ms); non-temporal loads as well cost the
-// vocoder +4.5 ms (the tile's halo / residual re-reads then miss) for a -3 ms decoder.
-// Switches for A/B builds: JANUS_ACT_NT (loads too), or the parts _LD (tile staging
-// loads), _RES (epilogue residual / accumulator re-reads); JANUS_ACT_ST_PLAIN (plain stores).
-#ifdef JANUS_ACT_NT
+// Measured (overlapped bench step, r02): non-temporal OUTPUT stores — 324.3 -> 319.3 ms,
+// both sides faster (decoder -5.5 ms: its re-read encoder output and weights survive in
+// the caches; vocoder -3 ms); non-temporal loads as well then cost the vocoder +4.5 ms
+// (the tile's halo / residual re-reads missed) for a -3 ms decoder. r03 v3: with the wide
+// units' residual resident and the vocoder side ~11 ms shorter than the decoder's, every
+// activation access is non-temporal by default: decoder side 278.4 -> 275.7 ms, vocoder
+// side +2 ms, step 289.6-290.7 -> 287.2-287.9 ms (A/B on one box; the staging loads alone
+// change nothing, the gain is the residual / accumulator re-reads).
+// Switches for A/B builds: JANUS_ACT_LD_PLAIN (plain loads), or JANUS_ACT_NT_LD /
+// JANUS_ACT_NT_RES alone (tile staging loads / epilogue re-reads); JANUS_ACT_ST_PLAIN
+// (plain stores).
+#ifndef JANUS_ACT_LD_PLAIN
+#ifndef JANUS_ACT_NT_LD
 #define JANUS_ACT_NT_LD
+#endif
+#ifndef JANUS_ACT_NT_RES
 #define JANUS_ACT_NT_RES
+#endif
 #endif
 #ifndef JANUS_ACT_ST_PLAIN
 #define JANUS_ACT_NT_ST
