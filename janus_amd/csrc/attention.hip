@@ -647,13 +647,16 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
   const _Float16* kb = k + (int64_t)b * kv_bs + h * kHd + dg * 8;
   const _Float16* vb = v + (int64_t)b * kv_bs + h * kHd + dg * 8;
   // key of round i: 8 (i * kHeadWaves + w) + kg; rows past the cache clamp to its last
-  // row (finite values, weight 0) so every load is unconditional
+  // row (finite values, weight 0) so every load is unconditional. The cache rows are read
+  // non-temporal (r03 v3; JANUS_KV_PLAIN for A/B): the Infinity Cache is better spent on
+  // the encoder output the cross-attention re-reads 6x per position and on the weights —
+  // same-box pairs 286.8-295.6 vs 294.8-301.8 ms per step, decoder side -6 to -11 ms
   const int tl = Tkv - 1;
   uint4 kr[NR], vr[NR];
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
-#ifdef JANUS_KV_NT
+#ifndef JANUS_KV_PLAIN
     kr[i] = ld_nt(kb + (int64_t)t * kv_rs);
 #else
     kr[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)t * kv_rs);
@@ -662,7 +665,7 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int t = min(8 * (i * kHeadWaves + w) + kg, tl);
-#ifdef JANUS_KV_NT
+#ifndef JANUS_KV_PLAIN
     vr[i] = ld_nt(vb + (int64_t)t * kv_rs);
 #else
     vr[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)t * kv_rs);
