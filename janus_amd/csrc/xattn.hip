@@ -225,7 +225,12 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
     const int row = 4 * lg + r;
     if (row >= H) continue;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr] = accc[n][r];
+    for (int n = 0; n < NT; ++n)
+#ifndef JANUS_XPART_PLAIN  // partials written / read past the caches (r03 v4; A/B switch)
+      __builtin_nontemporal_store(accc[n][r], &pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr]);
+#else
+      pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr] = accc[n][r];
+#endif
   }
   if (lane == 0) {
 #pragma unroll
@@ -368,7 +373,15 @@ __global__ __launch_bounds__(1024) void xattn_combine_vproj_kernel(
       for (int s = 0; s < kXCombMax; ++s) {
         if (s < nsplit) {
           ml[s] = *reinterpret_cast<const float2*>(pml + ((int64_t)s * H + h) * 2);
+#ifndef JANUS_XPART_PLAIN
+        {
+          typedef float f2v __attribute__((ext_vector_type(2)));
+          const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(pc + (int64_t)s * HD));
+          v[s] = make_float2(t.x, t.y);
+        }
+#else
           v[s] = *reinterpret_cast<const float2*>(pc + (int64_t)s * HD);
+#endif
         }
       }
       float M = -INFINITY;
