@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
     const int i = tid + k * kPostThreads;
     const int t = t0 - kPostK / 2 + (i >> 1);
     pv[k] = (i < kPostRows * 2 && t >= 0 && t < T)
-                ? *reinterpret_cast<const uint4*>(xb + (int64_t)t * kPostC + (i & 1) * 8)
+                ? ld_act(xb + (int64_t)t * kPostC + (i & 1) * 8)  // non-temporal (mfma.h)
                 : make_uint4(0, 0, 0, 0);
   }
   for (int i = tid; i < kPostC * 16; i += kPostThreads) {
