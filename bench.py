@@ -53,7 +53,7 @@ def parse():
                     help="CUs per XCD (of 32) for the greedy decoder in the overlapped serving step "
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--fallback", action="store_true",
                     help="run faster-whisper's temperature fallback on windows failing their gates "
                          "(generate_with_fallback: 5 temperatures x best_of 5 sampled re-decodes); "
