@@ -405,7 +405,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   // do not depend on it); later tiles' loads are issued before the previous epilogue
   half8 bw[NB][NKS];
   uint4 sm16[NB];
-#ifdef JANUS_W_NT
+#if defined(JANUS_W_NT) || defined(JANUS_LG_NT)  // A/B: token-embedding stream past the caches
 #define LG_WLD(P) ([&]() { const uint4 u_ = ld_nt(P); return *reinterpret_cast<const half8*>(&u_); }())
 #else
 #define LG_WLD(P) (*reinterpret_cast<const half8*>(P))
