@@ -90,7 +90,11 @@ __global__ __launch_bounds__(kYinThreads) void yin_hops_kernel(
         const bool in_pcm = p >= 0 && p < n;
         const bool in_st = p < 0 && st != nullptr;
         const float* src = in_pcm ? pcm + base + p : (in_st ? st + kYinBuf + p : pcm);
+#ifdef JANUS_YIN_NT  // A/B: the window stream past the caches (YIN runs beside the decoder)
+        v[u] = __builtin_nontemporal_load(src);
+#else
         v[u] = *src;
+#endif
         v[u] = (in_pcm || in_st) ? v[u] : 0.0f;
       }
 #pragma unroll
