@@ -54,6 +54,15 @@ def parse():
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--no-idle-latency", action="store_true",
+                    help="skip the flush and the three idle-pipeline latency steps after the timed "
+                         "region (profiling runs: only priming, warm-up and timed overlapped steps "
+                         "then reach the kernel trace)")
+    ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4),
+                    help="BASELINE.json config: 4 (default) = the headline, its per-GPU share "
+                         "(64 x 30 s end to end); 1 = the 5 s WAV through the drop-in "
+                         "Transcriber + prosody + packet; 2 = tiny.en + vocoder on one 30 s "
+                         "utterance (latency); 3 = base.en encode-only, 64 x 30 s")
     ap.add_argument("--fallback", action="store_true",
                     help="run faster-whisper's temperature fallback on windows failing their gates "
                          "(generate_with_fallback: 5 temperatures x best_of 5 sampled re-decodes); "
@@ -61,7 +70,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model: str, tokens_per_utt: float):
+def cpu_baseline(model: str, tokens_per_utt: float, seed: int = 999):
     """Oracle (CPU restatement) time for ONE whole 30 s utterance of the workload, every
     stage measured, nothing scaled: log-mel of the clip, the encoder on its window, the
     sequential KV-cache greedy loop for as many tokens as the GPU emitted per utterance
@@ -83,7 +92,7 @@ def cpu_baseline(model: str, tokens_per_utt: float):
     cfg = jw.CONFIGS[model]
     W = jw.synthetic_weights(cfg, 0)
     tk = load_tokenizer()
-    x = synth_speech(999, AUDIO_SECONDS)
+    x = synth_speech(seed, AUDIO_SECONDS)
     n_tok = max(1, int(round(tokens_per_utt)))
     t = {}
     t0 = time.perf_counter()
@@ -142,6 +151,46 @@ def family_lines(fams, cu_share):
     return out
 
 
+def decoder_bytes(cfg, B, positions):
+    """Algorithmic HBM bytes the greedy decoder must move per position, at
+    batch B over `positions` steps (position p attends over p + 1 keys):
+      cross_attention  the encoder output, read once per layer (absorbed projections):
+                       L * B * Te * d * 2
+      self_attention   the K and V cache rows that exist, averaged over the positions:
+                       L * B * (positions + 1) / 2 * d * 2 * 2
+      layer_weights    per layer QKV 3d^2, O d^2, absorbed query H d^2, per-head value d^2,
+                       cross O d^2, fc1 4d^2, fc2 4d^2 (fp16): L * (14 + H) * d^2 * 2
+      vocab_projection the tied token embedding: V * d * 2
+    Activations (a few hundred KB per launch) are left out."""
+    d, H, L, Te, V = cfg.d_model, cfg.n_heads, cfg.dec_layers, cfg.n_audio_ctx, cfg.n_vocab
+    return {"cross_attention": L * B * Te * d * 2,
+            "self_attention": L * B * (positions + 1) / 2.0 * d * 2 * 2,
+            "layer_weights": L * (14 + H) * d * d * 2,
+            "vocab_projection": V * d * 2}
+
+
+def decoder_roofline(cfg, B, positions, launches, side_ms, cu_share):
+    """roofline.decoder: the side that sets the overlapped step. side_ms = decoder-side
+    wall time per step (HIP events on the decoder's CU-masked stream, timed region)."""
+    if not side_ms or positions <= 0:
+        return None
+    by = decoder_bytes(cfg, B, positions)
+    per_pos = sum(by.values())
+    us = side_ms * 1000.0 / positions
+    gbs = per_pos / (us * 1e-6) / 1e9
+    return {"kernel": "greedy decoder, one position (cross-attention, self-attention, "
+                      "projections, vocabulary projection + selection)",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "cu_share": cu_share,
+            "frac_of_cu_share": round(gbs / (HBM_PEAK_GBS * cu_share), 4),
+            "bytes_per_position": int(per_pos),
+            "bytes_breakdown": {k: int(v) for k, v in by.items()},
+            "positions": positions, "side_ms": round(side_ms, 2),
+            "us_per_position": round(us, 2),
+            "launches_per_position": round(launches / positions, 2) if launches else None,
+            "us_per_launch": round(us * positions / launches, 2) if launches else None}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -152,8 +201,275 @@ def _cpu_model():
     return "unknown"
 
 
+def _line(args, metric, value, unit, ms, config, **extra):
+    out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+           "higher_is_better": True, "scaling": "none (single GPU config)", "vs_baseline": None,
+           "dtype": "fp16",
+           "data": "synthetic (seeded source-filter speech; seeded synthetic weights)",
+           "config": config}
+    out.update(extra)
+    print(json.dumps(out), flush=True)
+
+
+def _timed(fn, steps, warmup):
+    """fn() once per step, host-synchronised, after `warmup` untimed calls: per-step
+    seconds."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        t.append(time.perf_counter() - t0)
+    return t
+
+
+def run_config1(args):
+    """BASELINE config 1: one 5 s 16 kHz mono WAV through the drop-in Transcriber
+    (transcriber.py:66-91, tiny.en) + ProsodyExtractor (prosody.py:45-104, on the 48 kHz
+    buffer whose [::3] is the WAV) + JanusPacket.serialize (protocol.py:57-121): the
+    reference's CPU plumbing path, here on the GPU; per-call latency and xRT."""
+    import tempfile
+    import wave
+    from janus_amd.common.protocol import JanusMode, JanusPacket
+    from janus_amd.services.prosody import ProsodyExtractor
+    from janus_amd.services.transcriber import Transcriber
+    from janus_amd.workload import synth_speech
+    secs = 5.0
+    x = synth_speech(1000, secs, sr=16000)
+    path = os.path.join(tempfile.mkdtemp(), "config1.wav")
+    with wave.open(path, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes((x * 32768).astype("<i2").tobytes())
+    tr = Transcriber("tiny.en")
+    if not args.fallback:   # the headline's setting (T = 0); --fallback: faster-whisper's default
+        import functools
+        tr.model.transcribe = functools.partial(tr.model.transcribe, temperature=0.0)
+    ex = ProsodyExtractor(48000)
+    buf48 = np.repeat(x, 3)
+    res = {}
+
+    def one():
+        text = tr.transcribe_file(path)
+        tags = ex.analyze_buffer(buf48)
+        res["packet"] = JanusPacket(text, JanusMode.SEMANTIC_VOICE, tags, "Auto", 1.0).serialize()
+        res["text"] = text
+    t = _timed(one, args.steps, args.warmup)
+    p50 = float(np.median(t))
+    _line(args, "config 1: 5 s WAV -> tiny.en STT + prosody + MessagePack, latency", secs / p50,
+          "xRT (audio-s/wall-s)", p50 * 1000.0,
+          {"workload": "5 s 16 kHz WAV through Transcriber('tiny.en').transcribe_file + "
+                       "ProsodyExtractor + JanusPacket.serialize", "model": "tiny.en",
+           "global_batch": 1, "fallback": bool(args.fallback)},
+          p50_latency_ms=round(p50 * 1000.0, 2), step_ms=[round(v * 1000.0, 2) for v in t],
+          packet_bytes=len(res["packet"]), roofline=None,
+          roofline_note="latency-bound single-utterance plumbing: no kernel near a roofline")
+
+
+def run_config2(args):
+    """BASELINE config 2: tiny.en encode (mel, encoder, greedy decoder, YIN, packet) + the
+    Firefly-GAN decode of the packet, ONE 30 s utterance, back to back on the whole GPU
+    (JanusPipeline.step); p50 latency over the timed steps, xRT = 30 s / p50."""
+    from janus_amd.pipeline import JanusPipeline
+    from janus_amd.services.transcriber import TEMPERATURES
+    from janus_amd.workload import synth_speech
+    dev = torch.device("cuda", 0)
+    x = synth_speech(2000, args.seconds)
+    offs = torch.tensor([0, len(x)], dtype=torch.int64, device=dev)
+    pcm = torch.from_numpy(np.concatenate([x, np.zeros(1, np.float32)])).to(dev)
+    frames = int(np.ceil(args.seconds * 44100 / 512))
+    pipe = JanusPipeline("tiny.en", max_length=args.max_length,
+                         temperatures=TEMPERATURES if args.fallback else (0.0,))
+    last = {}
+
+    def one():
+        last["r"] = pipe.step(pcm, offs, [len(x)], frames)
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    pipe.vocoder.conv_stats(reset=True)
+    pipe.vocoder.family_stats(reset=True)
+    pipe.vocoder.set_timing(True)
+    t = _timed(one, args.steps, 0)
+    pipe.vocoder.set_timing(False)
+    flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
+    fams = pipe.vocoder.family_stats(reset=True)
+    p50 = float(np.median(t))
+    ach = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
+    enc = last["r"][0]
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline("tiny.en", float(enc.n_tokens.float().mean().item()), seed=2000)
+        except Exception as e:
+            cpu = {"error": repr(e)}
+    _line(args, "config 2: tiny.en encode + Firefly-GAN decode, one 30 s utterance, p50 latency",
+          args.seconds / p50, "xRT (audio-s/wall-s)", p50 * 1000.0,
+          {"workload": f"1 x {args.seconds:g} s utterance: mel, tiny.en encoder, greedy decoder "
+                       "(<= 448 tokens), YIN, packet, then unpack, prompt, vocoder "
+                       f"({frames} frames)", "model": "tiny.en", "global_batch": 1,
+           "max_length": args.max_length, "fallback": bool(args.fallback)},
+          p50_latency_ms=round(p50 * 1000.0, 2), step_ms=[round(v * 1000.0, 2) for v in t],
+          tokens=int(enc.n_tokens[0].item()),
+          roofline={"kernel": "vocoder conv / fused ResBlock1 units (whole GPU, batch 1)",
+                    "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4),
+                    "traffic": None, "launches": int(launches),
+                    "avg_launch_ms": round(kms / max(launches, 1), 4),
+                    "families": family_lines(fams, 1.0)},
+          cpu_baseline=cpu)
+
+
+def encoder_flops(cfg, B):
+    """Algorithmic FLOPs of one encoder forward at batch B (30 s windows): conv1 (k3, 80 ->
+    d, 3000 frames) + conv2 (k3 stride 2, d -> d, 1500 frames), and per layer the
+    projections 24 T d^2 plus attention 4 T^2 d."""
+    d, T, L = cfg.d_model, cfg.n_audio_ctx, cfg.enc_layers
+    stem = 2 * 3 * (2 * T) * 80 * d + 2 * 3 * T * d * d
+    gemm = L * 24 * T * d * d
+    attn = L * 4 * T * T * d
+    return {"stem": B * stem, "projections": B * gemm, "attention": B * attn}
+
+
+def run_config3(args):
+    """BASELINE config 3: base.en encode-only (log-mel + encoder: conv stem, 6 layers of
+    MFMA attention / FFN) on 64 x 30 s utterances; xRT and the encoder's MFMA fraction,
+    plus per-kernel lines for the projection GEMM (gemm_big) and the attention kernel at
+    the same shapes (HIP events)."""
+    import math
+    from janus_amd import _native as nat
+    from janus_amd.whisper import CONFIGS, WhisperEngine
+    from janus_amd.workload import synth_speech
+    dev = torch.device("cuda", 0)
+    B = args.batch
+    cfg = CONFIGS[args.model]
+    utts = [synth_speech(3000 + i, args.seconds) for i in range(B)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
+    w = WhisperEngine(cfg, seed=0)
+
+    def one():
+        return w.encode(w.logmel(pcm, offs, B, 3))
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    mel_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t = []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        mel_ev[i][0].record()
+        mel = w.logmel(pcm, offs, B, 3)
+        mel_ev[i][1].record()
+        ev[i][0].record()
+        w.encode(mel)
+        ev[i][1].record()
+        torch.cuda.synchronize()
+        t.append(time.perf_counter() - t0)
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    mel_ms = float(np.mean([a.elapsed_time(b) for a, b in mel_ev]))
+    fl = encoder_flops(cfg, B)
+    tot = sum(fl.values())
+    ach = tot / (enc_ms * 1e-3) / 1e12
+    # the encoder's kernels at the same shapes, alone (kernel ABI, HIP events)
+    s = torch.cuda.current_stream().cuda_stream
+    M, d = B * cfg.n_audio_ctx, cfg.d_model
+    kern = []
+    g = torch.Generator(device=dev).manual_seed(1)
+    for name, N, K, epi in [("qkv", 3 * d, d, 0), ("o_resid", d, d, 2), ("fc1_gelu", 4 * d, d, 1),
+                            ("fc2_resid", d, 4 * d, 2)]:
+        A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).half()
+        Wm = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) / math.sqrt(K)).half()
+        bias = torch.randn(N, device=dev, generator=g)
+        C = torch.zeros(M, N, device=dev, dtype=torch.float32 if epi == 2 else torch.float16)
+
+        def run():
+            nat.call("janus_gemm_f16", epi, A.data_ptr(), K, Wm.data_ptr(), K, bias.data_ptr(),
+                     C.data_ptr(), N, C.data_ptr() if epi == 2 else None, N, M, N, K, s)
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 100.0
+        tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+        kern.append({"kernel": f"gemm_big {name} ({M}x{N}x{K})", "us": round(us, 1),
+                     "achieved_tflops": round(tf, 1), "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4)})
+        del A, Wm, C
+    qkv = (torch.randn(B, cfg.n_audio_ctx, 3 * d, device=dev, generator=g) * 1.5).half()
+    out = torch.empty(B, cfg.n_audio_ctx, d, dtype=torch.float16, device=dev)
+    run = lambda: nat.call("janus_attention_f16", qkv.data_ptr(), out.data_ptr(), B,
+                           cfg.n_audio_ctx, cfg.n_heads, 0.125, s)
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 100.0
+    tf = 4.0 * B * cfg.n_heads * cfg.n_audio_ctx ** 2 * 64 / (us * 1e-6) / 1e12
+    kern.append({"kernel": f"attention_st ({B} x {cfg.n_heads} heads x {cfg.n_audio_ctx}^2)",
+                 "us": round(us, 1), "achieved_tflops": round(tf, 1),
+                 "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4)})
+    step_s = (mel_ms + enc_ms) / 1000.0
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_encoder_baseline(args.model)
+        except Exception as e:
+            cpu = {"error": repr(e)}
+    _line(args, "config 3: base.en encode-only, batch 64 x 30 s, xRT and MFMA fraction",
+          B * args.seconds / step_s, "xRT (audio-s/wall-s)", step_s * 1000.0,
+          {"workload": f"log-mel + {args.model} encoder, {B} x {args.seconds:g} s", "model": args.model,
+           "global_batch": B, "seq_len": cfg.n_audio_ctx},
+          mel_ms=round(mel_ms, 3), encoder_ms=round(enc_ms, 3),
+          host_step_ms=[round(v * 1000.0, 2) for v in t],
+          roofline={"kernel": "Whisper encoder forward (stem conv, QKV/O/fc1/fc2 on gemm_big, "
+                              "attention_st), HIP events around the encoder",
+                    "bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4),
+                    "traffic": None, "flops": {k: float(v) for k, v in fl.items()},
+                    "kernels": kern},
+          cpu_baseline=cpu)
+
+
+def cpu_encoder_baseline(model):
+    """Oracle log-mel + encoder for ONE 30 s utterance (numpy / torch fp32)."""
+    from janus_amd import whisper as jw
+    from janus_amd.workload import synth_speech
+    from oracle import whisper as ow
+    affinity = len(os.sched_getaffinity(0))
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    torch.set_num_threads(threads)
+    cfg = jw.CONFIGS[model]
+    W = jw.synthetic_weights(cfg, 0)
+    x = synth_speech(3999, AUDIO_SECONDS)
+    t0 = time.perf_counter()
+    mel = ow.logmel(x, 3, jw.mel_filters())
+    ow.encoder(mel[None], W, cfg)
+    dt = time.perf_counter() - t0
+    return {"value": AUDIO_SECONDS / dt, "unit": "xRT (audio-s/wall-s)", "cores": threads,
+            "kind": "port", "sample": "oracle log-mel + fp32 encoder, one 30 s utterance",
+            "cpu_model": _cpu_model()}
+
+
 def main():
     args = parse()
+    if args.config in (1, 2, 3):
+        torch.cuda.set_device(0)
+        {1: run_config1, 2: run_config2, 3: run_config3}[args.config](args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -205,6 +521,7 @@ def main():
         dist.barrier()
     pipe.vocoder.conv_stats(reset=True)
     pipe.vocoder.set_timing(True)
+    pipe.side_events = [] if args.overlap > 0 else None
     times = []
     tok_counts = []
     if use_dist:
@@ -222,15 +539,18 @@ def main():
         dist.barrier()
     t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
+    sides = [(e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in (pipe.side_events or [])]
+    pipe.side_events = None
+    dec_positions, dec_launches = pipe.whisper.decode_info()
     tok_counts = [float(n.float().mean().item()) for n in tok_counts]
     fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
     # latency of one batch through an IDLE pipeline (encode then decode back to back, nothing
     # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
     idle = []
-    if args.overlap > 0:
+    if args.overlap > 0 and not args.no_idle_latency:
         pipe.flush(frames)
-    for _ in range(3):
+    for _ in range(0 if args.no_idle_latency else 3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         pipe.step(pcm, offs, lengths, frames)
@@ -298,7 +618,11 @@ def main():
                 [a + b for a, b in zip(times[:-1], times[1:])] if args.overlap > 0 and len(times) > 1
                 else times)) * 1000.0, 2),
             # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
-            "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2),
+            "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
+            # wall time of the two CU partitions per timed step (HIP events on each side's
+            # stream): vocoder + YIN, greedy decoder
+            "side_ms": {"vocoder": [round(a, 1) for a, _ in sides],
+                        "decoder": [round(b, 1) for _, b in sides]} if sides else None,
             "overlap": args.overlap,
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
@@ -334,6 +658,13 @@ def main():
                 # and algorithmic HBM rate against their peaks on the CU share; "bound" =
                 # the resource nearer its roofline (the narrow units are not MFMA-bound)
                 "families": family_lines(fams, cu_share),
+                # the side that sets the overlapped step: the greedy decoder against its
+                # HBM roofline (algorithmic bytes per position / decoder-side time per
+                # position; launches per position from the captured decode graphs)
+                "decoder": decoder_roofline(
+                    pipe.whisper.cfg, B, dec_positions, dec_launches,
+                    float(np.mean([b for _, b in sides])) if sides else None,
+                    round(1.0 - cu_share, 4) if args.overlap > 0 else 1.0),
             },
             "cpu_baseline": None,
         }

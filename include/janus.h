@@ -299,6 +299,15 @@ int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* enc, int ba
                                    int32_t* n_tokens, float* sum_logprob, float* no_speech_prob,
                                    void* stream);
 
+/*
+ * Shape of the last decode call on this context (lane 0): positions the decoder stepped
+ * (every row together; the early-exit poll stops at a 16-position boundary) and the
+ * kernel launches those positions issued (nodes of the captured decode graphs; 0 when
+ * JANUS_NO_GRAPH runs without graphs). Measurement only (bench.py's decoder roofline:
+ * launches per position beside bytes per position); the reference has no counterpart.
+ */
+int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* launches);
+
 /* ------------------------------------------------------------ vocoder --- */
 /*
  * Local Firefly-GAN decoder (fish-speech HiFiGANGenerator architecture) replacing the

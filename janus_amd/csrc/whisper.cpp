@@ -66,6 +66,9 @@ struct DecLane {
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
       d_xc, d_xpc, d_xpml, d_enc, d_seed;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
+  std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
+  int last_positions = 0;        // positions the last decode stepped
+  int64_t last_launches = 0;     // kernel launches those positions issued (graph nodes)
   hipStream_t stream = nullptr;  // graph capture needs a non-null stream
   std::vector<uint32_t> stream_mask;  // CU mask the lane stream was created with (empty: none)
   hipEvent_t ev_done = nullptr;
@@ -139,6 +142,7 @@ static void prepare(janus_whisper* w, hipStream_t s) {
   for (auto& lane : w->lanes) {
     for (auto& kv : lane->graphs) (void)hipGraphExecDestroy(kv.second);
     lane->graphs.clear();
+    lane->graph_nodes.clear();
   }
   const auto& c = w->cfg;
   const int d = c.d_model, ff = 4 * d;
@@ -622,9 +626,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
     Z.graphs.clear();
+    Z.graph_nodes.clear();
   }
+  Z.last_positions = 0;
+  Z.last_launches = 0;
   for (int p0 = 0; p0 + 1 < maxlen; p0 += chunk) {
     const int n = std::min(chunk, maxlen - 1 - p0);
+    Z.last_positions += n;
     if (use_graph) {
       std::vector<int64_t> key = base_key;
       key.push_back(p0);
@@ -642,12 +650,16 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           throw;
         }
         JANUS_HIP(hipStreamEndCapture(s, &g));
+        size_t nodes = 0;
+        JANUS_HIP(hipGraphGetNodes(g, nullptr, &nodes));
         hipGraphExec_t ge;
         JANUS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         JANUS_HIP(hipGraphDestroy(g));
         it = Z.graphs.emplace(key, ge).first;
+        Z.graph_nodes[key] = nodes;
       }
       JANUS_HIP(hipGraphLaunch(it->second, s));
+      Z.last_launches += (int64_t)Z.graph_nodes[key];
     } else {
       for (int pos = p0; pos < p0 + n; ++pos) step(pos);
     }
@@ -786,6 +798,15 @@ extern "C" int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* 
                       &smp);
 }
 
+extern "C" int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* launches) {
+  return guarded([&] {
+    JANUS_CHECK(w && positions && launches, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    *positions = w->lanes.empty() ? 0 : w->lanes[0]->last_positions;
+    *launches = w->lanes.empty() ? 0 : w->lanes[0]->last_launches;
+  });
+}
+
 static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
                         const janus_decode_options* opt, const janus_decode_rows* rows,
                         int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
@@ -834,6 +855,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
         Z.stream = nullptr;
         for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
         Z.graphs.clear();
+        Z.graph_nodes.clear();
       }
       if (!Z.stream) {
         if (masked)

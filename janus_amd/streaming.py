@@ -29,6 +29,7 @@ import torch
 from . import _native as nat
 from .common.protocol import JanusMode, JanusPacket
 from .services.prosody import YIN_BUF, energy_tag, pitch_tag, prosody_launch
+from .services.transcriber import TEMPERATURES
 from .services.vad import VAD_CENTER_DB, VAD_WIDTH_DB, MultiStreamGate, VoiceActivityDetector
 
 CHUNK = 1536                  # audio_io.py:28-31 (48 kHz int16 -> f32 chunks)
@@ -111,10 +112,11 @@ class StreamingEncoder:
     def __init__(self, n_streams: int, whisper, max_length: int = 448,
                  mode: JanusMode = JanusMode.SEMANTIC_VOICE, override="auto",
                  vad_threshold: float = 0.5, hop: int = 512, asynchronous: bool = False,
-                 receiver=None, vad_weights: dict = None, temperatures=(0.0,)):
-        """temperatures: (0.0,) decodes each phrase window at T = 0 (gates reported, not
-        acted on); services.transcriber.TEMPERATURES adds faster-whisper's fallback, as
-        the reference's transcribe_buffer runs it."""
+                 receiver=None, vad_weights: dict = None, temperatures=TEMPERATURES):
+        """temperatures: faster-whisper's fallback schedule, as the reference's
+        transcribe_buffer runs it (the default); (0.0,) decodes each window once at T = 0
+        and never re-decodes (the config-5 stream bench's setting on synthetic weights,
+        whose windows all fail the gates: DESIGN.md §0)."""
         self.device = nat.require_gpu()
         self.temperatures = tuple(float(t) for t in temperatures)
         self.S = n_streams
@@ -130,7 +132,8 @@ class StreamingEncoder:
         self.receiver = receiver    # JanusPipeline-like .decode(packets, frames), or None
         self.asynchronous = asynchronous
         self.max_queue = 0
-        self.long_phrases = 0       # phrases over one 30 s window (full seek loop)
+        self.long_phrases = 0       # phrases over one 30 s window
+        self.extra_windows = 0      # seek-loop windows beyond each phrase's first
         if asynchronous:
             self._jobs = queue.Queue()
             self._results = queue.Queue()
@@ -242,9 +245,19 @@ class StreamingEncoder:
         offs = torch.from_numpy(offs_np).to(self.device)
         B = len(done)
         w = self.whisper
-        mel = w.logmel(pcm, offs, B, 3)                 # transcriber.py:51 [::3]
-        enc = w.encode(mel)
-        dec = w.decode_ex(enc, max_length=self.max_length)
+        # every phrase through faster-whisper's generate_segments, as the engine's
+        # transcribe_buffer call runs it (engine.py:514 -> transcriber.py:29-64): the
+        # phrases' first windows are one GPU batch, failing windows take the temperature
+        # fallback, and a phrase whose first window's seek stops short of its content
+        # (a trailing timestamp pair, or longer than 30 s) continues with the next window
+        # in the following round of the same batched loop
+        from .services.transcriber import generate_segments
+        auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in range(B)]
+        streams_st = generate_segments(w, auds, max_length=self.max_length,
+                                       temperatures=self.temperatures)
+        texts = [' '.join(sg.text.strip() for sg in st.segments).strip() for st in streams_st]
+        self.long_phrases += sum(1 for n in lengths if (n + 2) // 3 > WINDOW_16K)
+        self.extra_windows += sum(st.windows - 1 for st in streams_st)
         # prosody in rounds: round r takes every channel's r-th phrase of this tick, so a
         # channel that completed two phrases runs them in order, the second from the first's
         # end state (one aubio object per channel, prosody.py:32)
@@ -276,19 +289,6 @@ class StreamingEncoder:
                     tags[i] = t
         except Exception:                               # engine.py:520-525
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        from .pipeline import _texts_and_gates
-        texts, _ = _texts_and_gates(w, dec, self.temperatures, enc)
-        # a phrase longer than one 30 s window (continuous speech with no 0.5 s pause) gets
-        # the whole seek loop, as the engine's transcribe_buffer call does
-        # (engine.py:514 -> transcriber.py:53-64), instead of its first window only
-        long = [i for i, n in enumerate(lengths) if (n + 2) // 3 > WINDOW_16K]
-        if long:
-            from .services.transcriber import generate_segments
-            auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in long]
-            for i, st in zip(long, generate_segments(w, auds, max_length=self.max_length,
-                                                     temperatures=self.temperatures)):
-                texts[i] = ' '.join(sg.text.strip() for sg in st.segments).strip()
-            self.long_phrases += len(long)
         ts = time.time() if timestamp is None else timestamp
         res = []
         for s, t, g in zip(streams, texts, tags):

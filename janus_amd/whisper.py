@@ -351,6 +351,13 @@ class WhisperEngine:
         del keep, pr
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 
+    def decode_info(self):
+        """(positions stepped, kernel launches issued) by the last decode call
+        (janus_whisper_decode_info: captured graph nodes; measurement only)."""
+        pos, lau = ctypes.c_int32(0), ctypes.c_int64(0)
+        nat.call("janus_whisper_decode_info", self._h, ctypes.addressof(pos), ctypes.addressof(lau))
+        return int(pos.value), int(lau.value)
+
     def texts(self, tokens: torch.Tensor, prompt_lens=None):
         """Host-side detokenisation of decoded rows (after each row's prompt)."""
         t = tokens.cpu().numpy()

@@ -5,8 +5,11 @@ fp32 torch CPU restatement of the decode path that replaces the reference's clou
 docstring) and the fish-speech Firefly-GAN HiFiGANGenerator forward (conv_pre ->
 [SiLU, ConvTranspose1d, ParallelBlock(ResBlock1 x 3)] x 5 -> SiLU -> conv_post ->
 tanh), written from the public architecture. No reference implementation exists in
-/root/reference (its TTS is remote), so vocoder parity is GPU-vs-this-oracle only
-("parity unpinned" against any external vocoder).
+/root/reference (its TTS is remote). The generator's topology is pinned externally:
+with its activation switched to leaky ReLU it equals transformers' HiFi-GAN V1
+``SpeechT5HifiGan`` (transformers 5.15) on the same weights to 1e-5
+(tests/test_oracle_vocoder.py); only the SiLU choice and the front end stay
+build-defined.
 """
 import numpy as np
 import torch
@@ -55,13 +58,21 @@ def speaker(clips16k, W):
 
 
 @torch.no_grad()
-def generator(lat, W, cfg, pre_tanh=False):
+def generator(lat, W, cfg, pre_tanh=False, act=F.silu, post_act=None):
     """lat [B][F][latent] -> wav [B][F*prod(rates)] (fp32); with pre_tanh also the
-    conv_post output before tanh."""
+    conv_post output before tanh.
+
+    ``act`` is the activation ahead of every upsampler and every ResBlock1 conv,
+    ``post_act`` the one ahead of conv_post (default: ``act``). Firefly-GAN (the build)
+    uses SiLU throughout. With ``act = leaky_relu(0.1)`` and ``post_act = leaky_relu(0.01)``
+    the same function is HiFi-GAN V1, which pins this restatement's topology (padding,
+    dilation, transposed-conv upsampling, ParallelBlock mean, conv_post, tanh) against
+    transformers' ``SpeechT5HifiGan`` on shared weights (tests/test_oracle_vocoder.py)."""
+    post_act = act if post_act is None else post_act
     x = torch.as_tensor(lat, dtype=torch.float32).transpose(1, 2)
     x = F.conv1d(x, _t(W, "conv_pre.weight"), _t(W, "conv_pre.bias"), padding=(cfg.pre_kernel - 1) // 2)
     for i, u in enumerate(cfg.up_rates):
-        x = F.silu(x)
+        x = act(x)
         x = F.conv_transpose1d(x, _t(W, f"ups.{i}.weight"), _t(W, f"ups.{i}.bias"), stride=u,
                                padding=u // 2)
         outs = []
@@ -69,16 +80,16 @@ def generator(lat, W, cfg, pre_tanh=False):
             y = x
             p = f"resblocks.{i}.blocks.{j}"
             for m, d in enumerate(cfg.rb_dilations):
-                xt = F.silu(y)
+                xt = act(y)
                 xt = F.conv1d(xt, _t(W, f"{p}.convs1.{m}.weight"), _t(W, f"{p}.convs1.{m}.bias"),
                               padding=d * (k - 1) // 2, dilation=d)
-                xt = F.silu(xt)
+                xt = act(xt)
                 xt = F.conv1d(xt, _t(W, f"{p}.convs2.{m}.weight"), _t(W, f"{p}.convs2.{m}.bias"),
                               padding=(k - 1) // 2)
                 y = xt + y
             outs.append(y)
         x = torch.stack(outs, 0).mean(0)
-    x = F.silu(x)
+    x = post_act(x)
     x = F.conv1d(x, _t(W, "conv_post.weight"), _t(W, "conv_post.bias"), padding=(cfg.post_kernel - 1) // 2)
     return (torch.tanh(x)[:, 0], x[:, 0]) if pre_tanh else torch.tanh(x)[:, 0]
 

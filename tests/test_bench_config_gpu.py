@@ -45,7 +45,9 @@ def test_bench_workload_rows_match_oracle(gpu):
     lengths = [len(u) for u in utts]
     offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
-    pipe = JanusPipeline("base.en", max_length=448)
+    # the bench's headline setting: T = 0, gates reported (bench.py without --fallback)
+    pipe = JanusPipeline("base.en", max_length=448, temperatures=(0.0,))
+    pipe.keep_encoder_output = True
     # the bench's step: the batch enters the overlapped pipeline, flush renders it
     assert pipe.step_overlapped(pcm, offs, lengths, FRAMES, 16, timestamp=TS) == (None, None, None)
     enc_gpu = pipe.last_encoder_output.float().cpu()
@@ -86,6 +88,11 @@ def test_bench_workload_rows_match_oracle(gpu):
             text = tk.transcript(r)
             assert res.texts[b] == text
             assert res.packets[b] == opk.serialize(text, 0, tags, "auto", TS), b
+        # every row, diverged or not: the packet is the oracle packer's on the GPU's own
+        # tokens (detokenise + tags + MessagePack are exact; only a near-tie token differs)
+        own = tk.transcript(g)
+        assert res.texts[b] == own
+        assert res.packets[b] == opk.serialize(own, 0, tags, "auto", TS), b
     print(f"bench rows: {identical}/{len(rows)} token sequences identical")
     assert identical >= len(rows) - 1
     # the 30 s waveforms of two rows vs the fp32 generator

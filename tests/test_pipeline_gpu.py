@@ -47,6 +47,23 @@ def test_transcriber_wav(gpu, tmp_path):
     t1 = tr.transcribe_file(str(path))
     t2 = tr.transcribe_buffer(np.repeat(x, 3))  # 48 kHz buffer whose [::3] is x
     assert isinstance(t1, str) and t1 == t2
+    # BASELINE config 1 against the oracle: faster-whisper's seek loop with its default
+    # temperature fallback, restated (oracle/whisper.py transcribe_segments) on the same
+    # seeded tiny.en weights and the same int16 samples (tests/golden/
+    # make_config1_transcript.py wrote the fixture)
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "config1_transcript.json")))
+    assert t1 == gold["text"], (t1, gold["text"])
+    before = dict(tr.model.stats)
+    segs, _ = tr.model.transcribe(str(path), beam_size=1, language="en")
+    got = [[s.start, s.end, s.text, list(s.tokens)] for s in segs]
+    assert [g[2:] for g in got] == [g[2:] for g in gold["segments"]]
+    assert np.allclose([g[:2] for g in got], [g[:2] for g in gold["segments"]])
+    for k, ko in (("windows", "windows"), ("needs_fallback", "needs_fallback"),
+                  ("no_speech_skips", "skips"), ("fallback_decodes", "fallback_decodes")):
+        assert tr.model.stats[k] - before[k] == gold["counters"][ko], k
 
 
 @pytest.mark.parametrize("yin_dec", ["0", "1"])

@@ -30,7 +30,7 @@ def main():
     utts = [synth_speech(4000 + i, 30.0) for i in range(B)]
     offs = torch.tensor(np.concatenate([[0], np.cumsum([len(u) for u in utts])]), dtype=torch.int64, device=dev)
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
-    pipe = JanusPipeline("base.en", max_length=448)
+    pipe = JanusPipeline("base.en", max_length=448, temperatures=(0.0,))
     w = pipe.whisper
     enc = w.encode(w.logmel(pcm, offs, B, 3))
     frames = 2584

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--block-ms", type=int, default=320)
     ap.add_argument("--async", dest="asyn", type=int, default=1)
     ap.add_argument("--duplex", type=int, default=1)
+    ap.add_argument("--fallback", action="store_true",
+                    help="faster-whisper's temperature fallback on failing windows (the library "
+                         "default); off by default here: seeded synthetic weights fail every window")
     a = ap.parse_args()
     import time
     import torch
@@ -53,14 +56,16 @@ def main():
             t += n + int(rng.uniform(0.6, 2.0) * 48000)
             k += 1
     w = WhisperEngine(CONFIGS[a.model], seed=0)
+    from janus_amd.services.transcriber import TEMPERATURES
+    temps = TEMPERATURES if a.fallback else (0.0,)
     rx = None
     if a.duplex:
         from janus_amd.pipeline import JanusPipeline
         rx = JanusPipeline(a.model, max_length=8)   # its vocoder renders the far end
     enc = StreamingEncoder(a.streams, w, max_length=a.max_length, asynchronous=bool(a.asyn),
-                           receiver=rx)
+                           receiver=rx, temperatures=temps)
     # warm-up: one block of silence + one short phrase batch (graph capture, allocations)
-    warm = StreamingEncoder(a.streams, w, max_length=a.max_length, receiver=rx)
+    warm = StreamingEncoder(a.streams, w, max_length=a.max_length, receiver=rx, temperatures=temps)
     z = np.zeros((a.streams, per_block * CHUNK), np.float32)
     sp = np.tile(synth_speech(1, per_block * CHUNK / 48000.0)[None, :per_block * CHUNK], (a.streams, 1))
     warm.push(sp)
@@ -93,7 +98,8 @@ def main():
            "worker_max_queue": enc.max_queue,
            "wall_s": round(t_total, 2), "audio_s": round(n_blocks * a.block_ms / 1000.0, 2),
            "realtime": bool(np.percentile(lat, 99) < a.block_ms and np.percentile(plat, 99) < a.block_ms),
-           "model": a.model, "max_length": a.max_length,
+           "model": a.model, "max_length": a.max_length, "fallback": bool(a.fallback),
+           "extra_seek_windows": enc.extra_windows,
            "data": "synthetic seeded speech phrases with silences; energy speech gate; seeded synthetic weights"}
     print(json.dumps(res), flush=True)
 
