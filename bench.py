@@ -261,6 +261,13 @@ def run_config1(args):
         res["text"] = text
     t = _timed(one, args.steps, args.warmup)
     p50 = float(np.median(t))
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_config1(x, buf48, args.fallback)
+            cpu["packet_equal"] = cpu.pop("packet") == res["packet"]
+        except Exception as e:
+            cpu = {"error": repr(e)}
     _line(args, "config 1: 5 s WAV -> tiny.en STT + prosody + MessagePack, latency", secs / p50,
           "xRT (audio-s/wall-s)", p50 * 1000.0,
           {"workload": "5 s 16 kHz WAV through Transcriber('tiny.en').transcribe_file + "
@@ -268,7 +275,37 @@ def run_config1(args):
            "global_batch": 1, "fallback": bool(args.fallback)},
           p50_latency_ms=round(p50 * 1000.0, 2), step_ms=[round(v * 1000.0, 2) for v in t],
           packet_bytes=len(res["packet"]), roofline=None,
-          roofline_note="latency-bound single-utterance plumbing: no kernel near a roofline")
+          roofline_note="latency-bound single-utterance plumbing: no kernel near a roofline",
+          cpu_baseline=cpu)
+
+
+def cpu_config1(x16, buf48, fallback):
+    """Config 1 on the CPU oracle, the whole job (the reference's own path is CPU): the
+    seek loop (oracle.whisper.transcribe_segments, T = 0 unless --fallback) on the WAV's
+    int16 samples, the stateful prosody oracle on the 48 kHz buffer, the oracle packer."""
+    from janus_amd import whisper as jw
+    from janus_amd.tokenizer import load_tokenizer
+    from oracle import packet as opk
+    from oracle import whisper as ow
+    from oracle.prosody import OracleProsody
+    affinity = len(os.sched_getaffinity(0))
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    torch.set_num_threads(threads)
+    cfg = jw.CONFIGS["tiny.en"]
+    W = jw.synthetic_weights(cfg, 0)
+    tk = load_tokenizer()
+    a = (x16 * 32768).astype("<i2").astype(np.float32) / 32768.0
+    temps = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0) if fallback else (0.0,)
+    t0 = time.perf_counter()
+    segs, _ = ow.transcribe_segments(a, W, cfg, tk, jw.mel_filters(), temperatures=temps)
+    text = " ".join(sg[2].strip() for sg in segs).strip()
+    tags = OracleProsody(48000).analyze_buffer(buf48)[0]
+    pk = opk.serialize(text, 0, tags, "Auto", 1.0)
+    dt = time.perf_counter() - t0
+    return {"value": (len(x16) / 16000.0) / dt, "unit": "xRT (audio-s/wall-s)", "cores": threads,
+            "kind": "port", "latency_ms": round(dt * 1000.0, 1), "packet": pk,
+            "sample": "the whole config-1 job on the oracle: seek loop + prosody + packer",
+            "cpu_model": _cpu_model()}
 
 
 def run_config2(args):
@@ -297,8 +334,8 @@ def run_config2(args):
     pipe.vocoder.set_timing(True)
     t = _timed(one, args.steps, 0)
     pipe.vocoder.set_timing(False)
+    fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
-    fams = pipe.vocoder.family_stats(reset=True)
     p50 = float(np.median(t))
     ach = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
     enc = last["r"][0]

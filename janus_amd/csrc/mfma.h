@@ -81,6 +81,27 @@ __device__ __forceinline__ uint4 ld_act(const _Float16* p) {  // tile staging
   return *reinterpret_cast<const uint4*>(p);
 #endif
 }
+// Tile staging with the halo rows a neighbouring tile re-reads kept in L2 (r04): a row read
+// by two tiles (the (k-1)d + halo-recompute rows at either end of a tile's window) is
+// loaded with the default policy so the neighbour (same XCD: tile_remap) finds it in L2;
+// rows only this tile reads stay non-temporal. `keep` must be wave-uniform (one load form
+// per wave, no exec-masked pair). JANUS_HALO_NT: every staging load non-temporal (r03).
+// JANUS_STAGE_PLAIN (A/B build): the callers keep EVERY staged row (the C = 64 / 32 units'
+// epilogues re-read their body rows as the residual).
+#ifdef JANUS_STAGE_PLAIN
+#define JANUS_STAGE_KEEP_ALL 1
+#else
+#define JANUS_STAGE_KEEP_ALL 0
+#endif
+__device__ __forceinline__ uint4 ld_act_halo(const _Float16* p, bool keep) {
+#if defined(JANUS_ACT_NT_LD) && !defined(JANUS_HALO_NT)
+  if (keep) return *reinterpret_cast<const uint4*>(p);
+  return ld_nt(p);
+#else
+  (void)keep;
+  return ld_act(p);
+#endif
+}
 __device__ __forceinline__ uint4 ld_res(const _Float16* p) {  // epilogue re-reads
 #ifdef JANUS_ACT_NT_RES
   return ld_nt(p);

@@ -134,8 +134,11 @@ __global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int til
       const int idx = tid + i * NT;                                                         \
       const int r = idx / CPR, cc = idx % CPR;                                              \
       const int t = t0_ - P2 - P1 + r;                                                      \
+      const int rw_ = w * (64 / CPR) + i * (NT / CPR);                                      \
       pf[i] = (L_ < n_tiles && r < R0  && t >= 0 && t < T)                                 \
-                  ? ld_act(xb_ + (int64_t)t * C + cc * 8)                                 \
+                  ? ld_act_halo(xb_ + (int64_t)t * C + cc * 8,                              \
+                                C == 32 && (JANUS_STAGE_KEEP_ALL || rw_ < R0 - BM ||        \
+                                            rw_ + 64 / CPR > BM))                           \
                   : make_uint4(0, 0, 0, 0);                                                 \
     }                                                                                       \
   } while (0)

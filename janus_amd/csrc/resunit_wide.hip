@@ -650,15 +650,20 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
   // ---- 1. stage silu(x): all loads in flight, then convert + store
   {
     const int xbase = t0 - p2 - p1;
+    // window rows [0, R0 - BM) are the previous tile's, [BM, R0) the next tile's: those
+    // stay in L2 for the neighbour (per wave: any of its rows shared)
+    const int wr0 = wid * 64 / CPR;  // first window row of this wave at i = 0
     uint4 pf[G::NLD];
 #pragma unroll
     for (int i = 0; i < G::NLD; ++i) {
       const int idx = tid + i * NT;
       const int r = idx / CPR, cc = idx % CPR;
       const int t = xbase + r;
+      const int rw = wr0 + i * (NT / CPR);  // wave-uniform
+      const bool keep = JANUS_STAGE_KEEP_ALL || rw < R0 - BM || rw + 64 / CPR > BM;
       // unconditional load of a clamped row, zeroed below (no branch per load)
       const int tc = min(max(t, 0), T - 1);
-      pf[i] = ld_act(xb + (int64_t)tc * C + cc * 8);
+      pf[i] = ld_act_halo(xb + (int64_t)tc * C + cc * 8, keep);
       if (!(r < R0 && t >= 0 && t < T)) pf[i] = make_uint4(0, 0, 0, 0);
     }
     WIDE_WLOAD(rwA0, rwA1, a.w1, 0);
