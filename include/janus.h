@@ -269,6 +269,13 @@ typedef struct {
   const int32_t* prompt_lens;
   int stride;
   int no_speech_token;
+  /* Shared encoder outputs (faster-whisper's best_of hypotheses of one window,
+   * transcriber.py:53-57 with the library's defaults): enc_index [host] int32 [B], row b
+   * attends to encoder row enc_index[b] of enc, which then holds n_enc rows [n_enc][Te][d]
+   * instead of B. The cross-attention reads each shared row once per PAIR of decoder rows
+   * (both rows' heads in one MFMA tile). NULL = row b attends to enc row b. */
+  const int32_t* enc_index;
+  int n_enc;
 } janus_decode_rows;
 
 /*

@@ -632,19 +632,25 @@ void gemm_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(p.K % 8 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: K/lda/ldw must be multiples of 8");
   JANUS_CHECK(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-byte aligned");
   if (p.M <= 0 || p.N <= 0) return;
-  JANUS_CHECK(p.M <= 64 || (epi != EPI_QKV && !p.ln_part),
-              "gemm: the KV-cache and LayerNorm-piece epilogues need M <= 64");
-  JANUS_CHECK(p.a_group_cols == 0 || (p.M <= 64 && p.a_group_cols % 16 == 0),
-              "gemm: grouped A needs M <= 64 and 16-column groups");
+  // decoder batches above 64 rows (faster-whisper's best_of hypotheses of many windows in
+  // one sampled decode) stay on the skinny kernel: its blocks split the rows as well
+  JANUS_CHECK(p.M <= kSkinnyMaxRows || epi != EPI_QKV,
+              "gemm: the KV-cache epilogue needs M <= kSkinnyMaxRows");
+  JANUS_CHECK(p.M <= 64 || !p.ln_part, "gemm: the LayerNorm-piece epilogue needs M <= 64");
+  JANUS_CHECK(p.a_group_cols == 0 || (p.M <= kSkinnyMaxRows && p.a_group_cols % 16 == 0),
+              "gemm: grouped A needs M <= kSkinnyMaxRows and 16-column groups");
   JANUS_CHECK(!p.ln_part || (epi == EPI_RESID_F32 && p.N % 16 == 0),
               "gemm: LayerNorm pieces come from a RESID epilogue with N % 16 == 0");
-  JANUS_CHECK(!p.lnin_x || (p.M <= 64 && p.K <= 1024 && p.K % 32 == 0 && p.a_group_cols == 0 &&
+  JANUS_CHECK(!p.lnin_x || (p.M <= kSkinnyMaxRows && p.K <= 1024 && p.K % 32 == 0 && p.a_group_cols == 0 &&
                             p.lnin_g && p.lnin_b && epi != EPI_RESID_F32 && epi != EPI_F32),
-              "gemm: LayerNorm-prologue A needs M <= 64, K <= 1024 (multiple of 32), no groups");
+              "gemm: LayerNorm-prologue A needs M <= kSkinnyMaxRows, K <= 1024 (multiple of 32), no groups");
   JANUS_CHECK(!p.ln_out || (epi == EPI_RESID_F32 && p.M <= 64 && p.N <= 512 && p.N % 4 == 0 && p.ln_cnt &&
                             p.ln_g && p.ln_b && p.ldc == p.N),
               "gemm: fused LayerNorm needs a RESID epilogue, M <= 64, N <= 512, ldc == N");
-  if (p.M <= 64) launch_skinny(epi, p, s);
+  JANUS_CHECK(p.M <= 64 || p.decode_rows || (epi != EPI_QKV && !p.lnin_x && p.a_group_cols == 0),
+              "gemm: KV-cache / LayerNorm-prologue / grouped products above 64 rows are decoder steps "
+              "(GemmArgs::decode_rows)");
+  if (p.M <= 64 || (p.decode_rows && p.M <= kSkinnyMaxRows)) launch_skinny(epi, p, s);
   else if (gemm_big_supported(epi, p)) gemm_big_launch(epi, p, s);
   else launch_cfg<128, 128, 4, 4>(epi, p, s);
 }

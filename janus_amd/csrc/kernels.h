@@ -6,6 +6,9 @@ namespace janus {
 
 // ------------------------------------------------------------------ GEMM
 enum GemmEpi { EPI_F16 = 0, EPI_GELU_F16 = 1, EPI_RESID_F32 = 2, EPI_F32 = 3, EPI_QKV = 4 };
+// Largest M the skinny (decoder-step) GEMM takes: a decode batch of 64 windows x 5 sampled
+// hypotheses (faster-whisper's best_of) is 320 rows.
+constexpr int kSkinnyMaxRows = 512;
 
 struct GemmArgs {
   const _Float16* A; int64_t lda;  // [M][K]
@@ -25,6 +28,9 @@ struct GemmArgs {
   // M <= 64 only: outputs up to this many columns also split their rows over blocks
   // (0 = JANUS_SKINNY_MSPLIT_N or 2048, tuned on a whole GPU; 1024 on a half-GPU CU mask)
   int msplit_n = 0;
+  // a decoder step (rows = decode batch): M <= kSkinnyMaxRows runs on the skinny kernel
+  // (rows split over blocks) instead of the 128 x 128 / 256 x 256 tile kernels
+  bool decode_rows = false;
   // EPI_RESID_F32 (M <= 64 only): the LayerNorm of the NEW residual rows, fused: the
   // output rows are stored write-through (sc1), every block adds to its row block's
   // counter ln_cnt[blockIdx.y] once its stores have drained, and the last block of each
@@ -111,9 +117,12 @@ bool xattn_supported(int D, int H);
 int xattn_split_count(int Te, int requested);
 void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int H,
                   _Float16* wqk, float* bqk, hipStream_t s);
+// pairs (nullable, device int4 [npairs] = {b0, b1, e, -}): decoder rows b0 and b1 (b1 < 0:
+// none) attend to encoder row e of enc, read once for both (H <= 8, D <= 512); without it
+// row b reads enc row b.
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
                   int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
-                  bool combine = true);
+                  bool combine = true, const int4* pairs = nullptr, int npairs = 0);
 // The split merge of xattn_launch(..., combine = false) fused with the per-head value
 // projection: out[b][64h + j] = merge_s(part)[b][h] . wv[64h + j]^T + bv[64h + j]
 // (wv [H*64][D] fp16, out row stride ldo); bit-identical to the merge kernel followed by the

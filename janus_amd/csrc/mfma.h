@@ -109,8 +109,23 @@ __device__ __forceinline__ uint4 ld_res(const _Float16* p) {  // epilogue re-rea
   return *reinterpret_cast<const uint4*>(p);
 #endif
 }
+// Write-through (sc1) vector stores: the line leaves the XCD's L2 with the store, so no
+// dirty vocoder line is left for a kernel-boundary L2 writeback to flush (the greedy
+// decoder beside the vocoder shares every XCD's L2 and ends ~68 kernels per position).
+// Plain / nt stores KEEP the line dirty in L2 (MI355X_MICROARCH.md, store flavours).
+// Inline asm: hipcc counts no asm store; s_endpgm waits for them, and nothing in the
+// kernel re-reads a stored activation.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_wt16(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_wt8(void* p, u32x2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
 __device__ __forceinline__ void st_act(_Float16* p, const half8& v) {
-#ifdef JANUS_ACT_NT_ST
+#if defined(JANUS_ACT_WT)
+  st_wt16(p, __builtin_bit_cast(u32x4, v));
+#elif defined(JANUS_ACT_NT_ST)
   __builtin_nontemporal_store(v, reinterpret_cast<half8*>(p));
 #else
   *reinterpret_cast<half8*>(p) = v;

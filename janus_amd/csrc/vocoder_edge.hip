@@ -172,8 +172,19 @@ __global__ __launch_bounds__(kPostThreads) void conv_post_kernel(const _Float16*
   if (t + kPostR <= T && (T & 3) == 0) {  // aligned full group: vector stores, non-temporal
     typedef float f4v __attribute__((ext_vector_type(4)));
     typedef short s4v __attribute__((ext_vector_type(4)));
+#ifdef JANUS_ACT_WT
+    {
+      const f4v yv{y[0], y[1], y[2], y[3]};
+      st_wt16(wo, __builtin_bit_cast(u32x4, yv));
+      if (po) {
+        const s4v qv{q16[0], q16[1], q16[2], q16[3]};
+        st_wt8(po, __builtin_bit_cast(u32x2, qv));
+      }
+    }
+#else
     __builtin_nontemporal_store(f4v{y[0], y[1], y[2], y[3]}, reinterpret_cast<f4v*>(wo));
     if (po) __builtin_nontemporal_store(s4v{q16[0], q16[1], q16[2], q16[3]}, reinterpret_cast<s4v*>(po));
+#endif
   } else {
 #pragma unroll
     for (int o = 0; o < kPostR; ++o) {

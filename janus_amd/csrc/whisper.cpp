@@ -64,7 +64,7 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc, d_seed;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
@@ -300,13 +300,48 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
+  // shared encoder rows (janus_decode_rows::enc_index): row b attends to enc_in row
+  // enc_index[b] of n_enc; the absorbed cross-attention then reads each shared row once per
+  // pair of decoder rows (xattn PAIR blocks), other paths get a per-row gathered copy
+  const bool shared = rows && rows->enc_index;
+  const int n_enc = shared ? rows->n_enc : B;
+  std::vector<int4> h_pairs;
+  if (shared) {
+    JANUS_CHECK(n_enc >= 1, "decode: enc_index needs n_enc >= 1");
+    for (int b = 0; b < B; ++b)
+      JANUS_CHECK(rows->enc_index[b] >= 0 && rows->enc_index[b] < n_enc, "decode: enc_index out of range");
+  }
+  const bool pair_ok = shared && xattn_supported(d, H) && H <= 8 && d <= 512 && B <= kSkinnyMaxRows &&
+                       std::getenv("JANUS_NO_XABSORB") == nullptr && std::getenv("JANUS_NO_XPAIR") == nullptr;
+  if (pair_ok) {
+    // rows grouped by encoder row, paired in row order within a group
+    std::vector<std::vector<int>> grp(n_enc);
+    for (int b = 0; b < B; ++b) grp[rows->enc_index[b]].push_back(b);
+    for (int e = 0; e < n_enc; ++e)
+      for (size_t i = 0; i < grp[e].size(); i += 2)
+        h_pairs.push_back(make_int4(grp[e][i], i + 1 < grp[e].size() ? grp[e][i + 1] : -1, e, 0));
+  }
   // the captured decode graphs bake in every pointer they read: the encoder output goes
   // to a context-owned buffer first (one ~0.1 ms device copy) so the graphs are reused
   // whatever buffer the caller's allocator handed out this time
-  Z.d_enc.ensure(sizeof(_Float16) * (int64_t)B * Te * d);
-  JANUS_HIP(hipMemcpyAsync(Z.d_enc.p, enc_in, sizeof(_Float16) * (int64_t)B * Te * d,
-                           hipMemcpyDeviceToDevice, s));
+  const int enc_rows = pair_ok ? n_enc : B;
+  const int64_t erow = (int64_t)Te * d;
+  Z.d_enc.ensure(sizeof(_Float16) * (int64_t)enc_rows * erow);
+  if (shared && !pair_ok) {
+    for (int b = 0; b < B; ++b)
+      JANUS_HIP(hipMemcpyAsync(Z.d_enc.as<_Float16>() + (int64_t)b * erow, enc_in + (int64_t)rows->enc_index[b] * erow,
+                               sizeof(_Float16) * erow, hipMemcpyDeviceToDevice, s));
+  } else {
+    JANUS_HIP(hipMemcpyAsync(Z.d_enc.p, enc_in, sizeof(_Float16) * (int64_t)enc_rows * erow,
+                             hipMemcpyDeviceToDevice, s));
+  }
   const _Float16* enc = Z.d_enc.as<_Float16>();
+  const int npairs = (int)h_pairs.size();
+  if (npairs > 0) {
+    Z.d_xpairs.ensure(sizeof(int4) * npairs);
+    JANUS_HIP(hipMemcpyAsync(Z.d_xpairs.p, h_pairs.data(), sizeof(int4) * npairs, hipMemcpyHostToDevice, s));
+  }
+  const int4* xpairs = npairs > 0 ? Z.d_xpairs.as<int4>() : nullptr;
   const int maxlen = opt->max_length;
   // per-row prompts (janus_decode_rows): row b samples from position plen[b]; all rows step
   // together from position 0, rows still inside their prompt keep the forced token
@@ -355,6 +390,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   auto dgargs = [&](auto&&... args) {
     GemmArgs g = gargs(args...);
     g.msplit_n = msplit_n;
+    g.decode_rows = true;
     return g;
   };
   const int nblk = logits_partial_blocks(V, d, lg_cap);
@@ -395,7 +431,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   rules_init_launch(Z.d_rules.as<RowRules>(), B, s);
 
   // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
-  const bool xabs = xattn_supported(d, H) && B <= 64 && std::getenv("JANUS_NO_XABSORB") == nullptr;
+  const bool xabs = xattn_supported(d, H) && B <= kSkinnyMaxRows && std::getenv("JANUS_NO_XABSORB") == nullptr;
   const int xsplit = xattn_split_count(
       Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : opt->xattn_splits);
   if (xabs) {
@@ -462,7 +498,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // 64-row blocks would each normalise all 64 rows. Beside the vocoder (overlapped
   // step, decoder side): mask 0 303.5-308.7, 13 305.1-306.8, 9 304.0-304.2, 5 306.6-306.9
   // ms — within the box's noise; 9 (LN1 + final) is the default.
-  const int ln_pro_mask = (B <= 64 && d <= 512 && !fused_ln && !ln_fuse)
+  const int ln_pro_mask = (B <= kSkinnyMaxRows && d <= 512 && !fused_ln && !ln_fuse)
                               ? (std::getenv("JANUS_LN_PROLOGUE") ? std::atoi(std::getenv("JANUS_LN_PROLOGUE")) : 9)
                               : 0;
   // the embedding kernel owns whole rows (one block per utterance): it also writes the
@@ -527,7 +563,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         const bool lnp1 = (ln_pro_mask & 1) && !(embed_ln && l == 0);
         if (!ln_fuse && !lnp1 && !(embed_ln && l == 0))
           layernorm_launch(x, L.ln1g, L.ln1b, a, B, d, 1e-5f, s);
-        if (B <= 64) {
+        if (B <= kSkinnyMaxRows) {
           GemmArgs g = with_ln(dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
                                L.ln1g, L.ln1b, lnp1);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
@@ -556,7 +592,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo; the
         // split merge and the value projection in one launch (cvp) where supported
         xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s,
-                     !cvp);
+                     !cvp, xpairs, npairs);
         if (cvp) {
           xattn_combine_vproj_launch(Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xsplit, B, H, d,
                                      L.wv_c.as<_Float16>(), L.bv_c, o, d, s);
@@ -621,7 +657,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
-      (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p};
+      (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
+      (int64_t)npairs};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -825,6 +862,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     int nlanes = 1;
     if (const char* v = std::getenv("JANUS_DEC_LANES")) nlanes = std::atoi(v);
     nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
+    if (rows && rows->enc_index) nlanes = 1;  // shared encoder rows: one lane holds them all
     while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
     if (nlanes == 1 && s != nullptr) {
       decode_greedy(w, *w->lanes[0], e, batch, opt, rows, tokens, n_tokens, sum_logprob,

@@ -96,10 +96,15 @@ struct XGeo {
 
 // CH keys per chunk: 32 (4 waves, three blocks per CU) or 64 (8 waves: half the serial
 // chunk steps per split at the same registers per wave).
-template <int D, int CH>
+// PAIR (shared encoder output, r04): the block's 16 MFMA rows hold the heads of TWO decoder
+// rows that attend to the same encoder output (faster-whisper's best_of hypotheses of one
+// window): rows 0-7 are row b0's heads, rows 8-15 row b1's (H <= 8; b1 < 0: none), and
+// the block reads encoder row e once for both — where the one-row form pads 8 heads to 16
+// MFMA rows and reads E once per decoder row. pairs[blockIdx.y] = {b0, b1, e, -}.
+template <int D, int CH, bool PAIR = false>
 __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
-    float* __restrict__ part_c, float* __restrict__ part_ml) {
+    float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs) {
   using G = XGeo<D, CH>;
   constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT, NW = G::NW,
                 NKT = G::NKT, HPW = G::HPW;
@@ -109,10 +114,22 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
   float* sS = reinterpret_cast<float*>(sP + 16 * PP);  // [2][16][CH] partial scores
   float* sA = sS + 2 * 16 * CH;                // [16] rescale factors
 
-  const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
+  const int s = blockIdx.x, nsplit = gridDim.x;
+  int b = blockIdx.y, b1 = -1, e = blockIdx.y;
+  if constexpr (PAIR) {
+    const int4 q = pairs[blockIdx.y];
+    b = __builtin_amdgcn_readfirstlane(q.x);
+    b1 = __builtin_amdgcn_readfirstlane(q.y);
+    e = __builtin_amdgcn_readfirstlane(q.z);
+  }
+  // MFMA row r <-> (decoder row, head): one-row form (b, r) for r < H; PAIR (b, r) for
+  // r < 8, (b1, r - 8) above
+  auto row_b = [&](int r) { return (PAIR && r >= 8) ? b1 : b; };
+  auto row_h = [&](int r) { return PAIR ? (r & 7) : r; };
+  auto row_ok = [&](int r) { return PAIR ? ((r & 7) < H && (r < 8 || b1 >= 0)) : r < H; };
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int t0 = s * kps, t1 = min(Te, t0 + kps);
-  const _Float16* eb = enc + (int64_t)b * Te * D;
+  const _Float16* eb = enc + (int64_t)e * Te * D;
 
   // S-phase role: key tile nt (16 keys), dims half kh; the wave's Qk fragments (rows =
   // heads, zero rows >= H) stay in registers for the whole split
@@ -121,8 +138,9 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
   half8 qa[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
-    qa[ks] = lr < H ? *reinterpret_cast<const half8*>(qk + ((int64_t)b * H + lr) * D + kh * KH + 32 * ks + 8 * lg)
-                    : zero_half8();
+    qa[ks] = row_ok(lr) ? *reinterpret_cast<const half8*>(qk + ((int64_t)row_b(lr) * H + row_h(lr)) * D +
+                                                           kh * KH + 32 * ks + 8 * lg)
+                        : zero_half8();
   for (int i = tid; i < 16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
 
   half8 ef[KS];
@@ -169,8 +187,12 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
     const int nk = min(CH, t1 - t);
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
-      const int h = w + NW * i;
-      if (h >= H) break;  // wave-uniform
+      const int h = w + NW * i;  // MFMA row
+      if constexpr (PAIR) {
+        if (!row_ok(h)) continue;  // wave-uniform
+      } else {
+        if (h >= H) break;  // wave-uniform
+      }
       const bool valid = lane < nk;
       const float sc = valid ? sS[h * CH + lane] + sS[(16 + h) * CH + lane] : -INFINITY;
       float mc = sc;
@@ -191,7 +213,7 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * lg + r;
-      const float al = row < H ? sA[row] : 0.f;
+      const float al = row_ok(row) ? sA[row] : 0.f;
 #pragma unroll
       for (int n = 0; n < NT; ++n) accc[n][r] *= al;
     }
@@ -218,26 +240,26 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
     __syncthreads();  // sE / sS / sP are rewritten by the next chunk
   }
 
-  // ---- per-split partials: C rows < H (fp32), (m, l) per head
-  float* pc = part_c + ((int64_t)b * nsplit + s) * H * D;
+  // ---- per-split partials: C of the valid rows (fp32), (m, l) per head
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = 4 * lg + r;
-    if (row >= H) continue;
+    if (!row_ok(row)) continue;
+    float* pc = part_c + (((int64_t)row_b(row) * nsplit + s) * H + row_h(row)) * D;
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #ifndef JANUS_XPART_PLAIN  // partials written / read past the caches (r03 v4; A/B switch)
-      __builtin_nontemporal_store(accc[n][r], &pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr]);
+      __builtin_nontemporal_store(accc[n][r], &pc[w * (D / NW) + 16 * n + lr]);
 #else
-      pc[(int64_t)row * D + w * (D / NW) + 16 * n + lr] = accc[n][r];
+      pc[w * (D / NW) + 16 * n + lr] = accc[n][r];
 #endif
   }
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
-      const int h = w + NW * i;
-      if (h < H) {
-        float* pm = part_ml + (((int64_t)b * nsplit + s) * H + h) * 2;
+      const int h = w + NW * i;  // MFMA row
+      if (row_ok(h)) {
+        float* pm = part_ml + (((int64_t)row_b(h) * nsplit + s) * H + row_h(h)) * 2;
         pm[0] = m_run[i];
         pm[1] = l_run[i];
       }
@@ -459,17 +481,18 @@ int xattn_split_count(int Te, int requested) {
 
 template <int D, int CH>
 static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
-                      float* part_c, float* part_ml, hipStream_t s) {
+                      float* part_c, float* part_ml, hipStream_t s, const int4* pairs, int npairs) {
   const int chunks = (Te + CH - 1) / CH;
   const int kps = (chunks + nsplit - 1) / nsplit * CH;
-  auto kern = xattn_kernel<D, CH>;
-  static bool attr = false;
-  if (!attr) {
+  auto kern = pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[pairs != nullptr]) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
-    attr = true;
+    attr[pairs != nullptr] = true;
   }
-  kern<<<dim3(nsplit, B), CH * 8, XGeo<D, CH>::LDS, s>>>(qk, enc, Te, H, kps, part_c, part_ml);
+  kern<<<dim3(nsplit, pairs ? npairs : B), CH * 8, XGeo<D, CH>::LDS, s>>>(qk, enc, Te, H, kps, part_c,
+                                                                         part_ml, pairs);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -479,20 +502,21 @@ bool xattn_supported(int D, int H) {
 
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
                   int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
-                  bool combine) {
+                  bool combine, const int4* pairs, int npairs) {
   JANUS_CHECK(xattn_supported(D, H), "xattn: need D = 64 H in {384, 512, 768}");
   if (B <= 0 || Te <= 0) return;
   JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
+  JANUS_CHECK(!pairs || (H <= 8 && npairs >= 1 && D <= 512), "xattn: row pairs need H <= 8, D <= 512");
   // 64-key chunks (8 waves) unless JANUS_XATTN_CH32
   static const bool ch32 = std::getenv("JANUS_XATTN_CH32") != nullptr;
   if (D == 384) {
-    if (ch32) xattn_cfg<384, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
-    else xattn_cfg<384, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+    if (ch32) xattn_cfg<384, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);
+    else xattn_cfg<384, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);
   } else if (D == 512) {
-    if (ch32) xattn_cfg<512, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
-    else xattn_cfg<512, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+    if (ch32) xattn_cfg<512, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);
+    else xattn_cfg<512, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);
   } else {
-    xattn_cfg<768, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s);
+    xattn_cfg<768, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, nullptr, 0);
   }
   if (!combine) return;  // the caller merges (xattn_combine_vproj_launch)
   if (nsplit <= kXCombMax && D <= 512)

@@ -66,8 +66,9 @@ NO_SPEECH_THRESHOLD = 0.6
 TEMPERATURES = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0)   # faster-whisper transcribe(temperature=...)
 BEST_OF = 5
 PROMPT_RESET_ON_TEMPERATURE = 0.5
-FALLBACK_ROWS = 60       # hypotheses per sampling decode (12 windows x 5; B <= 64 keeps
-                         # the absorbed cross-attention path)
+FALLBACK_ROWS = 320      # hypotheses per sampling decode (64 windows x 5: one decode per
+                         # temperature for a 64-window round; the windows' encoder outputs are
+                         # shared by their hypotheses through enc_index)
 
 
 def _mix32(h: int) -> int:
@@ -259,12 +260,13 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
             break
         for c0 in range(0, len(pend), per):
             js = pend[c0:c0 + per]
-            idx = torch.tensor(js, device=enc.device).repeat_interleave(best_of)
-            rows_enc = enc.index_select(0, idx).contiguous()
+            # the hypotheses of window j share its encoder output: no per-row copy, and the
+            # cross-attention reads it once per pair of hypotheses (enc_index)
             rows_prompts = [prompts[j] for j in js for _ in range(best_of)]
             seeds = [fallback_seed(keys[j][0], keys[j][1], ti, h) for j in js for h in range(best_of)]
-            out = engine.decode_ex(rows_enc, prompts=rows_prompts, max_length=max_length,
-                                   temperature=T, seeds=seeds, **dec_kw).rows()
+            out = engine.decode_ex(enc, prompts=rows_prompts, max_length=max_length,
+                                   temperature=T, seeds=seeds,
+                                   enc_index=[j for j in js for _ in range(best_of)], **dec_kw).rows()
             for k, j in enumerate(js):
                 toks, avg_lp, nsp = best_hypothesis(out[k * best_of:(k + 1) * best_of])
                 results[j].append(candidate(tk, toks, avg_lp, nsp, T))

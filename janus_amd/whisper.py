@@ -62,7 +62,8 @@ class janus_decode_options(ctypes.Structure):
 class janus_decode_rows(ctypes.Structure):
     _fields_ = [("prompts", ctypes.POINTER(ctypes.c_int32)),
                 ("prompt_lens", ctypes.POINTER(ctypes.c_int32)),
-                ("stride", ctypes.c_int), ("no_speech_token", ctypes.c_int)]
+                ("stride", ctypes.c_int), ("no_speech_token", ctypes.c_int),
+                ("enc_index", ctypes.POINTER(ctypes.c_int32)), ("n_enc", ctypes.c_int)]
 
 
 # ----------------------------------------------------------------- front end
@@ -310,12 +311,14 @@ class WhisperEngine:
 
     def decode_ex(self, enc: torch.Tensor, prompts=None, max_length: int = 448,
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
-                  cu_count: int = 0, temperature: float = 0.0, seeds=None):
+                  cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
-        rule-filtered logits / T with per-row uint32 ``seeds``)."""
-        B = enc.shape[0]
+        rule-filtered logits / T with per-row uint32 ``seeds``). ``enc_index`` (one int per
+        decoder row): row b attends to enc[enc_index[b]] — the best_of hypotheses of a
+        window share its encoder output, read once per pair of rows."""
+        B = enc.shape[0] if enc_index is None else len(enc_index)
         if temperature > 0:
             if seeds is None or len(seeds) != B:
                 raise ValueError("sampling needs one uint32 seed per row")
@@ -323,6 +326,13 @@ class WhisperEngine:
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
+        ei = None
+        if enc_index is not None:
+            ei = np.ascontiguousarray(np.asarray(enc_index, np.int32))
+            if ei.size and (ei.min() < 0 or ei.max() >= enc.shape[0]):
+                raise ValueError("enc_index out of range")
+            rows.enc_index = ei.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            rows.n_enc = int(enc.shape[0])
         plens = np.full(B, len(self.tokenizer.sot_sequence), np.int32)
         pr = None
         if prompts is not None:
@@ -348,7 +358,7 @@ class WhisperEngine:
             nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
                      ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
                      nsp.data_ptr(), nat.stream_ptr())
-        del keep, pr
+        del keep, pr, ei
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 
     def decode_info(self):

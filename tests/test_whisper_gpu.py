@@ -188,6 +188,37 @@ def test_weight_reupload_after_decode(gpu):
     assert not (torch.equal(n1, n2) and all(torch.equal(t1[b, :n1[b]], t2[b, :n2[b]]) for b in range(3)))
 
 
+@pytest.mark.parametrize("T", [0.0, 0.6])
+def test_shared_encoder_rows_match_replicated(engine, gpu, T):
+    """Decoder rows sharing an encoder output (enc_index: faster-whisper's best_of
+    hypotheses of one window; the cross-attention reads each shared window once per PAIR of
+    rows) decode exactly as with a private copy per row, including a batch above 64 rows
+    (the skinny GEMMs split the rows over blocks): tokens, summed log-probabilities and
+    no-speech probabilities bit-identical."""
+    eng, _ = engine
+    utts = [synth_speech(70 + k, 2.0 + k) for k in range(3)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    idx = [0, 0, 0, 0, 0, 1, 1, 2, 2, 2, 2, 2, 1, 0]          # odd / even groups, interleaved
+    for reps in (1, 6):                                        # 14 rows, then 84 (> 64)
+        ei = idx * reps
+        seeds = [1000 + i for i in range(len(ei))] if T > 0 else None
+        rep = enc.index_select(0, torch.tensor(ei, device=gpu)).contiguous()
+        a = eng.decode_ex(rep, max_length=40, temperature=T, seeds=seeds)
+        b = eng.decode_ex(enc, max_length=40, temperature=T, seeds=seeds, enc_index=ei)
+        torch.cuda.synchronize()
+        assert torch.equal(a.tokens.cpu(), b.tokens.cpu())
+        assert torch.equal(a.n_tokens.cpu(), b.n_tokens.cpu())
+        assert torch.equal(a.sum_logprob.cpu(), b.sum_logprob.cpu())
+        assert torch.equal(a.no_speech_prob.cpu(), b.no_speech_prob.cpu())
+        # rows are independent of the batch they ride in: the 84-row decode repeats the
+        # 14-row one
+        if reps == 1:
+            first = b.tokens.cpu()
+        else:
+            assert torch.equal(b.tokens.cpu()[:len(idx)], first)
+
+
 def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
     """Opt-in decoder lanes (JANUS_DEC_LANES: the batch split over concurrent streams and
     host threads) decode every utterance exactly as the single-lane decoder does: rows
