@@ -123,6 +123,12 @@ void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int 
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
                   int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
                   bool combine = true, const int4* pairs = nullptr, int npairs = 0);
+// Groups of <= 6 decoder rows sharing an encoder row, one block per (split, group):
+// groups [device] int [ngroups][8] = {e, row_0 .. row_5 (-1: none), -}; partials as
+// xattn_launch(combine = false) writes them (merged by xattn_combine_vproj_launch).
+void xattn_group_launch(const _Float16* qk, const _Float16* enc, int Te, int D, int H, int nsplit,
+                        float* part_c, float* part_ml, hipStream_t s, const int* groups, int ngroups,
+                        int rows_per_group);
 // The split merge of xattn_launch(..., combine = false) fused with the per-head value
 // projection: out[b][64h + j] = merge_s(part)[b][h] . wv[64h + j]^T + bv[64h + j]
 // (wv [H*64][D] fp16, out row stride ldo); bit-identical to the merge kernel followed by the

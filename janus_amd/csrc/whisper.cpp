@@ -64,7 +64,7 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
@@ -313,13 +313,30 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   }
   const bool pair_ok = shared && xattn_supported(d, H) && H <= 8 && d <= 512 && B <= kSkinnyMaxRows &&
                        std::getenv("JANUS_NO_XABSORB") == nullptr && std::getenv("JANUS_NO_XPAIR") == nullptr;
+  // more than two rows per encoder row (best_of = 5): GROUP blocks of up to 6 rows
+  // (xattn_group_kernel: the window's output read once for all its hypotheses); at most
+  // two: PAIR blocks (xattn_kernel<PAIR>, two blocks per CU)
+  std::vector<int> h_groups;
+  int grp_rows = 0;
   if (pair_ok) {
-    // rows grouped by encoder row, paired in row order within a group
     std::vector<std::vector<int>> grp(n_enc);
     for (int b = 0; b < B; ++b) grp[rows->enc_index[b]].push_back(b);
-    for (int e = 0; e < n_enc; ++e)
-      for (size_t i = 0; i < grp[e].size(); i += 2)
-        h_pairs.push_back(make_int4(grp[e][i], i + 1 < grp[e].size() ? grp[e][i + 1] : -1, e, 0));
+    size_t maxg = 0;
+    for (auto& g : grp) maxg = std::max(maxg, g.size());
+    if (maxg > 2 && std::getenv("JANUS_NO_XGROUP") == nullptr) {
+      grp_rows = (int)std::min<size_t>(6, maxg);
+      for (int e = 0; e < n_enc; ++e)
+        for (size_t i = 0; i < grp[e].size(); i += grp_rows) {
+          h_groups.push_back(e);
+          for (int j = 0; j < 7; ++j)
+            h_groups.push_back(j < grp_rows && i + j < grp[e].size() ? grp[e][i + j] : -1);
+        }
+    } else {
+      // rows grouped by encoder row, paired in row order within a group
+      for (int e = 0; e < n_enc; ++e)
+        for (size_t i = 0; i < grp[e].size(); i += 2)
+          h_pairs.push_back(make_int4(grp[e][i], i + 1 < grp[e].size() ? grp[e][i + 1] : -1, e, 0));
+    }
   }
   // the captured decode graphs bake in every pointer they read: the encoder output goes
   // to a context-owned buffer first (one ~0.1 ms device copy) so the graphs are reused
@@ -342,6 +359,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     JANUS_HIP(hipMemcpyAsync(Z.d_xpairs.p, h_pairs.data(), sizeof(int4) * npairs, hipMemcpyHostToDevice, s));
   }
   const int4* xpairs = npairs > 0 ? Z.d_xpairs.as<int4>() : nullptr;
+  const int ngroups = (int)h_groups.size() / 8;
+  if (ngroups > 0) {
+    Z.d_xgroups.ensure(sizeof(int) * h_groups.size());
+    JANUS_HIP(hipMemcpyAsync(Z.d_xgroups.p, h_groups.data(), sizeof(int) * h_groups.size(),
+                             hipMemcpyHostToDevice, s));
+  }
+  const int* xgroups = ngroups > 0 ? Z.d_xgroups.as<int>() : nullptr;
   const int maxlen = opt->max_length;
   // per-row prompts (janus_decode_rows): row b samples from position plen[b]; all rows step
   // together from position 0, rows still inside their prompt keep the forced token
@@ -591,8 +615,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         }
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo; the
         // split merge and the value projection in one launch (cvp) where supported
-        xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s,
-                     !cvp, xpairs, npairs);
+        JANUS_CHECK(!xgroups || cvp, "decode: shared-encoder groups need the fused merge (JANUS_NO_CVP unset)");
+        if (xgroups)
+          xattn_group_launch(xqk, enc, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), s,
+                             xgroups, ngroups, grp_rows);
+        else
+          xattn_launch(xqk, enc, B, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xc, s,
+                       !cvp, xpairs, npairs);
         if (cvp) {
           xattn_combine_vproj_launch(Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), xsplit, B, H, d,
                                      L.wv_c.as<_Float16>(), L.bv_c, o, d, s);
@@ -658,7 +687,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
       (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
-      (int64_t)npairs};
+      (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);

@@ -268,6 +268,245 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
 }
 
 
+// GROUP (r04): up to 2*NMT decoder rows attending to the same encoder row — the best_of = 5
+// sampled hypotheses of one window (faster-whisper's generate_with_fallback) — in ONE
+// block: NMT m-tiles of 16 MFMA rows (8 per decoder row, H <= 8), so the block reads the
+// window's encoder output ONCE for all of them and each E fragment (S phase) and each
+// transposed E read (C phase) feeds NMT MFMAs. Per row the same MFMA k-sequence, softmax
+// and merge arithmetic as xattn_kernel, so every row's partials are bit-identical to its
+// one-row (or PAIR) computation. groups[g][8] = {e, row_0 .. row_{2 NMT - 1} (-1: none), -}.
+// One block per CU (NMT = 3: ~220 VGPRs).
+template <int D, int CH, int NMT>
+__global__ __launch_bounds__(CH * 8, 1) void xattn_group_kernel(
+    const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
+    float* __restrict__ part_c, float* __restrict__ part_ml, const int* __restrict__ groups) {
+  using G = XGeo<D, CH>;
+  constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT, NW = G::NW,
+                NKT = G::NKT;
+  constexpr int R16 = 16 * NMT;        // MFMA rows
+  constexpr int HPW = R16 / NW;        // softmax rows per wave
+  constexpr int NR = 2 * NMT;          // decoder rows per group
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* sE = smem;                          // [CH][QP] keys x dims
+  _Float16* sP = sE + CH * QP;                  // [R16][PP] rows x (permuted) keys
+  float* sS = reinterpret_cast<float*>(sP + R16 * PP);  // [2][R16][CH] partial scores
+  float* sA = sS + 2 * R16 * CH;                // [R16] rescale factors
+  // NMT = 3: the query fragments of m-tiles 1.. live in LDS (registers: m-tile 0 only), as
+  // 256 VGPRs would not hold all three: sQ [NMT-1][16][D]
+  constexpr int QR = NMT >= 3 ? 1 : NMT;        // m-tiles with register query fragments
+  _Float16* sQ = reinterpret_cast<_Float16*>(sA + R16);
+
+  const int s = blockIdx.x, nsplit = gridDim.x;
+  const int* gp = groups + (int64_t)blockIdx.y * 8;
+  const int e = __builtin_amdgcn_readfirstlane(gp[0]);
+  int rb[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) rb[j] = __builtin_amdgcn_readfirstlane(gp[1 + j]);
+  // MFMA row r (0 .. R16-1) <-> decoder row rb[r >> 3], head r & 7
+  auto row_b = [&](int r) {
+    int v = rb[0];
+#pragma unroll
+    for (int j = 1; j < NR; ++j) v = (r >> 3) == j ? rb[j] : v;
+    return v;
+  };
+  auto row_ok = [&](int r) { return (r & 7) < H && row_b(r) >= 0; };
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int t0 = s * kps, t1 = min(Te, t0 + kps);
+  const _Float16* eb = enc + (int64_t)e * Te * D;
+
+  const int nt = w % NKT, kh = w / NKT;
+  const int lr = lane & 15, lg = lane >> 4;
+  half8 qa[QR][KS];
+#pragma unroll
+  for (int t = 0; t < QR; ++t) {
+    const int r = 16 * t + lr;
+    const bool ok = row_ok(r);
+    const int qb = ok ? row_b(r) : 0;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qa[t][ks] = ok ? *reinterpret_cast<const half8*>(qk + ((int64_t)qb * H + (r & 7)) * D + kh * KH +
+                                                        32 * ks + 8 * lg)
+                     : zero_half8();
+  }
+  if constexpr (QR < NMT) {  // rows of m-tiles QR.. -> sQ, 8 halves per thread-step
+    for (int i = tid; i < (NMT - QR) * 16 * (D / 8); i += NW * 64) {
+      const int rr = i / (D / 8), c8 = (i % (D / 8)) * 8;
+      const int r = 16 * QR + rr;
+      const bool ok = row_ok(r);
+      const int qb = ok ? row_b(r) : 0;
+      *reinterpret_cast<half8*>(sQ + rr * D + c8) =
+          ok ? *reinterpret_cast<const half8*>(qk + ((int64_t)qb * H + (r & 7)) * D + c8) : zero_half8();
+    }
+  }
+  for (int i = tid; i < R16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // invalid rows stay zero
+
+  half8 ef[KS];
+  auto load_e = [&](int t) {
+    const int key = t + 16 * nt + lr;
+    const bool ok = key < t1;
+    const _Float16* src = eb + (int64_t)key * D + kh * KH + 8 * lg;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) ef[ks] = ok ? *reinterpret_cast<const half8*>(src + 32 * ks) : zero_half8();
+  };
+
+  f32x4 accc[NMT][NT];
+#pragma unroll
+  for (int t = 0; t < NMT; ++t)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) accc[t][n] = zero_f32x4();
+  float m_run[HPW], l_run[HPW];
+#pragma unroll
+  for (int i = 0; i < HPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
+
+  if (t0 < t1) load_e(t0);
+  __syncthreads();
+  for (int t = t0; t < t1; t += CH) {
+    // ---- S partials of every m-tile from the same E fragments
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) {
+      f32x4 accs = zero_f32x4();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        half8 qf;
+        if (mt < QR) qf = qa[mt < QR ? mt : 0][ks];
+        else qf = *reinterpret_cast<const half8*>(sQ + ((mt - QR) * 16 + lr) * D + kh * KH + 32 * ks + 8 * lg);
+        accs = mfma16(qf, ef[ks], accs);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sS[(kh * R16 + 16 * mt + 4 * lg + r) * CH + 16 * nt + lr] = accs[r];
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = ef[ks];
+    if (t + CH < t1) load_e(t + CH);
+    __syncthreads();
+
+    // ---- online softmax: wave w owns MFMA rows w, w + NW, ...; lane = key
+    const int nk = min(CH, t1 - t);
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int h = w + NW * i;  // MFMA row
+      if (!row_ok(h)) continue;  // wave-uniform
+      const bool valid = lane < nk;
+      const float sc = valid ? sS[h * CH + lane] + sS[(R16 + h) * CH + lane] : -INFINITY;
+      float mc = sc;
+      for (int o = 32; o > 0; o >>= 1) mc = fmaxf(mc, __shfl_xor(mc, o));
+      const float m_new = fmaxf(m_run[i], mc);
+      const float alpha = exp2f(m_run[i] - m_new);
+      const float p = valid ? exp2f(sc - m_new) : 0.f;
+      float ps = p;
+      for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
+      l_run[i] = l_run[i] * alpha + ps;
+      m_run[i] = m_new;
+      if (lane < CH) sP[h * PP + (lane & ~31) + xkappa_inv(lane & 31)] = (_Float16)p;
+      if (lane == 0) sA[h] = alpha;
+    }
+    __syncthreads();
+
+    // ---- C += P . E: each transposed E read feeds the NMT m-tiles
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * mt + 4 * lg + r;
+        const float al = row_ok(row) ? sA[row] : 0.f;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) accc[mt][n][r] *= al;
+      }
+    const int q = lr >> 2, pcol = 4 * (lr & 3);
+    const int row0 = 16 * (lg >> 1) + 4 * (lg & 1) + q;
+#pragma unroll
+    for (int kk = 0; kk < CH / 32; ++kk) {
+      half8 pa[NMT];
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt)
+        pa[mt] = *reinterpret_cast<const half8*>(sP + (16 * mt + lr) * PP + 32 * kk + 8 * lg);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int c0 = w * (D / NW) + 16 * n + pcol;
+        const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)(sE + (32 * kk + row0) * QP + c0));
+        const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)(sE + (32 * kk + row0 + 8) * QP + c0));
+        half8 bv;
+        const _Float16* l4 = reinterpret_cast<const _Float16*>(&lo);
+        const _Float16* h4 = reinterpret_cast<const _Float16*>(&hi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { bv[j] = l4[j]; bv[4 + j] = h4[j]; }
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) accc[mt][n] = mfma16(pa[mt], bv, accc[mt][n]);
+      }
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * mt + 4 * lg + r;
+      if (!row_ok(row)) continue;
+      float* pc = part_c + (((int64_t)row_b(row) * nsplit + s) * H + (row & 7)) * D;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#ifndef JANUS_XPART_PLAIN
+        __builtin_nontemporal_store(accc[mt][n][r], &pc[w * (D / NW) + 16 * n + lr]);
+#else
+        pc[w * (D / NW) + 16 * n + lr] = accc[mt][n][r];
+#endif
+    }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int h = w + NW * i;
+      if (row_ok(h)) {
+        float* pm = part_ml + (((int64_t)row_b(h) * nsplit + s) * H + (h & 7)) * 2;
+        pm[0] = m_run[i];
+        pm[1] = l_run[i];
+      }
+    }
+  }
+}
+
+template <int D, int CH, int NMT>
+static void xattn_group_cfg(const _Float16* qk, const _Float16* enc, int Te, int H, int nsplit,
+                            float* part_c, float* part_ml, hipStream_t s, const int* groups, int ngroups) {
+  const int chunks = (Te + CH - 1) / CH;
+  const int kps = (chunks + nsplit - 1) / nsplit * CH;
+  using G = XGeo<D, CH>;
+  constexpr int R16 = 16 * NMT;
+  constexpr int QR = NMT >= 3 ? 1 : NMT;
+  constexpr size_t lds = (size_t)(CH * G::QP + R16 * G::PP) * 2 + (size_t)2 * R16 * CH * 4 + R16 * 4 +
+                         (size_t)(NMT - QR) * 16 * D * 2;
+  auto kern = xattn_group_kernel<D, CH, NMT>;
+  static bool attr = false;
+  if (!attr) {
+    JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  kern<<<dim3(nsplit, ngroups), CH * 8, lds, s>>>(qk, enc, Te, H, kps, part_c, part_ml, groups);
+  JANUS_LAUNCH_CHECK();
+}
+
+void xattn_group_launch(const _Float16* qk, const _Float16* enc, int Te, int D, int H, int nsplit,
+                        float* part_c, float* part_ml, hipStream_t s, const int* groups, int ngroups,
+                        int rows_per_group) {
+  JANUS_CHECK(H <= 8 && (D == 384 || D == 512) && H * 64 == D, "xattn groups: H <= 8, D in {384, 512}");
+  JANUS_CHECK(rows_per_group >= 1 && rows_per_group <= 6, "xattn groups: 1..6 rows per group");
+  JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
+  if (ngroups <= 0 || Te <= 0) return;
+  const int nmt = (rows_per_group + 1) / 2;
+  if (D == 512) {
+    if (nmt == 1) xattn_group_cfg<512, 64, 1>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+    else if (nmt == 2) xattn_group_cfg<512, 64, 2>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+    else xattn_group_cfg<512, 64, 3>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+  } else {
+    if (nmt == 1) xattn_group_cfg<384, 64, 1>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+    else if (nmt == 2) xattn_group_cfg<384, 64, 2>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+    else xattn_group_cfg<384, 64, 3>(qk, enc, Te, H, nsplit, part_c, part_ml, s, groups, ngroups);
+  }
+}
+
 // c[b][h*D + j] = sum_s 2^(m_s - M) C_s[h][j] / sum_s 2^(m_s - M) l_s   (fp16)
 __global__ __launch_bounds__(256) void xattn_combine_kernel(const float* __restrict__ part_c,
                                                             const float* __restrict__ part_ml,

@@ -189,18 +189,20 @@ def test_weight_reupload_after_decode(gpu):
 
 
 @pytest.mark.parametrize("T", [0.0, 0.6])
-def test_shared_encoder_rows_match_replicated(engine, gpu, T):
+@pytest.mark.parametrize("idx", [[0, 0, 0, 0, 0, 1, 1, 2, 2, 2, 2, 2, 1, 0], [0, 0, 1, 2, 2, 1, 0]],
+                         ids=["groups", "pairs"])
+def test_shared_encoder_rows_match_replicated(engine, gpu, T, idx):
     """Decoder rows sharing an encoder output (enc_index: faster-whisper's best_of
-    hypotheses of one window; the cross-attention reads each shared window once per PAIR of
-    rows) decode exactly as with a private copy per row, including a batch above 64 rows
-    (the skinny GEMMs split the rows over blocks): tokens, summed log-probabilities and
+    hypotheses of one window) decode exactly as with a private copy per row: with more than
+    two rows per window the cross-attention reads it once per GROUP of up to 6 rows
+    (xattn_group_kernel), with at most two once per PAIR; including a batch above 64 rows
+    (the skinny GEMMs split the rows over blocks). Tokens, summed log-probabilities and
     no-speech probabilities bit-identical."""
     eng, _ = engine
     utts = [synth_speech(70 + k, 2.0 + k) for k in range(3)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    idx = [0, 0, 0, 0, 0, 1, 1, 2, 2, 2, 2, 2, 1, 0]          # odd / even groups, interleaved
-    for reps in (1, 6):                                        # 14 rows, then 84 (> 64)
+    for reps in (1, 10):                                       # then > 64 rows
         ei = idx * reps
         seeds = [1000 + i for i in range(len(ei))] if T > 0 else None
         rep = enc.index_select(0, torch.tensor(ei, device=gpu)).contiguous()
