@@ -54,6 +54,10 @@ def parse():
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--stagger", type=int, default=int(os.environ.get("JANUS_STAGGER", "0")),
+                    help="1: continuous batching in the decoder (JanusPipeline.step_staggered): "
+                         "each step's decoder call advances batch i from position 0 and batch "
+                         "i-1 from the middle, 128 rows; still one batch in and one out per step")
     ap.add_argument("--no-idle-latency", action="store_true",
                     help="skip the flush and the three idle-pipeline latency steps after the timed "
                          "region (profiling runs: only priming, warm-up and timed overlapped steps "
@@ -173,12 +177,14 @@ def decoder_bytes(cfg, B, positions):
             "vocab_projection": V * d * 2}
 
 
-def decoder_roofline(cfg, B, positions, launches, side_ms, cu_share):
+def decoder_roofline(cfg, B, positions, launches, side_ms, cu_share, tkv_positions=None):
     """roofline.decoder: the side that sets the overlapped step. side_ms = decoder-side
-    wall time per step (HIP events on the decoder's CU-masked stream, timed region)."""
+    wall time per step (HIP events on the decoder's CU-masked stream, timed region) over
+    `positions` decoder steps of B rows; tkv_positions: the decode length whose average key
+    count the rows see (staggered: the two row sets together see a full decode's)."""
     if not side_ms or positions <= 0:
         return None
-    by = decoder_bytes(cfg, B, positions)
+    by = decoder_bytes(cfg, B, tkv_positions or positions)
     per_pos = sum(by.values())
     us = side_ms * 1000.0 / positions
     gbs = per_pos / (us * 1e-6) / 1e9
@@ -189,7 +195,7 @@ def decoder_roofline(cfg, B, positions, launches, side_ms, cu_share):
             "frac_of_cu_share": round(gbs / (HBM_PEAK_GBS * cu_share), 4),
             "bytes_per_position": int(per_pos),
             "bytes_breakdown": {k: int(v) for k, v in by.items()},
-            "positions": positions, "side_ms": round(side_ms, 2),
+            "rows": B, "positions": positions, "side_ms": round(side_ms, 2),
             "us_per_position": round(us, 2),
             "launches_per_position": round(launches / positions, 2) if launches else None,
             "us_per_launch": round(us * positions / launches, 2) if launches else None}
@@ -543,7 +549,11 @@ def main():
     last = {}
 
     def step():
-        if args.overlap > 0:
+        if args.overlap > 0 and args.stagger and len(pipe.temperatures) == 1:
+            # continuous batching: batch i's first half and batch i-1's second half of the
+            # decode in one decoder call, the vocoder of batch i-2 beside it
+            enc, wav, pcm16 = pipe.step_staggered(pcm, offs, lengths, frames, args.overlap)
+        elif args.overlap > 0:
             # steady-state serving pipeline: batch i through mel / encoder / decoder / YIN,
             # batch i-1 through packets and the vocoder (the warm-up step primes it, so
             # every timed step carries a full encode and a full decode)
@@ -555,7 +565,8 @@ def main():
 
     # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
-    for _ in range(args.warmup + (1 if args.overlap > 0 else 0)):
+    prime = (2 if args.stagger else 1) if args.overlap > 0 else 0
+    for _ in range(args.warmup + prime):
         enc = step()
     torch.cuda.synchronize()
     if use_dist:
@@ -590,7 +601,7 @@ def main():
     # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
     idle = []
     if args.overlap > 0 and not args.no_idle_latency:
-        pipe.flush(frames)
+        pipe.flush_staggered(frames) if args.stagger else pipe.flush(frames)
     for _ in range(0 if args.no_idle_latency else 3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -677,9 +688,14 @@ def main():
                        "parallelism": f"dp{world}", "max_length": args.max_length},
             "xrt_per_gpu": round(value / world, 2),
             # overlapped: an utterance is encoded in one step and vocoded in the next
+            # an utterance's steps: encode + decode, then vocoder (overlapped: 2 steps);
+            # staggered: encode + first half, second half, vocoder (3 steps)
             "p50_latency_ms": round(float(np.median(
-                [a + b for a, b in zip(times[:-1], times[1:])] if args.overlap > 0 and len(times) > 1
+                [sum(times[i:i + (3 if args.stagger else 2)])
+                 for i in range(len(times) - (2 if args.stagger else 1))]
+                if args.overlap > 0 and len(times) > (2 if args.stagger else 1)
                 else times)) * 1000.0, 2),
+            "stagger": int(args.stagger),
             # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
             "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
             # wall time of the two CU partitions per timed step (HIP events on each side's
@@ -729,9 +745,10 @@ def main():
                 # HBM roofline (algorithmic bytes per position / decoder-side time per
                 # position; launches per position from the captured decode graphs)
                 "decoder": decoder_roofline(
-                    pipe.whisper.cfg, B, dec_positions, dec_launches,
+                    pipe.whisper.cfg, (2 if args.stagger else 1) * B, dec_positions, dec_launches,
                     float(np.mean([b for _, b in sides])) if sides else None,
-                    round(1.0 - cu_share, 4) if args.overlap > 0 else 1.0),
+                    round(1.0 - cu_share, 4) if args.overlap > 0 else 1.0,
+                    tkv_positions=(2 * dec_positions - 1) if args.stagger else None),
             },
             "cpu_baseline": None,
         }

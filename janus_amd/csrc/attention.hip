@@ -630,11 +630,14 @@ constexpr int kHeadKeys = 8 * kHeadWaves * kHeadRounds;      // 512
 template <int NR>
 __global__ __launch_bounds__(512) void decode_head_kernel(
     const _Float16* __restrict__ q, int64_t q_bs, const _Float16* __restrict__ k,
-    const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv, float scale_log2,
-    _Float16* __restrict__ out, int64_t o_bs) {
+    const _Float16* __restrict__ v, int64_t kv_bs, int64_t kv_rs, int Tkv0, float scale_log2,
+    _Float16* __restrict__ out, int64_t o_bs, const int32_t* __restrict__ roff) {
   __shared__ float wo[kHeadWaves][kHd];
   __shared__ float wm[kHeadWaves], wl[kHeadWaves];
   const int h = blockIdx.x, b = blockIdx.y;
+  // staggered rows (roff): row b attends over its own Tkv0 + roff[b] keys; NR covers the
+  // longest row, a shorter row's extra rounds load its clamped last key at weight 0
+  const int Tkv = Tkv0 + (roff ? roff[b] : 0);
   const int lane = threadIdx.x & 63, w = wave_id();
   const int kg = lane >> 3, dg = lane & 7;
   float qv[8];
@@ -738,24 +741,27 @@ int decode_split_count(int Tkv) {
 void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
                                    const _Float16* v, int64_t kv_bs, int64_t kv_rs, int Tkv,
                                    _Float16* out, int64_t o_bs, int B, int H, float scale,
-                                   float* part_o, float* part_ml, hipStream_t s) {
+                                   float* part_o, float* part_ml, hipStream_t s,
+                                   const int32_t* roff, int max_roff) {
   JANUS_CHECK(H <= kMaxHeads, "split decode attention: at most 8 heads (d <= 512)");
   if (B <= 0 || Tkv <= 0) return;
   static const bool force_split = std::getenv("JANUS_DEC_SPLIT") != nullptr;
-  if (Tkv <= kHeadKeys && (!force_split || part_o == nullptr)) {
+  const int tmax = Tkv + (roff ? max_roff : 0);
+  JANUS_CHECK(!roff || tmax <= kHeadKeys, "decode attention: staggered rows need <= 512 keys");
+  if (tmax <= kHeadKeys && (!force_split || part_o == nullptr || roff)) {
     static const bool all_rounds = std::getenv("JANUS_HEAD_ALL_ROUNDS") != nullptr;
-    const int nr = all_rounds ? kHeadRounds : (Tkv + 8 * kHeadWaves - 1) / (8 * kHeadWaves);
+    const int nr = all_rounds ? kHeadRounds : (tmax + 8 * kHeadWaves - 1) / (8 * kHeadWaves);
     const float sl = scale * 1.4426950408889634f;
     const dim3 grid(H, B), blk(64 * kHeadWaves);
     switch (nr) {
-      case 1: decode_head_kernel<1><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 2: decode_head_kernel<2><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 3: decode_head_kernel<3><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 4: decode_head_kernel<4><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 5: decode_head_kernel<5><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 6: decode_head_kernel<6><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      case 7: decode_head_kernel<7><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
-      default: decode_head_kernel<kHeadRounds><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs); break;
+      case 1: decode_head_kernel<1><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 2: decode_head_kernel<2><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 3: decode_head_kernel<3><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 4: decode_head_kernel<4><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 5: decode_head_kernel<5><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 6: decode_head_kernel<6><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      case 7: decode_head_kernel<7><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
+      default: decode_head_kernel<kHeadRounds><<<grid, blk, 0, s>>>(q, q_bs, k, v, kv_bs, kv_rs, Tkv, sl, out, o_bs, roff); break;
     }
     JANUS_LAUNCH_CHECK();
     return;

@@ -62,10 +62,12 @@ void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t 
 // (SkinnyLnArgs), d % 16 == 0
 // x[b] = tok_emb[token] + pos_emb[pos]; optionally the first layer's LayerNorm of the
 // row into ln_out [B][d] fp16 (d <= 512, eps 1e-5).
+// roff (nullable, device int32 [B]): per-row position offsets — row b is at pos + roff[b]
+// (staggered decode: janus_decode_rows.pos_offset)
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
                   int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s,
                   const float* ln_g = nullptr, const float* ln_b = nullptr,
-                  _Float16* ln_out = nullptr);
+                  _Float16* ln_out = nullptr, const int32_t* roff = nullptr);
 void kv_store_launch(const _Float16* qkv, int d, int pos, int n_ctx, _Float16* kc, _Float16* vc,
                      int B, hipStream_t s);
 void init_tokens_launch(int32_t* tokens, int ld, const int32_t* prompt, int plen, int32_t* done,
@@ -97,13 +99,15 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
                             float* sum_lp, int32_t* n_tok, int B, hipStream_t s,
-                            const int32_t* plen = nullptr, float* nsp = nullptr);
+                            const int32_t* plen = nullptr, float* nsp = nullptr,
+                            const int32_t* roff = nullptr);
 // select_partials_launch at pos followed by embed_launch at pos + 1, in one launch
 void select_embed_launch(const LogitPart* parts, int nblk, const DecodeRules& R, RowRules* rules,
                          int32_t* tokens, int ld, int pos, int32_t* done, float* sum_lp,
                          int32_t* n_tok, int B, hipStream_t s, const int32_t* plen, float* nsp,
                          const _Float16* tok_emb, const float* pos_emb, int d, float* x,
-                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out);
+                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out,
+                         const int32_t* roff = nullptr);
 void build_mask_launch(const int32_t* list, int n, uint8_t* mask, int V, hipStream_t s);
 // out [B][V] = sample_gumbel(noise_base(seeds[b], pos), t)
 void sample_gumbel_launch(const uint32_t* seeds, int B, int pos, int V, float* out, hipStream_t s);

@@ -106,19 +106,21 @@ __global__ __launch_bounds__(256) void embed_kernel(const _Float16* __restrict__
                                                     float2* __restrict__ part,
                                                     const float* __restrict__ ln_g,
                                                     const float* __restrict__ ln_b,
-                                                    _Float16* __restrict__ ln_out) {
+                                                    _Float16* __restrict__ ln_out,
+                                                    const int32_t* __restrict__ roff) {
   const int b = blockIdx.x;
-  embed_row(tok_emb, pos_emb, tokens[(int64_t)b * ld_tokens + pos], b, pos, d, x, part, ln_g, ln_b,
+  const int pb = pos + (roff ? roff[b] : 0);  // the row's own position (staggered rows)
+  embed_row(tok_emb, pos_emb, tokens[(int64_t)b * ld_tokens + pb], b, pb, d, x, part, ln_g, ln_b,
             ln_out);
 }
 
 void embed_launch(const _Float16* tok_emb, const float* pos_emb, const int32_t* tokens,
                   int ld_tokens, int pos, int d, float* x, float2* part, int B, hipStream_t s,
-                  const float* ln_g, const float* ln_b, _Float16* ln_out) {
+                  const float* ln_g, const float* ln_b, _Float16* ln_out, const int32_t* roff) {
   JANUS_CHECK(d % 16 == 0, "embed: d % 16 != 0");
   JANUS_CHECK(!ln_out || d <= 512, "embed: fused LayerNorm needs d <= 512");
   embed_kernel<<<B, 256, 0, s>>>(tok_emb, pos_emb, tokens, ld_tokens, pos, d, x, part, ln_g, ln_b,
-                                 ln_out);
+                                 ln_out, roff);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -673,13 +675,20 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
 // the token, accumulate its log-probability and derive the next step's row rules.
 // Row b's selection at position pos; returns (in thread 0) the row's token at pos + 1:
 // the selected one, eot for a finished row, the forced one inside the row's prompt.
+// roff (nullable): per-row position offsets (staggered rows, janus_decode_rows.pos_offset):
+// row b is at position pos + roff[b]; a row whose next position would pass the token
+// buffer (pos + 1 >= ld) has finished and writes nothing (returns -1).
 __device__ __forceinline__ int select_row(
     const LogitPart* __restrict__ parts, int nblk, const DecodeRules& R, RowRules* __restrict__ rules,
     int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
     float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
-    float* __restrict__ nsp) {
+    float* __restrict__ nsp, const int32_t* __restrict__ roff = nullptr) {
   __shared__ LogitPart sh[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  if (roff) {
+    pos += roff[b];
+    if (pos + 1 >= ld) return -1;  // block-uniform
+  }
   int32_t* row_tok = tokens + (int64_t)b * ld;
   const int pl = plen ? plen[b] : 1;
   if (pos + 1 < pl) return row_tok[pos + 1];  // inside this row's prompt: the forced token stays
@@ -776,8 +785,8 @@ __global__ __launch_bounds__(256) void select_partials_kernel(
     const LogitPart* __restrict__ parts, int nblk, DecodeRules R, RowRules* __restrict__ rules,
     int32_t* __restrict__ tokens, int ld, int pos, int32_t* __restrict__ done,
     float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
-    float* __restrict__ nsp) {
-  (void)select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp);
+    float* __restrict__ nsp, const int32_t* __restrict__ roff) {
+  (void)select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp, roff);
 }
 
 // The selection at position pos and the embedding of the chosen token at pos + 1 in one
@@ -789,32 +798,36 @@ __global__ __launch_bounds__(256) void select_embed_kernel(
     float* __restrict__ sum_lp, int32_t* __restrict__ n_tok, const int32_t* __restrict__ plen,
     float* __restrict__ nsp, const _Float16* __restrict__ tok_emb, const float* __restrict__ pos_emb,
     int d, float* __restrict__ x, float2* __restrict__ part, const float* __restrict__ ln_g,
-    const float* __restrict__ ln_b, _Float16* __restrict__ ln_out) {
+    const float* __restrict__ ln_b, _Float16* __restrict__ ln_out, const int32_t* __restrict__ roff) {
   __shared__ int s_tok;
-  const int t = select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp);
+  const int t = select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp, roff);
+  const int pb = pos + (roff ? roff[blockIdx.x] : 0);
+  if (pb + 1 >= ld) return;  // a staggered row past its last position: nothing to embed
   if (threadIdx.x == 0) s_tok = t;
   __syncthreads();
-  embed_row(tok_emb, pos_emb, s_tok, blockIdx.x, pos + 1, d, x, part, ln_g, ln_b, ln_out);
+  embed_row(tok_emb, pos_emb, s_tok, blockIdx.x, pb + 1, d, x, part, ln_g, ln_b, ln_out);
 }
 
 void select_embed_launch(const LogitPart* parts, int nblk, const DecodeRules& R, RowRules* rules,
                          int32_t* tokens, int ld, int pos, int32_t* done, float* sum_lp,
                          int32_t* n_tok, int B, hipStream_t s, const int32_t* plen, float* nsp,
                          const _Float16* tok_emb, const float* pos_emb, int d, float* x,
-                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out) {
+                         float2* part, const float* ln_g, const float* ln_b, _Float16* ln_out,
+                         const int32_t* roff) {
   JANUS_CHECK(d % 16 == 0, "embed: d % 16 != 0");
   JANUS_CHECK(!ln_out || d <= 512, "embed: fused LayerNorm needs d <= 512");
   select_embed_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok,
-                                        plen, nsp, tok_emb, pos_emb, d, x, part, ln_g, ln_b, ln_out);
+                                        plen, nsp, tok_emb, pos_emb, d, x, part, ln_g, ln_b, ln_out,
+                                        roff);
   JANUS_LAUNCH_CHECK();
 }
 
 void select_partials_launch(const LogitPart* parts, int nblk, const DecodeRules& R,
                             RowRules* rules, int32_t* tokens, int ld, int pos, int32_t* done,
                             float* sum_lp, int32_t* n_tok, int B, hipStream_t s,
-                            const int32_t* plen, float* nsp) {
+                            const int32_t* plen, float* nsp, const int32_t* roff) {
   select_partials_kernel<<<B, 256, 0, s>>>(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp,
-                                           n_tok, plen, nsp);
+                                           n_tok, plen, nsp, roff);
   JANUS_LAUNCH_CHECK();
 }
 

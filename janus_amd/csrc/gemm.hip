@@ -203,6 +203,7 @@ struct SkinnyArgs {
   int msplit_n;
   const float* ln_g; const float* ln_b; float ln_eps; _Float16* ln_out; int* ln_cnt;
   const float* lnin_g; const float* lnin_b;  // AM_LNX: A = LayerNorm(x) computed in-block
+  const int32_t* roff;  // EPI_QKV: per-row position offsets (row r's cache row pos + roff[r])
 };
 
 // A operand modes: fp16 from global memory; LayerNorm-on-load from producer pieces
@@ -438,7 +439,8 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(SkinnyArgs p) {
       static_cast<_Float16*>(p.C)[(int64_t)erow * p.ldc + ecol] = (_Float16)v;
     } else {
       _Float16* cache = ecol < 2 * dq ? p.kc : p.vc;
-      cache[((int64_t)erow * p.n_ctx + p.pos) * dq + (ecol % dq)] = (_Float16)v;
+      const int cpos = p.pos + (p.roff ? p.roff[erow] : 0);
+      cache[((int64_t)erow * p.n_ctx + cpos) * dq + (ecol % dq)] = (_Float16)v;
     }
   } else {
     static_cast<float*>(p.C)[(int64_t)erow * p.ldc + ecol] = v;
@@ -604,6 +606,7 @@ static void launch_skinny(int epi, const GemmArgs& g, hipStream_t s) {
   p.A = g.A; p.lda = g.lda; p.W = g.W; p.ldw = g.ldw; p.bias = g.bias; p.C = g.C; p.ldc = g.ldc;
   p.R = g.R; p.ldr = g.ldr; p.M = g.M; p.N = g.N; p.K = g.K;
   p.kc = g.kc; p.vc = g.vc; p.pos = g.pos; p.n_ctx = g.n_ctx; p.qkv_d = g.qkv_d;
+  p.roff = g.roff;
   p.ln_part = g.ln_part;
   p.a_group_cols = g.a_group_cols;
   p.msplit_n = g.msplit_n;

@@ -19,6 +19,7 @@ struct GemmArgs {
   int M, N, K;
   // EPI_QKV (M <= 64 only): columns [0,d) -> C, [d,2d) -> kc, [2d,3d) -> vc at row pos
   _Float16* kc = nullptr; _Float16* vc = nullptr; int pos = 0, n_ctx = 0, qkv_d = 0;
+  const int32_t* roff = nullptr;  // EPI_QKV: row r's cache row is pos + roff[r] (staggered rows)
   // EPI_RESID_F32 (M <= 64 only): also write the LayerNorm pieces of the new rows,
   // ln_part[row][col / 16] (see SkinnyLnArgs)
   float2* ln_part = nullptr;
@@ -142,7 +143,8 @@ int decode_split_count(int Tkv);
 void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float16* k,
                                    const _Float16* v, int64_t kv_bs, int64_t kv_rs, int Tkv,
                                    _Float16* out, int64_t o_bs, int B, int H, float scale,
-                                   float* part_o, float* part_ml, hipStream_t s);
+                                   float* part_o, float* part_ml, hipStream_t s,
+                                   const int32_t* roff = nullptr, int max_roff = 0);
 
 // ----------------------------------------------------------------- conv
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3 };

@@ -64,7 +64,7 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups, d_roff;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
@@ -385,8 +385,29 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     for (int b = 0; b < B; ++b)
       for (int i = 0; i < opt->prompt_len; ++i) h_init[(size_t)b * maxlen + i] = opt->prompt[i];
   }
-  const int min_plen = *std::min_element(h_plen.begin(), h_plen.end());
-  const int max_plen = *std::max_element(h_plen.begin(), h_plen.end());
+  // staggered rows (janus_decode_rows.pos_offset): rows with an offset > 0 continue the
+  // previous call's state in the same slots (tokens, KV cache, counters, rule state); rows
+  // with 0 start fresh and must be one contiguous range [f0, f1). Every row runs `steps`
+  // positions from its own offset.
+  const bool stagger = rows && rows->pos_offset;
+  int f0 = 0, f1 = B, max_roff = 0;
+  std::vector<int32_t> h_roff;
+  if (stagger) {
+    JANUS_CHECK(!shared && !(smp && smp->temperature > 0.f), "decode: staggered rows are greedy, unshared");
+    h_roff.assign(rows->pos_offset, rows->pos_offset + B);
+    f0 = B; f1 = 0;
+    for (int b = 0; b < B; ++b) {
+      JANUS_CHECK(h_roff[b] >= 0 && h_roff[b] < maxlen, "decode: pos_offset out of range");
+      max_roff = std::max(max_roff, h_roff[b]);
+      if (h_roff[b] == 0) { f0 = std::min(f0, b); f1 = std::max(f1, b + 1); }
+    }
+    if (f1 <= f0) f0 = f1 = 0;
+    for (int b = f0; b < f1; ++b) JANUS_CHECK(h_roff[b] == 0, "decode: fresh rows must be contiguous");
+  }
+  const int steps = (stagger && rows->steps > 0) ? rows->steps : maxlen - 1;
+  JANUS_CHECK(!stagger || max_roff + steps <= maxlen, "decode: pos_offset + steps > max_length");
+  const int min_plen = f1 > f0 ? *std::min_element(h_plen.begin() + f0, h_plen.begin() + f1) : 1;
+  const int max_plen = f1 > f0 ? *std::max_element(h_plen.begin() + f0, h_plen.begin() + f1) : 1;
   JANUS_CHECK(min_plen >= 1 && max_plen < maxlen && maxlen <= NC,
               "decode: need 1 <= prompt_len < max_length <= n_text_ctx");
   const int64_t Me = (int64_t)B * Te;
@@ -437,9 +458,17 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
            *q2 = Z.d_q2.as<_Float16>(), *f = Z.d_f.as<_Float16>();
   int32_t* done = Z.d_done.as<int32_t>();
 
-  // synchronous uploads: the host vectors die with this call
-  JANUS_HIP(hipMemcpyAsync(Z.d_prompt.p, h_plen.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
-  JANUS_HIP(hipMemcpyAsync(tokens, h_init.data(), sizeof(int32_t) * h_init.size(), hipMemcpyHostToDevice, s));
+  // synchronous uploads: the host vectors die with this call (staggered: fresh rows only)
+  if (f1 > f0) {
+    JANUS_HIP(hipMemcpyAsync(Z.d_prompt.as<int32_t>() + f0, h_plen.data() + f0, sizeof(int32_t) * (f1 - f0),
+                             hipMemcpyHostToDevice, s));
+    JANUS_HIP(hipMemcpyAsync(tokens + (int64_t)f0 * maxlen, h_init.data() + (size_t)f0 * maxlen,
+                             sizeof(int32_t) * (size_t)(f1 - f0) * maxlen, hipMemcpyHostToDevice, s));
+  }
+  Z.d_roff.ensure(sizeof(int32_t) * B);
+  if (stagger)
+    JANUS_HIP(hipMemcpyAsync(Z.d_roff.p, h_roff.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
+  const int32_t* roff = stagger ? Z.d_roff.as<int32_t>() : nullptr;
   const bool sampling = smp && smp->temperature > 0.f;
   Z.d_seed.ensure(sizeof(uint32_t) * B);
   if (sampling) {
@@ -451,8 +480,10 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                              hipMemcpyHostToDevice, s));
   JANUS_HIP(hipStreamSynchronize(s));
   build_mask_launch(Z.d_supp.as<int32_t>(), opt->n_suppress, Z.d_smask.as<uint8_t>(), V, s);
-  init_counters_launch(done, sum_lp, n_tokens, Z.d_nsp.as<float>(), B, s);
-  rules_init_launch(Z.d_rules.as<RowRules>(), B, s);
+  if (f1 > f0) {
+    init_counters_launch(done + f0, sum_lp + f0, n_tokens + f0, Z.d_nsp.as<float>() + f0, f1 - f0, s);
+    rules_init_launch(Z.d_rules.as<RowRules>() + f0, f1 - f0, s);
+  }
 
   // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
   const bool xabs = xattn_supported(d, H) && B <= kSkinnyMaxRows && std::getenv("JANUS_NO_XABSORB") == nullptr;
@@ -489,7 +520,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const float scale = 0.125f;
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
-  const int sample_begin = min_plen;  // index of the first sampled token (earliest row)
+  // index of the first sampled token (earliest row); staggered continuing rows sample from
+  // the first step on
+  const int sample_begin = (stagger && f1 - f0 < B) ? 0 : min_plen;
   // JANUS_FUSED_LN (B <= 64): LayerNorm rides on the projections (row-statistic pieces
   // written by the producer of each residual row, normalised on load by the consumer).
   // Opt-in: with the 16-wave skinny GEMM the separate LayerNorm launch measured faster
@@ -568,11 +601,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // bit-identical; JANUS_NO_SEL_EMBED restores the two launches): a step from the first
   // sampled position on finds its row already embedded by the previous step's selection
   const bool fuse_se = std::getenv("JANUS_NO_SEL_EMBED") == nullptr;
+  JANUS_CHECK(!stagger || (!fused_ln && !ln_fuse && !rln && xabs),
+              "decode: staggered rows run the default decoder kernels only");
   auto step = [&](int pos) {
     if (!(fuse_se && pos >= sample_begin && pos > 0))
       embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
                    fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
-                   (ln_fuse || embed_ln) ? a : nullptr);
+                   (ln_fuse || embed_ln) ? a : nullptr, roff);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = Z.d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
@@ -591,14 +626,16 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           GemmArgs g = with_ln(dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d),
                                L.ln1g, L.ln1b, lnp1);
           g.kc = kc; g.vc = vc; g.pos = pos; g.n_ctx = NC; g.qkv_d = d;
+          g.roff = roff;
           gemm_launch(EPI_QKV, g, s);
         } else {
+          JANUS_CHECK(!stagger, "decode: staggered rows need B <= kSkinnyMaxRows");
           gemm_launch(EPI_F16, dgargs(a, d, L.wqkv.as<_Float16>(), d, L.bqkv.as<float>(), qkv, 3 * d, B, 3 * d, d), s);
           kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
         }
       }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
-                                    part_o, part_ml, s);
+                                    part_o, part_ml, s, roff, max_roff);
       if (rln2) resid_ln(o, L.wo, L.bo, L.ln2g, L.ln2b);
       else resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
       if (xabs) {
@@ -669,11 +706,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
                           Z.d_nsp.as<float>(), w->tok16.as<_Float16>(), pos_emb, d, x,
                           fused_ln ? lnp : nullptr, w->dec[0].ln1g, w->dec[0].ln1b,
-                          (ln_fuse || embed_ln) ? a : nullptr);
+                          (ln_fuse || embed_ln) ? a : nullptr, roff);
     else
       select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                              maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
-                             Z.d_nsp.as<float>());
+                             Z.d_nsp.as<float>(), roff);
   };
   const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
   const int chunk = opt->check_every > 0 ? opt->check_every : 16;
@@ -687,7 +724,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
       (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
-      (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows};
+      (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows, (int64_t)roff,
+      (int64_t)max_roff};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -696,8 +734,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   }
   Z.last_positions = 0;
   Z.last_launches = 0;
-  for (int p0 = 0; p0 + 1 < maxlen; p0 += chunk) {
-    const int n = std::min(chunk, maxlen - 1 - p0);
+  for (int p0 = 0; p0 < steps; p0 += chunk) {
+    const int n = std::min(chunk, steps - p0);
     Z.last_positions += n;
     if (use_graph) {
       std::vector<int64_t> key = base_key;
@@ -891,7 +929,8 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     int nlanes = 1;
     if (const char* v = std::getenv("JANUS_DEC_LANES")) nlanes = std::atoi(v);
     nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
-    if (rows && rows->enc_index) nlanes = 1;  // shared encoder rows: one lane holds them all
+    // shared encoder rows / staggered rows: one lane holds them all (and its slots' state)
+    if (rows && (rows->enc_index || rows->pos_offset)) nlanes = 1;
     while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
     if (nlanes == 1 && s != nullptr) {
       decode_greedy(w, *w->lanes[0], e, batch, opt, rows, tokens, n_tokens, sum_logprob,

@@ -345,6 +345,130 @@ class JanusPipeline:
         stats = _prosody_stats(parts if pres is not None else None, B, dec.tokens.device)
         return EncodeResult(texts, tags, packets, dec.tokens, dec.n_tokens, stats, gts)
 
+    # ------------------------------------------- staggered (continuous-batching) step
+    def step_staggered(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
+                       mode=JanusMode.SEMANTIC_VOICE, override="auto", timestamp=None):
+        """The overlapped serving step with the greedy decoder as a continuous batch of TWO
+        batches at different positions (janus_decode_rows.pos_offset): each call of the
+        decoder advances 2B rows by S = ceil((max_length - 1) / 2) positions — batch i's
+        rows (fresh, positions 0 .. S-1) and batch i-1's (continuing in their slots,
+        positions S .. 2S-1), so every step still completes exactly one batch's decode, but
+        the decoder's latency-bound launches serve twice the rows. Per step: mel + encoder of
+        batch i (whole GPU), then decoder (batch i, batch i-1) on the decoder's CUs beside
+        the vocoder of batch i-2 + YIN of batch i on the vocoder's CUs. Returns (EncodeResult,
+        wav, pcm16) of batch i-2, (None, None, None) for the first two calls;
+        ``flush_staggered`` drains. Greedy (T = 0) only; per-row results are bit-identical to
+        the one-batch decode (rows are independent of their neighbours' positions)."""
+        if tuple(self.temperatures) != (0.0,):
+            raise NotImplementedError("staggered decode runs at temperature 0 only")
+        B = len(lengths)
+        w = self.whisper
+        L = self.max_length
+        S = L // 2
+        dev = pcm.device if pcm is not None else self.device
+        main = torch.cuda.current_stream(dev)
+        hi = self._hi_stream(dev)
+        ds, vs = self._split_streams(dev, dec_per_xcd)
+        st = getattr(self, "_stag", None)
+        if st is None or st["B"] != B:
+            d = w.cfg.d_model
+            st = self._stag = {"B": B, "parity": 0, "sets": [None, None], "done": None,
+                               "enc": torch.zeros(2 * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
+                                                  device=dev)}
+        f = st["parity"]
+        c = 1 - f
+        hi.wait_stream(main)
+        with torch.cuda.stream(hi):
+            if pcm is not None:
+                mel = w.logmel(pcm, offsets, B, 3)
+                st["enc"][f * B:(f + 1) * B].copy_(w.encode(mel))
+        # batch i-2 (completed by the previous call) on the host while the encoder runs
+        prev = st["done"]
+        st["done"] = None
+        res_prev = self._finish(*prev) if prev is not None else None
+        vs.wait_stream(hi)
+        ds.wait_stream(hi)
+        record = getattr(self, "side_events", None) is not None
+        if record:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(vs)
+            ev[2].record(ds)
+        wav = pcm16 = None
+        pres = None
+        # YIN of the first JANUS_YIN_DEC_UTTS utterances runs on the decoder side after the
+        # decoder call (evens out the two sides), the rest behind the vocoder
+        n_dec = min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "0"))) if pcm is not None else 0
+
+        def yin(u0, u1):
+            try:
+                return prosody_launch(pcm, offsets[u0:u1 + 1], lengths[u0:u1], CAPTURE_RATE, 512,
+                                      max_blocks=0)
+            except Exception:  # engine.py:520-525
+                return None
+        with torch.cuda.stream(vs):
+            if res_prev is not None:
+                wav, pcm16, _ = self.decode(res_prev.packets, frames)
+            if pcm is not None:
+                pres = yin(n_dec, B)
+            if record:
+                ev[1].record(vs)
+        cont = st["sets"][c]
+        # fresh rows start at 0, the continuing set at S. The first call starts every slot
+        # fresh (no slot holds state yet); later, a slot set without a batch runs as
+        # continuing rows over the finished state it holds (its output is not read)
+        if not st.get("started"):
+            offs = [0] * (2 * B)
+        else:
+            offs = [0] * (2 * B)
+            for k in range(2 * B):
+                if k // B == c or pcm is None:
+                    offs[k] = S if k // B == c else L - S
+        dec = None
+        if pcm is not None or cont is not None:
+            with torch.cuda.stream(ds):
+                dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
+                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+                                  cu_count=self._dec_s.n_cus)
+                if n_dec > 0:
+                    pres = (yin(0, n_dec), pres)
+        st["sets"][f] = (None if pcm is None else {"pres": pres, "B": B, "mode": mode,
+                                                  "override": override, "timestamp": timestamp})
+        if record:
+            ev[3].record(ds)
+            self.side_events.append(ev)
+        st["started"] = True
+        main.wait_stream(ds)
+        main.wait_stream(vs)
+        if cont is not None:
+            sl = slice(c * B, (c + 1) * B)
+            from .whisper import DecodeOut
+            part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
+                             dec.no_speech_prob[sl], dec.prompt_lens[sl])
+            st["done"] = (part, cont["pres"], B, cont["mode"], cont["override"], cont["timestamp"])
+        st["sets"][c] = None
+        st["parity"] = c
+        return res_prev, wav, pcm16
+
+    def flush_staggered(self, frames):
+        """Drain the staggered pipeline: finish the batch still in the decoder and render
+        the last two batches. Returns a list of (EncodeResult, wav, pcm16)."""
+        out = []
+        st = getattr(self, "_stag", None)
+        if st is None:
+            return out
+        dev = st["enc"].device
+        for _ in range(2):
+            r = self.step_staggered(None, None, [0] * st["B"], frames)
+            if r[0] is not None:
+                out.append(r)
+        prev, st["done"] = st["done"], None
+        if prev is not None:
+            res = self._finish(*prev)
+            wav, pcm16, _ = self.decode(res.packets, frames)
+            out.append((res, wav, pcm16))
+        self._stag = None
+        return out
+
     def flush(self, frames):
         """Finish and render the batch the last overlapped step left pending:
         (EncodeResult, wav, pcm16), or (None, None, None)."""

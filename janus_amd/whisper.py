@@ -63,7 +63,8 @@ class janus_decode_rows(ctypes.Structure):
     _fields_ = [("prompts", ctypes.POINTER(ctypes.c_int32)),
                 ("prompt_lens", ctypes.POINTER(ctypes.c_int32)),
                 ("stride", ctypes.c_int), ("no_speech_token", ctypes.c_int),
-                ("enc_index", ctypes.POINTER(ctypes.c_int32)), ("n_enc", ctypes.c_int)]
+                ("enc_index", ctypes.POINTER(ctypes.c_int32)), ("n_enc", ctypes.c_int),
+                ("pos_offset", ctypes.POINTER(ctypes.c_int32)), ("steps", ctypes.c_int)]
 
 
 # ----------------------------------------------------------------- front end
@@ -311,13 +312,18 @@ class WhisperEngine:
 
     def decode_ex(self, enc: torch.Tensor, prompts=None, max_length: int = 448,
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
-                  cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None):
+                  cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None,
+                  pos_offset=None, steps: int = 0):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
         rule-filtered logits / T with per-row uint32 ``seeds``). ``enc_index`` (one int per
         decoder row): row b attends to enc[enc_index[b]] — the best_of hypotheses of a
-        window share its encoder output, read once per pair of rows."""
+        window share its encoder output, read once per pair of rows. ``pos_offset`` /
+        ``steps`` (greedy): a staggered call — row b runs ``steps`` positions from
+        pos_offset[b]; rows with an offset > 0 continue this context's previous call in the
+        same row (pass the same batch size and their encoder output again), rows with 0
+        start fresh (one contiguous range)."""
         B = enc.shape[0] if enc_index is None else len(enc_index)
         if temperature > 0:
             if seeds is None or len(seeds) != B:
@@ -326,6 +332,13 @@ class WhisperEngine:
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
+        po = None
+        if pos_offset is not None:
+            po = np.ascontiguousarray(np.asarray(pos_offset, np.int32))
+            if po.shape != (B,):
+                raise ValueError("pos_offset needs one offset per row")
+            rows.pos_offset = po.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            rows.steps = int(steps)
         ei = None
         if enc_index is not None:
             ei = np.ascontiguousarray(np.asarray(enc_index, np.int32))
@@ -358,7 +371,7 @@ class WhisperEngine:
             nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
                      ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
                      nsp.data_ptr(), nat.stream_ptr())
-        del keep, pr, ei
+        del keep, pr, ei, po
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 
     def decode_info(self):

@@ -221,6 +221,63 @@ def test_shared_encoder_rows_match_replicated(engine, gpu, T, idx):
             assert torch.equal(b.tokens.cpu()[:len(idx)], first)
 
 
+@pytest.mark.parametrize("L", [40, 448])
+def test_staggered_decode_matches_full(engine, gpu, L):
+    """Continuous batching across decode calls (janus_decode_rows.pos_offset): two row sets
+    share one context, each call runs S = L / 2 positions; a set starts fresh in one call
+    and continues (offset S, its KV cache / tokens / rule state kept in its slots) in the
+    next, while the other set does the opposite. Every batch's tokens, summed
+    log-probabilities and no-speech probabilities equal a single full decode of that batch
+    alone: rows are independent of their neighbours' positions."""
+    eng, _ = engine
+    N, S = 3, L // 2
+    batches = []
+    for k in range(3):
+        utts = [synth_speech(300 + 10 * k + j, 1.5 + j) for j in range(N)]
+        pcm, offs = pack(utts, gpu)
+        batches.append(eng.encode(eng.logmel(pcm, offs, N, 3)))
+    ref = [eng.decode_ex(e, max_length=L) for e in batches]
+    sets = [None, None]          # slot set -> batch index in it
+    got = {}
+    for call in range(4):
+        fresh = call % 2         # slot set taking a new batch this call
+        cont = 1 - fresh
+        if call < 3:
+            sets[fresh] = call
+        else:
+            sets[fresh] = None   # nothing new: zero rows at the end of their positions
+        rows_enc, offs = [], []
+        for st in (0, 1):
+            bi = sets[st]
+            if bi is None:
+                rows_enc.append(torch.zeros_like(batches[0]))
+                offs += [L - S] * N if st == cont or call == 3 else [0] * N
+            else:
+                rows_enc.append(batches[bi])
+                offs += [0 if st == fresh else S] * N
+        if call == 0:
+            offs = [0] * (2 * N)                      # the first call: everything fresh
+        out = eng.decode_ex(torch.cat(rows_enc), max_length=L, pos_offset=offs, steps=S)
+        if call > 0 and sets[cont] is not None:       # the continuing set just finished
+            bi = sets[cont]
+            sl = slice(cont * N, cont * N + N)
+            got[bi] = (out.tokens[sl].cpu(), out.n_tokens[sl].cpu(), out.sum_logprob[sl].cpu(),
+                       out.no_speech_prob[sl].cpu())
+            sets[cont] = None
+    torch.cuda.synchronize()
+    assert sorted(got) == [0, 1, 2]
+    plen = len(eng.tokenizer.sot_sequence)
+    for bi, r in enumerate(ref):
+        t, n, lp, ns = got[bi]
+        assert torch.equal(n, r.n_tokens.cpu()) and torch.equal(lp, r.sum_logprob.cpu())
+        assert torch.equal(ns, r.no_speech_prob.cpu())
+        rt = r.tokens.cpu()
+        for j in range(N):   # up to the row's end (past an eot the two pad differently)
+            k = plen + int(n[j])
+            assert torch.equal(t[j, :k], rt[j, :k]), (bi, j)
+        assert int(n.min()) >= min(16, L - plen - 1)
+
+
 def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
     """Opt-in decoder lanes (JANUS_DEC_LANES: the batch split over concurrent streams and
     host threads) decode every utterance exactly as the single-lane decoder does: rows
