@@ -679,9 +679,12 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const _Float16* h8 = reinterpret_cast<const _Float16*>(&kr[i]);
+    // explicit fmaf (here and below): left to the compiler, the contraction of these
+    // sums into fma / pk_mul + add differed between NR instantiations, so a row's result
+    // depended on the LONGEST row of its launch (staggered rows) in the last bits
     float dot = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dot += (float)h8[j] * qv[j];
+    for (int j = 0; j < 8; ++j) dot = fmaf((float)h8[j], qv[j], dot);
     dot += __shfl_xor(dot, 1);
     dot += __shfl_xor(dot, 2);
     dot += __shfl_xor(dot, 4);
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
       l += p;
       const _Float16* h8 = reinterpret_cast<const _Float16*>(&vr[i]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += p * (float)h8[j];
+      for (int j = 0; j < 8; ++j) a[j] = fmaf(p, (float)h8[j], a[j]);
     }
   }
   // sum over the 8 key groups (lanes sharing dg); l is replicated over dg
@@ -726,8 +729,8 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
 #pragma unroll
     for (int i = 0; i < kHeadWaves; ++i) {
       const float f = exp2f(wm[i] - M);  // empty wave: -inf -> 0
-      L += wl[i] * f;
-      O += wo[i][threadIdx.x] * f;
+      L = fmaf(wl[i], f, L);
+      O = fmaf(wo[i][threadIdx.x], f, O);
     }
     out[(int64_t)b * o_bs + h * kHd + threadIdx.x] = (_Float16)(O / L);
   }
