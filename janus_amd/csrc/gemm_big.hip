@@ -19,6 +19,8 @@
 //
 // Accumulation order: one fp32 accumulator per output, k-steps of 32 in order — the same
 // MFMA sequence per output as gemm_nt_kernel (gemm.hip), so the two are bit-identical.
+#include <cstdlib>
+
 #include "mfma.h"
 #include "kernels.h"
 
@@ -44,6 +46,72 @@ __device__ __forceinline__ void glds_rows8(const _Float16* __restrict__ src, int
   const _Float16* g = src + (int64_t)gr * ld + k0 + 8 * c;
   typedef __attribute__((address_space(3))) void lds_void;
   __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)lds_piece, 16, 0, 0);
+}
+
+// epilogue, two passes of 64 rows per wave through the wave's own LDS image (the staging
+// LDS is free by then)
+template <int EPI>
+__device__ __forceinline__ void gemm_big_epilogue(const GemmArgs& p, f32x4 (&acc)[kWMT][kWNT],
+                                                  unsigned char* smem_raw, int row0, int col0,
+                                                  int wm, int wn, int lane, int wid) {
+  const int M = p.M;
+  const int fr = lane & 15;
+  float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
+  const int er = lane >> 3, ec = (lane & 7) * 8;           // 8 rows x 8 lanes per pass step
+  const int gcol = col0 + wn * 64 + ec;
+  float bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = p.bias ? p.bias[gcol + j] : 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sC[(m * 16 + (lane >> 4) * 4 + r) * kEP + n * 16 + fr] = acc[4 * h + m][n][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's stores land before its reads
+    __builtin_amdgcn_wave_barrier();
+    // RESID: the pass's residual rows are loaded before any of its stores (vmcnt retires in
+    // issue order, so a residual load issued behind a store waits for that store)
+    float4 res[8][2];
+    if constexpr (EPI == EPI_RESID_F32) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = min(row0 + wm * 128 + h * 64 + it * 8 + er, M - 1);
+        res[it][0] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol);
+        res[it][1] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol + 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + er;
+      const int row = row0 + wm * 128 + h * 64 + lr;
+      const float4 lo = *reinterpret_cast<const float4*>(sC + lr * kEP + ec);
+      const float4 hi = *reinterpret_cast<const float4*>(sC + lr * kEP + ec + 4);
+      float v[8] = {lo.x + bias[0], lo.y + bias[1], lo.z + bias[2], lo.w + bias[3],
+                    hi.x + bias[4], hi.y + bias[5], hi.z + bias[6], hi.w + bias[7]};
+      if (row < M) {
+        if constexpr (EPI == EPI_F16 || EPI == EPI_GELU_F16) {
+          half8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (_Float16)(EPI == EPI_GELU_F16 ? gelu_erf(v[j]) : v[j]);
+          *reinterpret_cast<half8*>(static_cast<_Float16*>(p.C) + (int64_t)row * p.ldc + gcol) = o;
+        } else {
+          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + gcol;
+          if constexpr (EPI == EPI_RESID_F32) {
+            v[0] += res[it][0].x; v[1] += res[it][0].y; v[2] += res[it][0].z; v[3] += res[it][0].w;
+            v[4] += res[it][1].x; v[5] += res[it][1].y; v[6] += res[it][1].z; v[7] += res[it][1].w;
+          }
+          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();       // the next pass overwrites the image
+  }
 }
 
 template <int EPI>
@@ -112,63 +180,134 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  // epilogue, two passes of 64 rows per wave through the wave's own LDS image
-  float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
-  const int er = lane >> 3, ec = (lane & 7) * 8;           // 8 rows x 8 lanes per pass step
-  const int gcol = col0 + wn * 64 + ec;
-  float bias[8];
+  gemm_big_epilogue<EPI>(p, acc, smem_raw, row0, col0, wm, wn, lane, wid);
+}
+
+// Ping-pong variant (JANUS_GEMM_BIG=pp): the same tile, fragments, MFMA order and epilogue,
+// but the two wave groups (wm = 0 / 1, one wave of each per SIMD) run half a k-tile apart:
+// between two consecutive barriers one group reads its fragments of a k-tile out of LDS (and
+// issues its half of the next k-tile's DMA) while the other runs its 64 MFMAs, so the LDS
+// reads and the matrix pipe overlap instead of every wave waiting on LDS at the same time.
+// Barrier slots (group 1 enters one slot late, group 0 leaves one slot late):
+//   slot 2t   : g0 reads k-tile t, DMAs A of k-tile t+1 | g1 MFMAs k-tile t-1, DMAs B of t+1
+//   slot 2t+1 : g0 MFMAs k-tile t                        | g1 reads k-tile t
+// k-tile t+1's DMA (into the buffer k-tile t-1 used, whose reads retired by slot 2t-1's end)
+// is waited (vmcnt(0)) by the issuing waves before slot 2t+1's closing barrier and read from
+// slot 2t+2 on. Each read slot ends with lgkmcnt(0) so the buffer is free for the DMA two
+// slots later.
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// a buffer descriptor from wave-uniform inputs, made provably uniform (readfirstlane), so the
+// compiler keeps it in SGPRs instead of wrapping the load in a waterfall loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const _Float16* base, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_big_pp_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int row0 = bm * kBM, col0 = bn * kBN;
+  const int lane = threadIdx.x & 63, wid = wave_id();
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // group 0 DMAs the A tile, group 1 the B tile: wave wn of the group rows [64 wn, 64 wn + 64),
+  // eight 8-row pieces
+  // DMA through buffer descriptors (buffer_load ... lds), one per 8-row piece (SGPRs: base
+  // at the piece's first row, range = the piece's rows that exist), a 32-bit per-lane voffset
+  // (row within the piece, swizzled chunk: two variants, since piece i's rows r satisfy
+  // ((r >> 1) & 7) = 4 (i & 1) + (lane >> 4)) and the k-tile in soffset: four VGPRs of
+  // addressing in all. A rows past M are out of their piece's range and read as zero.
+  const int lr8 = lane >> 3;
+  const uint32_t c0 = 16u * ((lane & 7) ^ ((lr8 >> 1) & 7));
+  const uint32_t c1 = 16u * ((lane & 7) ^ (((lr8 >> 1) + 4) & 7));
+  const uint32_t va0 = (uint32_t)(lr8 * p.lda) * 2u + c0, va1 = (uint32_t)(lr8 * p.lda) * 2u + c1;
+  const uint32_t vw0 = (uint32_t)(lr8 * p.ldw) * 2u + c0, vw1 = (uint32_t)(lr8 * p.ldw) * 2u + c1;
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto stage_a = [&](int kt) {
+    _Float16* sA = smem + (kt & 1) * kStageHalves;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bias[j] = p.bias ? p.bias[gcol + j] : 0.0f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < kWNT; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sC[(m * 16 + (lane >> 4) * 4 + r) * kEP + n * 16 + fr] = acc[4 * h + m][n][r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's stores land before its reads
-    __builtin_amdgcn_wave_barrier();
-    // RESID: the pass's residual rows are loaded before any of its stores (vmcnt retires in
-    // issue order, so a residual load issued behind a store waits for that store)
-    float4 res[8][2];
-    if constexpr (EPI == EPI_RESID_F32) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int row = min(row0 + wm * 128 + h * 64 + it * 8 + er, M - 1);
-        res[it][0] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol);
-        res[it][1] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol + 4);
-      }
+    for (int i = 0; i < 8; ++i) {
+      const int rl = wn * 64 + i * 8;
+      const int rows = max(0, min(8, M - row0 - rl));
+      const __amdgpu_buffer_rsrc_t r = uniform_rsrc(p.A + (int64_t)(row0 + rl) * p.lda, rows * p.lda * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(sA + rl * kBK), 16, (i & 1) ? va1 : va0,
+                                               kt * kBK * 2, 0, 0);
     }
+  };
+  auto stage_b = [&](int kt) {
+    _Float16* sB = smem + (kt & 1) * kStageHalves + kBM * kBK;
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int lr = it * 8 + er;
-      const int row = row0 + wm * 128 + h * 64 + lr;
-      const float4 lo = *reinterpret_cast<const float4*>(sC + lr * kEP + ec);
-      const float4 hi = *reinterpret_cast<const float4*>(sC + lr * kEP + ec + 4);
-      float v[8] = {lo.x + bias[0], lo.y + bias[1], lo.z + bias[2], lo.w + bias[3],
-                    hi.x + bias[4], hi.y + bias[5], hi.z + bias[6], hi.w + bias[7]};
-      if (row < M) {
-        if constexpr (EPI == EPI_F16 || EPI == EPI_GELU_F16) {
-          half8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (_Float16)(EPI == EPI_GELU_F16 ? gelu_erf(v[j]) : v[j]);
-          *reinterpret_cast<half8*>(static_cast<_Float16*>(p.C) + (int64_t)row * p.ldc + gcol) = o;
-        } else {
-          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + gcol;
-          if constexpr (EPI == EPI_RESID_F32) {
-            v[0] += res[it][0].x; v[1] += res[it][0].y; v[2] += res[it][0].z; v[3] += res[it][0].w;
-            v[4] += res[it][1].x; v[5] += res[it][1].y; v[6] += res[it][1].z; v[7] += res[it][1].w;
-          }
-          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      }
+    for (int i = 0; i < 8; ++i) {
+      const int rl = wn * 64 + i * 8;
+      const __amdgpu_buffer_rsrc_t r = uniform_rsrc(p.W + (int64_t)(col0 + rl) * p.ldw, 8 * p.ldw * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(sB + rl * kBK), 16, (i & 1) ? vw1 : vw0,
+                                               kt * kBK * 2, 0, 0);
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();       // the next pass overwrites the image
+  };
+
+  f32x4 acc[kWMT][kWNT];
+#pragma unroll
+  for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+    for (int n = 0; n < kWNT; ++n) acc[m][n] = zero_f32x4();
+
+  const int fr = lane & 15, sw = fr >> 1;
+  const int a_off = (wm * 128 + fr) * kBK, b_off = kBM * kBK + (wn * 64 + fr) * kBK;
+  const int nk = K / kBK;
+
+  if (wm == 0) stage_a(0); else stage_b(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wm == 1) {
+    if (nk > 1) stage_b(1);
+    pp_barrier();                          // group 1 enters one slot late
   }
+  for (int kt = 0; kt < nk; ++kt) {
+    // read slot
+    if (wm == 0 && kt + 1 < nk) stage_a(kt + 1);
+    const _Float16* buf = smem + (kt & 1) * kStageHalves;
+    half8 a[2][kWMT], b[2][kWNT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n) b[s][n] = *reinterpret_cast<const half8*>(buf + b_off + n * 16 * kBK + ch);
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m) a[s][m] = *reinterpret_cast<const half8*>(buf + a_off + m * 16 * kBK + ch);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    // MFMA slot
+    if (wm == 1 && kt + 2 < nk) stage_b(kt + 2);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+        for (int n = 0; n < kWNT; ++n) acc[m][n] = mfma16(a[s][m], b[s][n], acc[m][n]);
+    __builtin_amdgcn_s_setprio(0);
+    if (wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();               // group 0 leaves one slot late
+  __syncthreads();                         // the epilogue overwrites the staging buffers
+  gemm_big_epilogue<EPI>(p, acc, smem_raw, row0, col0, wm, wn, lane, wid);
 }
 
 bool gemm_big_supported(int epi, const GemmArgs& p) {
@@ -184,6 +323,17 @@ bool gemm_big_supported(int epi, const GemmArgs& p) {
 void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
   const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
+  const char* v = std::getenv("JANUS_GEMM_BIG");   // read per launch: A/B in one process
+  if (v && v[0] == 'p') {
+    switch (epi) {
+      case EPI_F16: gemm_big_pp_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_GELU_F16: gemm_big_pp_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_RESID_F32: gemm_big_pp_kernel<EPI_RESID_F32><<<blocks, kThreads, 0, s>>>(p); break;
+      default: gemm_big_pp_kernel<EPI_F32><<<blocks, kThreads, 0, s>>>(p); break;
+    }
+    JANUS_LAUNCH_CHECK();
+    return;
+  }
   switch (epi) {
     case EPI_F16: gemm_big_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
     case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;

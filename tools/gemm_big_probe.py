@@ -50,6 +50,38 @@ def main():
             us = e0.elapsed_time(e1) * 1000 / 20
             res[fn.replace("janus_", "") + "_us"] = round(us, 1)
             res[fn.replace("janus_", "") + "_tflops"] = round(2.0 * M * N * K / us / 1e6, 1)
+        # JANUS_GEMM_BIG schedules A/B'd in one process, interleaved rounds (the variant is
+        # read per launch): median and min microseconds, bit-identity with the default
+        for v in [x for x in os.environ.get("GEMM_VARIANTS", "").split(",") if x]:
+            os.environ["JANUS_GEMM_BIG"] = v
+            if epi == 2:
+                C.copy_(R0)
+            else:
+                C.zero_()
+            run()
+            torch.cuda.synchronize()
+            res["eq_" + v] = bool(torch.equal(C.float(), outs.get("janus_gemm_f16", C.float())))
+        rounds = {}
+        for r in range(int(os.environ.get("GEMM_ROUNDS", "5")) if os.environ.get("GEMM_VARIANTS") else 0):
+            for v in [x for x in os.environ["GEMM_VARIANTS"].split(",") if x]:
+                os.environ["JANUS_GEMM_BIG"] = v
+                def run_v():
+                    nat.call("janus_gemm_f16", epi, A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(),
+                             C.data_ptr(), N, C.data_ptr() if epi == 2 else None, N, M, N, K, s)
+                run_v()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    run_v()
+                e1.record()
+                torch.cuda.synchronize()
+                rounds.setdefault(v, []).append(e0.elapsed_time(e1) * 100)
+        os.environ.pop("JANUS_GEMM_BIG", None)
+        for v, ts in rounds.items():
+            ts.sort()
+            res[v + "_us_median"] = round(ts[len(ts) // 2], 1)
+            res[v + "_us_min"] = round(ts[0], 1)
+            res[v + "_tflops_median"] = round(2.0 * M * N * K / ts[len(ts) // 2] / 1e6, 1)
         if "janus_gemm_f16" in outs and "janus_gemm_nt128_f16" in outs:
             res["big_eq_nt128"] = bool(torch.equal(outs["janus_gemm_f16"], outs["janus_gemm_nt128_f16"]))
         if "janus_gemm_f16" in outs and "janus_gemm_lt_f16" in outs:
