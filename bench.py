@@ -57,7 +57,11 @@ def parse():
     ap.add_argument("--stagger", type=int, default=int(os.environ.get("JANUS_STAGGER", "0")),
                     help="1: continuous batching in the decoder (JanusPipeline.step_staggered): "
                          "each step's decoder call advances batch i from position 0 and batch "
-                         "i-1 from the middle, 128 rows; still one batch in and one out per step")
+                         "i-1 from the middle, 128 rows; still one batch in and one out per step. "
+                         "2: the same with the encoder on its own CU lane beside the decoder "
+                         "and the vocoder (JanusPipeline.step_pipelined, --enc-cus)")
+    ap.add_argument("--enc-cus", type=int, default=int(os.environ.get("JANUS_ENC_CUS", "4")),
+                    help="--stagger 2: CUs per XCD for the encoder lane, carved out of --overlap")
     ap.add_argument("--no-idle-latency", action="store_true",
                     help="skip the flush and the three idle-pipeline latency steps after the timed "
                          "region (profiling runs: only priming, warm-up and timed overlapped steps "
@@ -549,7 +553,11 @@ def main():
     last = {}
 
     def step():
-        if args.overlap > 0 and args.stagger and len(pipe.temperatures) == 1:
+        if args.overlap > 0 and args.stagger == 2 and len(pipe.temperatures) == 1:
+            # three lanes: encoder of batch i, decoder of batches i-1 / i-2, vocoder of i-3
+            enc, wav, pcm16 = pipe.step_pipelined(pcm, offs, lengths, frames, args.overlap,
+                                                  args.enc_cus)
+        elif args.overlap > 0 and args.stagger and len(pipe.temperatures) == 1:
             # continuous batching: batch i's first half and batch i-1's second half of the
             # decode in one decoder call, the vocoder of batch i-2 beside it
             enc, wav, pcm16 = pipe.step_staggered(pcm, offs, lengths, frames, args.overlap)
@@ -565,7 +573,7 @@ def main():
 
     # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
-    prime = (2 if args.stagger else 1) if args.overlap > 0 else 0
+    prime = (1 + int(args.stagger)) if args.overlap > 0 else 0
     for _ in range(args.warmup + prime):
         enc = step()
     torch.cuda.synchronize()
@@ -592,6 +600,7 @@ def main():
     t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
     sides = [(e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in (pipe.side_events or [])]
+    enc_side = [e[4].elapsed_time(e[5]) for e in (pipe.side_events or []) if len(e) >= 6]
     pipe.side_events = None
     dec_positions, dec_launches = pipe.whisper.decode_info()
     tok_counts = [float(n.float().mean().item()) for n in tok_counts]
@@ -601,7 +610,7 @@ def main():
     # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
     idle = []
     if args.overlap > 0 and not args.no_idle_latency:
-        pipe.flush_staggered(frames) if args.stagger else pipe.flush(frames)
+        {0: pipe.flush, 1: pipe.flush_staggered, 2: pipe.flush_pipelined}[args.stagger](frames)
     for _ in range(0 if args.no_idle_latency else 3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -689,19 +698,23 @@ def main():
             "xrt_per_gpu": round(value / world, 2),
             # overlapped: an utterance is encoded in one step and vocoded in the next
             # an utterance's steps: encode + decode, then vocoder (overlapped: 2 steps);
-            # staggered: encode + first half, second half, vocoder (3 steps)
+            # staggered: encode + first half, second half, vocoder (3 steps); pipelined:
+            # encode, first half, second half, vocoder (4 steps)
             "p50_latency_ms": round(float(np.median(
-                [sum(times[i:i + (3 if args.stagger else 2)])
-                 for i in range(len(times) - (2 if args.stagger else 1))]
-                if args.overlap > 0 and len(times) > (2 if args.stagger else 1)
+                [sum(times[i:i + 2 + int(args.stagger)])
+                 for i in range(len(times) - 1 - int(args.stagger))]
+                if args.overlap > 0 and len(times) > 1 + int(args.stagger)
                 else times)) * 1000.0, 2),
             "stagger": int(args.stagger),
             # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
             "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
             # wall time of the two CU partitions per timed step (HIP events on each side's
             # stream): vocoder + YIN, greedy decoder
-            "side_ms": {"vocoder": [round(a, 1) for a, _ in sides],
-                        "decoder": [round(b, 1) for _, b in sides]} if sides else None,
+            "side_ms": dict({"vocoder": [round(a, 1) for a, _ in sides],
+                             "decoder": [round(b, 1) for _, b in sides]},
+                            **({"encoder": [round(x, 1) for x in enc_side]} if enc_side else {}))
+            if sides else None,
+            "enc_cus": args.enc_cus if args.stagger == 2 else None,
             "overlap": args.overlap,
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),
@@ -747,7 +760,8 @@ def main():
                 "decoder": decoder_roofline(
                     pipe.whisper.cfg, (2 if args.stagger else 1) * B, dec_positions, dec_launches,
                     float(np.mean([b for _, b in sides])) if sides else None,
-                    round(1.0 - cu_share, 4) if args.overlap > 0 else 1.0,
+                    round(1.0 - cu_share - (args.enc_cus * 8 / n_cus if args.stagger == 2 else 0), 4)
+                    if args.overlap > 0 else 1.0,
                     tkv_positions=(2 * dec_positions - 1) if args.stagger else None),
             },
             "cpu_baseline": None,

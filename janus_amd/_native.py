@@ -6,6 +6,8 @@ valid in both. There is no fallback: if the library is missing or fails to load,
 every janus_amd entry point raises.
 """
 import ctypes
+
+import numpy as np
 import os
 
 import torch  # noqa: F401  (must precede the dlopen below)
@@ -171,6 +173,21 @@ class MaskedStream:
                 lib().janus_stream_destroy(h)
             except Exception:
                 pass
+
+
+def group_cu_masks(n_cus: int, per_xcd, n_xcd: int = 8):
+    """Disjoint CU masks for consecutive groups of per_xcd[g] CUs on every XCD (the same
+    interleaved numbering as split_cu_masks: CU i on XCD i % 8, slot i // 8)."""
+    slots = n_cus // n_xcd
+    assert all(k > 0 for k in per_xcd) and sum(per_xcd) <= slots, (per_xcd, slots)
+    words = (n_cus + 31) // 32
+    masks = [[0] * words for _ in per_xcd]
+    edges = np.cumsum([0] + list(per_xcd))
+    for i in range(n_cus):
+        g = int(np.searchsorted(edges, i // n_xcd, side="right")) - 1
+        if g < len(per_xcd):
+            masks[g][i // 32] |= 1 << (i % 32)
+    return masks
 
 
 def split_cu_masks(n_cus: int, dec_per_xcd: int, n_xcd: int = 8):

@@ -114,7 +114,10 @@ __device__ __forceinline__ void gemm_big_epilogue(const GemmArgs& p, f32x4 (&acc
   }
 }
 
-template <int EPI>
+// ROT (diagnostic, JANUS_GEMM_BIG=rot): block b walks its k-tiles starting at b % nk, so the
+// blocks in flight stage different k-column bands of A / W at the same time (probes L2 channel
+// camping; changes the fp32 accumulation order, so not bit-identical to gemm_nt_kernel)
+template <int EPI, bool ROT = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
   auto stage = [&](int kt, int b) {
     _Float16* sA = smem + b * kStageHalves;
     _Float16* sB = sA + kBM * kBK;
-    const int k0 = kt * kBK;
+    const int k0 = (ROT ? (kt + bid) % (K / kBK) : kt) * kBK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rl = wid * 32 + i * 8;
@@ -324,6 +327,16 @@ void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
   const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
   const char* v = std::getenv("JANUS_GEMM_BIG");   // read per launch: A/B in one process
+  if (v && v[0] == 'r') {
+    switch (epi) {
+      case EPI_F16: gemm_big_kernel<EPI_F16, true><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16, true><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_RESID_F32: gemm_big_kernel<EPI_RESID_F32, true><<<blocks, kThreads, 0, s>>>(p); break;
+      default: gemm_big_kernel<EPI_F32, true><<<blocks, kThreads, 0, s>>>(p); break;
+    }
+    JANUS_LAUNCH_CHECK();
+    return;
+  }
   if (v && v[0] == 'p') {
     switch (epi) {
       case EPI_F16: gemm_big_pp_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;

@@ -209,6 +209,7 @@ class JanusPipeline:
             # a second stream on the decoder's CUs: YIN beside the latency-bound decoder
             self._yin_s = nat.MaskedStream(dmask, device)
             self._split_key = key
+            self._lane_key = None
         return self._dec_s.stream, self._voc_s.stream
 
     def step_overlapped(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
@@ -467,6 +468,160 @@ class JanusPipeline:
             wav, pcm16, _ = self.decode(res.packets, frames)
             out.append((res, wav, pcm16))
         self._stag = None
+        return out
+
+    # ------------------------------ three-lane step: the encoder off the critical path
+    def _lane_streams(self, device, dec_per_xcd: int, enc_per_xcd: int):
+        key = (str(device), dec_per_xcd, enc_per_xcd)
+        if getattr(self, "_lane_key", None) != key:
+            n = torch.cuda.get_device_properties(device).multi_processor_count
+            dmask, emask, vmask = nat.group_cu_masks(
+                n, [dec_per_xcd - enc_per_xcd, enc_per_xcd, n // 8 - dec_per_xcd])
+            self._dec_s = nat.MaskedStream(dmask, device)
+            self._enc_s = nat.MaskedStream(emask, device)
+            self._voc_s = nat.MaskedStream(vmask, device)
+            self._lane_key = key
+            self._split_key = None
+        return self._dec_s.stream, self._enc_s.stream, self._voc_s.stream
+
+    def step_pipelined(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
+                       enc_per_xcd: int = 4, mode=JanusMode.SEMANTIC_VOICE, override="auto",
+                       timestamp=None):
+        """The staggered serving step with the encoder moved OFF the critical path: three
+        CU-disjoint lanes run side by side for the whole step —
+          encoder lane (``enc_per_xcd`` CUs of each XCD, carved out of the decoder's
+            ``dec_per_xcd``): mel + encoder of batch i into a staging buffer;
+          decoder lane (the other dec_per_xcd - enc_per_xcd): ONE continuous-batch decode
+            call of batch i-1 (fresh, positions 0 .. S-1, its encoder output copied out of
+            the staging buffer first) and batch i-2 (continuing, positions S .. 2S-1);
+          vocoder lane (the rest): the vocoder of batch i-3 (finished on the host at the
+            end of the previous call), then YIN of batch i.
+        The host finishes batch i-2 (transcripts, tags, packets) as soon as the decoder lane
+        is done, inside the vocoder lane's time. Returns (EncodeResult, wav, pcm16) of batch
+        i-3 ((None, None, None) for the first three calls); ``flush_pipelined`` drains.
+        Greedy (T = 0) only; per-row results are those of the one-batch decode (the
+        staggered decode's parity, and the encoder is the same kernels on fewer CUs)."""
+        if tuple(self.temperatures) != (0.0,):
+            raise NotImplementedError("pipelined step runs at temperature 0 only")
+        B = len(lengths)
+        w = self.whisper
+        L = self.max_length
+        S = L // 2
+        dev = pcm.device if pcm is not None else self.device
+        main = torch.cuda.current_stream(dev)
+        ds, es, vs = self._lane_streams(dev, dec_per_xcd, enc_per_xcd)
+        st = getattr(self, "_lanes", None)
+        if st is None or st["B"] != B:
+            d = w.cfg.d_model
+            st = self._lanes = {"B": B, "parity": 0, "sets": [None, None], "staged": None,
+                                "vocode": None, "started": False,
+                                "enc": torch.zeros(2 * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
+                                                   device=dev),
+                                "stage": torch.zeros(B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
+                                                     device=dev)}
+        f = st["parity"]
+        c = 1 - f
+        for x in (ds, es, vs):
+            x.wait_stream(main)
+        record = getattr(self, "side_events", None) is not None
+        if record:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+            ev[0].record(vs)
+            ev[2].record(ds)
+            ev[4].record(es)
+        staged, cont = st["staged"], st["sets"][c]
+        # decoder lane, first: batch i-1's encoder output out of the staging buffer into its
+        # slot set (the encoder lane overwrites the stage only after this copy)
+        copied = torch.cuda.Event()
+        with torch.cuda.stream(ds):
+            if staged is not None:
+                st["enc"][f * B:(f + 1) * B].copy_(st["stage"])
+            copied.record(ds)
+        n_dec = min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "0"))) if pcm is not None else 0
+
+        def yin(u0, u1):
+            try:
+                return prosody_launch(pcm, offsets[u0:u1 + 1], lengths[u0:u1], CAPTURE_RATE, 512,
+                                      max_blocks=0)
+            except Exception:  # engine.py:520-525
+                return None
+        # encoder lane: batch i
+        with torch.cuda.stream(es):
+            es.wait_event(copied)
+            if pcm is not None:
+                mel = w.logmel(pcm, offsets, B, 3)
+                st["stage"].copy_(w.encode(mel))
+            if record:
+                ev[5].record(es)
+        # decoder lane: fresh rows (set f) start at 0, the continuing set at S; a set with no
+        # batch runs as continuing rows over the finished state it holds (output unread)
+        dec = None
+        if staged is not None or cont is not None:
+            started = st["started"]
+            offs = [0] * (2 * B)
+            for k in range(2 * B):
+                if k // B == f:
+                    offs[k] = 0 if staged is not None or not started else L - S
+                else:
+                    offs[k] = S if cont is not None else (L - S if started else 0)
+            with torch.cuda.stream(ds):
+                dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
+                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+                                  cu_count=self._dec_s.n_cus)
+            st["started"] = True
+        pres = None
+        with torch.cuda.stream(ds):
+            if n_dec > 0:
+                pres = yin(0, n_dec)
+            if record:
+                ev[3].record(ds)
+        # vocoder lane: the batch the host finished at the end of the previous call
+        res_prev = st["vocode"]
+        st["vocode"] = None
+        wav = pcm16 = None
+        with torch.cuda.stream(vs):
+            if res_prev is not None:
+                wav, pcm16, _ = self.decode(res_prev.packets, frames)
+            if pcm is not None:
+                rest = yin(n_dec, B)
+                pres = (pres, rest) if n_dec > 0 else rest
+            if record:
+                ev[1].record(vs)
+        if record:
+            self.side_events.append(ev)
+        # host: batch i-2 is complete once the decoder lane is; finish it while the vocoder
+        # lane runs (its YIN ran two calls ago)
+        st["sets"][f] = staged
+        if cont is not None:
+            main.wait_stream(ds)
+            sl = slice(c * B, (c + 1) * B)
+            from .whisper import DecodeOut
+            part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
+                             dec.no_speech_prob[sl], dec.prompt_lens[sl])
+            st["vocode"] = self._finish(part, cont["pres"], B, cont["mode"], cont["override"],
+                                        cont["timestamp"])
+        st["sets"][c] = None
+        st["parity"] = c
+        st["staged"] = (None if pcm is None else {"pres": pres, "B": B, "mode": mode,
+                                                  "override": override, "timestamp": timestamp})
+        for x in (ds, es, vs):
+            main.wait_stream(x)
+        return res_prev, wav, pcm16
+
+    def flush_pipelined(self, frames):
+        """Drain the three-lane pipeline: list of (EncodeResult, wav, pcm16) for the batches
+        still in it, in order."""
+        out = []
+        st = getattr(self, "_lanes", None)
+        if st is None:
+            return out
+        while (st["staged"] is not None or st["vocode"] is not None
+               or any(x is not None for x in st["sets"])):
+            r = self.step_pipelined(None, None, [0] * st["B"], frames,
+                                    *(self._lane_key[1:] if getattr(self, "_lane_key", None) else ()))
+            if r[0] is not None:
+                out.append(r)
+        self._lanes = None
         return out
 
     def flush(self, frames):

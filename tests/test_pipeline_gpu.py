@@ -139,6 +139,43 @@ def test_staggered_step_matches_sequential(gpu):
         assert torch.equal(pcm16, seq[i][2])
 
 
+def test_pipelined_step_matches_sequential(gpu):
+    """The three-lane serving step (step_pipelined: encoder of batch i on its own CU lane,
+    the continuous-batch decoder of batches i-1 / i-2 and the vocoder of batch i-3 beside
+    it) produces, per batch and three steps later, the same packets, tokens and waveforms
+    as the back-to-back step of that batch alone; flush_pipelined drains the rest."""
+    pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,))
+    batches = []
+    for i in range(4):
+        utts = [synth_speech(900 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]
+        lengths = [len(u) for u in utts]
+        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+        pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+        batches.append((pcm, offs, lengths))
+    frames = 16
+    seq = []
+    for pcm, offs, lengths in batches:
+        enc = pipe.encode(pcm, offs, lengths, timestamp=5.0)
+        wav, pcm16, _ = pipe.decode(enc.packets, frames)
+        seq.append((enc.packets, wav, pcm16, enc.tokens.cpu()))
+    outs = [pipe.step_pipelined(pcm, offs, lengths, frames, 16, 4, timestamp=5.0)
+            for pcm, offs, lengths in batches]
+    assert all(o == (None, None, None) for o in outs[:3])
+    done = [outs[3]] + pipe.flush_pipelined(frames)
+    assert len(done) == 4
+    for i, (res, wav, pcm16) in enumerate(done):
+        assert res.packets == seq[i][0], i
+        n = res.n_tokens.cpu()
+        for j in range(len(n)):
+            k = 1 + int(n[j])
+            assert torch.equal(res.tokens.cpu()[j, :k], seq[i][3][j, :k])
+        if seq[i][1] is None:
+            assert wav is None
+            continue
+        torch.testing.assert_close(wav, seq[i][1], rtol=0, atol=0)
+        assert torch.equal(pcm16, seq[i][2])
+
+
 def test_pipeline_fallback_matches_seek_loop(gpu):
     """The batched pipeline with faster-whisper's fallback (temperatures 0 ... 1.0, best_of
     5: every window of the seeded synthetic model fails at T = 0) settles each utterance

@@ -4,7 +4,7 @@
 set -o pipefail
 out=gpurun_out/stag_sweep
 mkdir -p $out
-for cfg in "16 0" "16 16" "16 32" "14 0" "14 16" "12 0"; do
+for cfg in "16 16" "16 32" "14 0" "14 16" "12 0"; do
   set -- $cfg
   ov=$1; yd=$2; tag=ov${ov}_yd${yd}
   JANUS_YIN_DEC_UTTS=$yd timeout -k 10 300 python3 -u bench.py --stagger 1 --overlap $ov --steps 3 --warmup 1 \
