@@ -19,8 +19,6 @@
 //
 // Accumulation order: one fp32 accumulator per output, k-steps of 32 in order — the same
 // MFMA sequence per output as gemm_nt_kernel (gemm.hip), so the two are bit-identical.
-#include <cstdlib>
-
 #include "mfma.h"
 #include "kernels.h"
 
@@ -48,14 +46,73 @@ __device__ __forceinline__ void glds_rows8(const _Float16* __restrict__ src, int
   __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)lds_piece, 16, 0, 0);
 }
 
-// epilogue, two passes of 64 rows per wave through the wave's own LDS image (the staging
-// LDS is free by then)
 template <int EPI>
-__device__ __forceinline__ void gemm_big_epilogue(const GemmArgs& p, f32x4 (&acc)[kWMT][kWNT],
-                                                  unsigned char* smem_raw, int row0, int col0,
-                                                  int wm, int wn, int lane, int wid) {
-  const int M = p.M;
-  const int fr = lane & 15;
+__global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int row0 = bm * kBM, col0 = bn * kBN;
+  const int lane = threadIdx.x & 63, wid = wave_id();
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // stage k-tile kt into buffer b: wave w DMAs rows [32w, 32w + 32) of the A tile and of
+  // the B tile, four 8-row pieces each
+  auto stage = [&](int kt, int b) {
+    _Float16* sA = smem + b * kStageHalves;
+    _Float16* sB = sA + kBM * kBK;
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wid * 32 + i * 8;
+      glds_rows8(p.A, p.lda, row0 + rl, rl, M - 1, k0, sA + rl * kBK, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wid * 32 + i * 8;
+      glds_rows8(p.W, p.ldw, col0 + rl, rl, N - 1, k0, sB + rl * kBK, lane);
+    }
+  };
+
+  f32x4 acc[kWMT][kWNT];
+#pragma unroll
+  for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+    for (int n = 0; n < kWNT; ++n) acc[m][n] = zero_f32x4();
+
+  // per-lane fragment offsets (halves): row lane & 15 of each 16-row tile, swizzled chunk
+  const int fr = lane & 15, sw = fr >> 1;
+  const int a_off = (wm * 128 + fr) * kBK, b_off = kBM * kBK + (wn * 64 + fr) * kBK;
+
+  const int nk = K / kBK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const _Float16* buf = smem + cur * kStageHalves;
+#pragma unroll
+    for (int s = 0; s < kBK / 32; ++s) {
+      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
+      half8 a[kWMT], b[kWNT];
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n) b[n] = *reinterpret_cast<const half8*>(buf + b_off + n * 16 * kBK + ch);
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m) a[m] = *reinterpret_cast<const half8*>(buf + a_off + m * 16 * kBK + ch);
+#pragma unroll
+      for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+        for (int n = 0; n < kWNT; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue, two passes of 64 rows per wave through the wave's own LDS image
   float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
   const int er = lane >> 3, ec = (lane & 7) * 8;           // 8 rows x 8 lanes per pass step
   const int gcol = col0 + wn * 64 + ec;
@@ -114,205 +171,6 @@ __device__ __forceinline__ void gemm_big_epilogue(const GemmArgs& p, f32x4 (&acc
   }
 }
 
-// ROT (diagnostic, JANUS_GEMM_BIG=rot): block b walks its k-tiles starting at b % nk, so the
-// blocks in flight stage different k-column bands of A / W at the same time (probes L2 channel
-// camping; changes the fp32 accumulation order, so not bit-identical to gemm_nt_kernel)
-template <int EPI, bool ROT = false>
-__global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
-  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
-
-  const int M = p.M, N = p.N, K = p.K;
-  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
-  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
-  const int bm = bid / nbn, bn = bid % nbn;
-  const int row0 = bm * kBM, col0 = bn * kBN;
-  const int lane = threadIdx.x & 63, wid = wave_id();
-  const int wm = wid >> 2, wn = wid & 3;
-
-  // stage k-tile kt into buffer b: wave w DMAs rows [32w, 32w + 32) of the A tile and of
-  // the B tile, four 8-row pieces each
-  auto stage = [&](int kt, int b) {
-    _Float16* sA = smem + b * kStageHalves;
-    _Float16* sB = sA + kBM * kBK;
-    const int k0 = (ROT ? (kt + bid) % (K / kBK) : kt) * kBK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = wid * 32 + i * 8;
-      glds_rows8(p.A, p.lda, row0 + rl, rl, M - 1, k0, sA + rl * kBK, lane);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = wid * 32 + i * 8;
-      glds_rows8(p.W, p.ldw, col0 + rl, rl, N - 1, k0, sB + rl * kBK, lane);
-    }
-  };
-
-  f32x4 acc[kWMT][kWNT];
-#pragma unroll
-  for (int m = 0; m < kWMT; ++m)
-#pragma unroll
-    for (int n = 0; n < kWNT; ++n) acc[m][n] = zero_f32x4();
-
-  // per-lane fragment offsets (halves): row lane & 15 of each 16-row tile, swizzled chunk
-  const int fr = lane & 15, sw = fr >> 1;
-  const int a_off = (wm * 128 + fr) * kBK, b_off = kBM * kBK + (wn * 64 + fr) * kBK;
-
-  const int nk = K / kBK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const _Float16* buf = smem + cur * kStageHalves;
-#pragma unroll
-    for (int s = 0; s < kBK / 32; ++s) {
-      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
-      half8 a[kWMT], b[kWNT];
-#pragma unroll
-      for (int n = 0; n < kWNT; ++n) b[n] = *reinterpret_cast<const half8*>(buf + b_off + n * 16 * kBK + ch);
-#pragma unroll
-      for (int m = 0; m < kWMT; ++m) a[m] = *reinterpret_cast<const half8*>(buf + a_off + m * 16 * kBK + ch);
-#pragma unroll
-      for (int m = 0; m < kWMT; ++m)
-#pragma unroll
-        for (int n = 0; n < kWNT; ++n) acc[m][n] = mfma16(a[m], b[n], acc[m][n]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  gemm_big_epilogue<EPI>(p, acc, smem_raw, row0, col0, wm, wn, lane, wid);
-}
-
-// Ping-pong variant (JANUS_GEMM_BIG=pp): the same tile, fragments, MFMA order and epilogue,
-// but the two wave groups (wm = 0 / 1, one wave of each per SIMD) run half a k-tile apart:
-// between two consecutive barriers one group reads its fragments of a k-tile out of LDS (and
-// issues its half of the next k-tile's DMA) while the other runs its 64 MFMAs, so the LDS
-// reads and the matrix pipe overlap instead of every wave waiting on LDS at the same time.
-// Barrier slots (group 1 enters one slot late, group 0 leaves one slot late):
-//   slot 2t   : g0 reads k-tile t, DMAs A of k-tile t+1 | g1 MFMAs k-tile t-1, DMAs B of t+1
-//   slot 2t+1 : g0 MFMAs k-tile t                        | g1 reads k-tile t
-// k-tile t+1's DMA (into the buffer k-tile t-1 used, whose reads retired by slot 2t-1's end)
-// is waited (vmcnt(0)) by the issuing waves before slot 2t+1's closing barrier and read from
-// slot 2t+2 on. Each read slot ends with lgkmcnt(0) so the buffer is free for the DMA two
-// slots later.
-__device__ __forceinline__ void pp_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// a buffer descriptor from wave-uniform inputs, made provably uniform (readfirstlane), so the
-// compiler keeps it in SGPRs instead of wrapping the load in a waterfall loop
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const _Float16* base, int bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
-                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(kThreads, 1) void gemm_big_pp_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
-  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
-
-  const int M = p.M, N = p.N, K = p.K;
-  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
-  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
-  const int bm = bid / nbn, bn = bid % nbn;
-  const int row0 = bm * kBM, col0 = bn * kBN;
-  const int lane = threadIdx.x & 63, wid = wave_id();
-  const int wm = wid >> 2, wn = wid & 3;
-
-  // group 0 DMAs the A tile, group 1 the B tile: wave wn of the group rows [64 wn, 64 wn + 64),
-  // eight 8-row pieces
-  // DMA through buffer descriptors (buffer_load ... lds), one per 8-row piece (SGPRs: base
-  // at the piece's first row, range = the piece's rows that exist), a 32-bit per-lane voffset
-  // (row within the piece, swizzled chunk: two variants, since piece i's rows r satisfy
-  // ((r >> 1) & 7) = 4 (i & 1) + (lane >> 4)) and the k-tile in soffset: four VGPRs of
-  // addressing in all. A rows past M are out of their piece's range and read as zero.
-  const int lr8 = lane >> 3;
-  const uint32_t c0 = 16u * ((lane & 7) ^ ((lr8 >> 1) & 7));
-  const uint32_t c1 = 16u * ((lane & 7) ^ (((lr8 >> 1) + 4) & 7));
-  const uint32_t va0 = (uint32_t)(lr8 * p.lda) * 2u + c0, va1 = (uint32_t)(lr8 * p.lda) * 2u + c1;
-  const uint32_t vw0 = (uint32_t)(lr8 * p.ldw) * 2u + c0, vw1 = (uint32_t)(lr8 * p.ldw) * 2u + c1;
-  typedef __attribute__((address_space(3))) void lds_void;
-  auto stage_a = [&](int kt) {
-    _Float16* sA = smem + (kt & 1) * kStageHalves;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rl = wn * 64 + i * 8;
-      const int rows = max(0, min(8, M - row0 - rl));
-      const __amdgpu_buffer_rsrc_t r = uniform_rsrc(p.A + (int64_t)(row0 + rl) * p.lda, rows * p.lda * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(sA + rl * kBK), 16, (i & 1) ? va1 : va0,
-                                               kt * kBK * 2, 0, 0);
-    }
-  };
-  auto stage_b = [&](int kt) {
-    _Float16* sB = smem + (kt & 1) * kStageHalves + kBM * kBK;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rl = wn * 64 + i * 8;
-      const __amdgpu_buffer_rsrc_t r = uniform_rsrc(p.W + (int64_t)(col0 + rl) * p.ldw, 8 * p.ldw * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(sB + rl * kBK), 16, (i & 1) ? vw1 : vw0,
-                                               kt * kBK * 2, 0, 0);
-    }
-  };
-
-  f32x4 acc[kWMT][kWNT];
-#pragma unroll
-  for (int m = 0; m < kWMT; ++m)
-#pragma unroll
-    for (int n = 0; n < kWNT; ++n) acc[m][n] = zero_f32x4();
-
-  const int fr = lane & 15, sw = fr >> 1;
-  const int a_off = (wm * 128 + fr) * kBK, b_off = kBM * kBK + (wn * 64 + fr) * kBK;
-  const int nk = K / kBK;
-
-  if (wm == 0) stage_a(0); else stage_b(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wm == 1) {
-    if (nk > 1) stage_b(1);
-    pp_barrier();                          // group 1 enters one slot late
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    // read slot
-    if (wm == 0 && kt + 1 < nk) stage_a(kt + 1);
-    const _Float16* buf = smem + (kt & 1) * kStageHalves;
-    half8 a[2][kWMT], b[2][kWNT];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
-#pragma unroll
-      for (int n = 0; n < kWNT; ++n) b[s][n] = *reinterpret_cast<const half8*>(buf + b_off + n * 16 * kBK + ch);
-#pragma unroll
-      for (int m = 0; m < kWMT; ++m) a[s][m] = *reinterpret_cast<const half8*>(buf + a_off + m * 16 * kBK + ch);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-    // MFMA slot
-    if (wm == 1 && kt + 2 < nk) stage_b(kt + 2);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int m = 0; m < kWMT; ++m)
-#pragma unroll
-        for (int n = 0; n < kWNT; ++n) acc[m][n] = mfma16(a[s][m], b[s][n], acc[m][n]);
-    __builtin_amdgcn_s_setprio(0);
-    if (wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-  }
-  if (wm == 0) pp_barrier();               // group 0 leaves one slot late
-  __syncthreads();                         // the epilogue overwrites the staging buffers
-  gemm_big_epilogue<EPI>(p, acc, smem_raw, row0, col0, wm, wn, lane, wid);
-}
-
 bool gemm_big_supported(int epi, const GemmArgs& p) {
   if (!(epi == EPI_F16 || epi == EPI_GELU_F16 || epi == EPI_RESID_F32 || epi == EPI_F32)) return false;
   if (p.M < kBM || p.N % kBN != 0 || p.K % kBK != 0 || p.K < kBK) return false;
@@ -326,27 +184,6 @@ bool gemm_big_supported(int epi, const GemmArgs& p) {
 void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
   const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
-  const char* v = std::getenv("JANUS_GEMM_BIG");   // read per launch: A/B in one process
-  if (v && v[0] == 'r') {
-    switch (epi) {
-      case EPI_F16: gemm_big_kernel<EPI_F16, true><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16, true><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_RESID_F32: gemm_big_kernel<EPI_RESID_F32, true><<<blocks, kThreads, 0, s>>>(p); break;
-      default: gemm_big_kernel<EPI_F32, true><<<blocks, kThreads, 0, s>>>(p); break;
-    }
-    JANUS_LAUNCH_CHECK();
-    return;
-  }
-  if (v && v[0] == 'p') {
-    switch (epi) {
-      case EPI_F16: gemm_big_pp_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_GELU_F16: gemm_big_pp_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_RESID_F32: gemm_big_pp_kernel<EPI_RESID_F32><<<blocks, kThreads, 0, s>>>(p); break;
-      default: gemm_big_pp_kernel<EPI_F32><<<blocks, kThreads, 0, s>>>(p); break;
-    }
-    JANUS_LAUNCH_CHECK();
-    return;
-  }
   switch (epi) {
     case EPI_F16: gemm_big_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
     case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;

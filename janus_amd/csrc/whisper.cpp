@@ -313,9 +313,12 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   }
   const bool pair_ok = shared && xattn_supported(d, H) && H <= 8 && d <= 512 && B <= kSkinnyMaxRows &&
                        std::getenv("JANUS_NO_XABSORB") == nullptr && std::getenv("JANUS_NO_XPAIR") == nullptr;
-  // more than two rows per encoder row (best_of = 5): GROUP blocks of up to 6 rows
-  // (xattn_group_kernel: the window's output read once for all its hypotheses); at most
-  // two: PAIR blocks (xattn_kernel<PAIR>, two blocks per CU)
+  // rows sharing an encoder row (best_of = 5 hypotheses of a window): PAIR blocks
+  // (xattn_kernel<PAIR>, two blocks per CU, the window's output read once per two rows).
+  // GROUP blocks of up to 6 rows (xattn_group_kernel: one read for all hypotheses) are
+  // opt-in, JANUS_XGROUP=1: measured slower in the fallback step (4 810 vs 4 380 ms per
+  // step, two same-box pairs, profiles/r04_lanes_sweep_fallback_ab.json) — one block per
+  // CU with three m-tiles of queries staged through LDS loses more than the reads it saves
   std::vector<int> h_groups;
   int grp_rows = 0;
   if (pair_ok) {
@@ -323,7 +326,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     for (int b = 0; b < B; ++b) grp[rows->enc_index[b]].push_back(b);
     size_t maxg = 0;
     for (auto& g : grp) maxg = std::max(maxg, g.size());
-    if (maxg > 2 && std::getenv("JANUS_NO_XGROUP") == nullptr) {
+    if (maxg > 2 && std::getenv("JANUS_XGROUP") != nullptr) {
       grp_rows = (int)std::min<size_t>(6, maxg);
       for (int e = 0; e < n_enc; ++e)
         for (size_t i = 0; i < grp[e].size(); i += grp_rows) {

@@ -530,6 +530,9 @@ class JanusPipeline:
             ev[2].record(ds)
             ev[4].record(es)
         staged, cont = st["staged"], st["sets"][c]
+        # enqueue order matters: the decoder call can hold the host until its lane has
+        # drained what is queued ahead of it, so the vocoder and encoder lanes are filled
+        # first (measured: the vocoder lane queued behind the decoder call ran serially)
         # decoder lane, first: batch i-1's encoder output out of the staging buffer into its
         # slot set (the encoder lane overwrites the stage only after this copy)
         copied = torch.cuda.Event()
@@ -545,6 +548,19 @@ class JanusPipeline:
                                       max_blocks=0)
             except Exception:  # engine.py:520-525
                 return None
+        # vocoder lane: the batch the host finished at the end of the previous call, then
+        # YIN of batch i (all but the first n_dec utterances)
+        res_prev = st["vocode"]
+        st["vocode"] = None
+        wav = pcm16 = None
+        rest = None
+        with torch.cuda.stream(vs):
+            if res_prev is not None:
+                wav, pcm16, _ = self.decode(res_prev.packets, frames)
+            if pcm is not None:
+                rest = yin(n_dec, B)
+            if record:
+                ev[1].record(vs)
         # encoder lane: batch i
         with torch.cuda.stream(es):
             es.wait_event(copied)
@@ -569,37 +585,26 @@ class JanusPipeline:
                                   xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
                                   cu_count=self._dec_s.n_cus)
             st["started"] = True
-        pres = None
+        pres = rest
         with torch.cuda.stream(ds):
             if n_dec > 0:
-                pres = yin(0, n_dec)
+                pres = (yin(0, n_dec), rest)
             if record:
                 ev[3].record(ds)
-        # vocoder lane: the batch the host finished at the end of the previous call
-        res_prev = st["vocode"]
-        st["vocode"] = None
-        wav = pcm16 = None
-        with torch.cuda.stream(vs):
-            if res_prev is not None:
-                wav, pcm16, _ = self.decode(res_prev.packets, frames)
-            if pcm is not None:
-                rest = yin(n_dec, B)
-                pres = (pres, rest) if n_dec > 0 else rest
-            if record:
-                ev[1].record(vs)
         if record:
             self.side_events.append(ev)
-        # host: batch i-2 is complete once the decoder lane is; finish it while the vocoder
-        # lane runs (its YIN ran two calls ago)
+        # host: batch i-2 is complete once the decoder lane is; finish it on the decoder
+        # lane's stream (its copies then wait for that lane only) while the vocoder lane
+        # runs (its YIN ran two calls ago)
         st["sets"][f] = staged
         if cont is not None:
-            main.wait_stream(ds)
             sl = slice(c * B, (c + 1) * B)
             from .whisper import DecodeOut
             part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
                              dec.no_speech_prob[sl], dec.prompt_lens[sl])
-            st["vocode"] = self._finish(part, cont["pres"], B, cont["mode"], cont["override"],
-                                        cont["timestamp"])
+            with torch.cuda.stream(ds):
+                st["vocode"] = self._finish(part, cont["pres"], B, cont["mode"], cont["override"],
+                                            cont["timestamp"])
         st["sets"][c] = None
         st["parity"] = c
         st["staged"] = (None if pcm is None else {"pres": pres, "B": B, "mode": mode,

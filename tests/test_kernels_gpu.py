@@ -49,13 +49,10 @@ def test_gemm(gpu, M, N, K, epi):
 @pytest.mark.parametrize("M,N,K", [(3000, 1536, 512), (256, 512, 512), (4500, 2048, 512),
                                    (3000, 512, 2048), (257, 256, 64), (300, 256, 128)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
-@pytest.mark.parametrize("variant", ["dbuf", "pp"])
-def test_gemm_big(gpu, monkeypatch, M, N, K, epi, variant):
+def test_gemm_big(gpu, M, N, K, epi):
     """The encoder-size kernel (janus_gemm_f16 with N % 256 == 0, K % 64 == 0 -> gemm_big:
-    256 x 256 tiles, LDS-DMA staging; double-buffered and ping-pong schedules) against an
-    fp64 reference, ragged M included, and bit-identical to the 128 x 128-tile kernel (same
-    k-step order per output)."""
-    monkeypatch.setenv("JANUS_GEMM_BIG", variant)
+    256 x 256 tiles, LDS-DMA staging) against an fp64 reference, ragged M included, and
+    bit-identical to the 128 x 128-tile kernel (same k-step order per output)."""
     g = torch.Generator().manual_seed(M + N * 5 + K + epi)
     A = (torch.rand(M, K, generator=g) * 2 - 1).half()
     W = ((torch.rand(N, K, generator=g) * 2 - 1) / math.sqrt(K)).half()
@@ -81,12 +78,10 @@ def test_gemm_big(gpu, monkeypatch, M, N, K, epi, variant):
 
 
 @pytest.mark.parametrize("N,K,epi", [(1536, 512, 0), (512, 512, 2), (2048, 512, 1), (512, 2048, 2)])
-@pytest.mark.parametrize("variant", ["dbuf", "pp"])
-def test_gemm_big_bench_shapes(gpu, monkeypatch, N, K, epi, variant):
+def test_gemm_big_bench_shapes(gpu, N, K, epi):
     """The bench's encoder projections at M = 64 x 1500 = 96 000 rows (QKV, attention output
     + residual, fc1 + GELU, fc2 + residual): bit-identical to the 128 x 128-tile kernel,
     and a sampled row block against fp64."""
-    monkeypatch.setenv("JANUS_GEMM_BIG", variant)
     M = 96000
     g = torch.Generator(device=gpu).manual_seed(N + K)
     A = (torch.rand(M, K, device=gpu, generator=g) * 2 - 1).half()

@@ -190,14 +190,19 @@ def test_weight_reupload_after_decode(gpu):
 
 @pytest.mark.parametrize("T", [0.0, 0.6])
 @pytest.mark.parametrize("idx", [[0, 0, 0, 0, 0, 1, 1, 2, 2, 2, 2, 2, 1, 0], [0, 0, 1, 2, 2, 1, 0]],
-                         ids=["groups", "pairs"])
-def test_shared_encoder_rows_match_replicated(engine, gpu, T, idx):
+                         ids=["five", "two"])
+@pytest.mark.parametrize("xgroup", ["", "1"], ids=["pairs", "groups"])
+def test_shared_encoder_rows_match_replicated(engine, gpu, monkeypatch, T, idx, xgroup):
     """Decoder rows sharing an encoder output (enc_index: faster-whisper's best_of
-    hypotheses of one window) decode exactly as with a private copy per row: with more than
-    two rows per window the cross-attention reads it once per GROUP of up to 6 rows
-    (xattn_group_kernel), with at most two once per PAIR; including a batch above 64 rows
-    (the skinny GEMMs split the rows over blocks). Tokens, summed log-probabilities and
-    no-speech probabilities bit-identical."""
+    hypotheses of one window) decode exactly as with a private copy per row: the
+    cross-attention reads it once per PAIR of rows (default), or with JANUS_XGROUP=1 and
+    more than two rows per window once per GROUP of up to 6 (xattn_group_kernel);
+    including a batch above 64 rows (the skinny GEMMs split the rows over blocks). Tokens,
+    summed log-probabilities and no-speech probabilities bit-identical."""
+    if xgroup:
+        monkeypatch.setenv("JANUS_XGROUP", xgroup)
+    else:
+        monkeypatch.delenv("JANUS_XGROUP", raising=False)
     eng, _ = engine
     utts = [synth_speech(70 + k, 2.0 + k) for k in range(3)]
     pcm, offs = pack(utts, gpu)
