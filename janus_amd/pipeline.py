@@ -475,8 +475,12 @@ class JanusPipeline:
         key = (str(device), dec_per_xcd, enc_per_xcd)
         if getattr(self, "_lane_key", None) != key:
             n = torch.cuda.get_device_properties(device).multi_processor_count
-            dmask, emask, vmask = nat.group_cu_masks(
-                n, [dec_per_xcd - enc_per_xcd, enc_per_xcd, n // 8 - dec_per_xcd])
+            if enc_per_xcd > 0:
+                dmask, emask, vmask = nat.group_cu_masks(
+                    n, [dec_per_xcd - enc_per_xcd, enc_per_xcd, n // 8 - dec_per_xcd])
+            else:   # 0: the encoder shares the decoder's CUs on a stream of its own
+                dmask, vmask = nat.split_cu_masks(n, dec_per_xcd)
+                emask = dmask
             self._dec_s = nat.MaskedStream(dmask, device)
             self._enc_s = nat.MaskedStream(emask, device)
             self._voc_s = nat.MaskedStream(vmask, device)
@@ -490,7 +494,9 @@ class JanusPipeline:
         """The staggered serving step with the encoder moved OFF the critical path: three
         CU-disjoint lanes run side by side for the whole step —
           encoder lane (``enc_per_xcd`` CUs of each XCD, carved out of the decoder's
-            ``dec_per_xcd``): mel + encoder of batch i into a staging buffer;
+            ``dec_per_xcd``; 0: a stream of its own on the decoder's CUs, filling the
+            latency-bound decoder's idle issue slots): mel + encoder of batch i into a
+            staging buffer;
           decoder lane (the other dec_per_xcd - enc_per_xcd): ONE continuous-batch decode
             call of batch i-1 (fresh, positions 0 .. S-1, its encoder output copied out of
             the staging buffer first) and batch i-2 (continuing, positions S .. 2S-1);
