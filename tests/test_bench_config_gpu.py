@@ -1,8 +1,9 @@
 """Parity at the benchmark's own size (VERDICT r2 "next" #1): the bench's workload —
 JanusPipeline("base.en") on 64 x 30 s utterances, seeds 4000 + i (bench.py), run through
-the overlapped serving step exactly as bench.py times it (encoder on the whole GPU at
-M = 64 x 1500 rows and 64 x 8 attention heads; the greedy decoder at B = 64 on its 16
-CUs per XCD; the vocoder on 64 x 2584 frames on the other half) — compared row by row
+the staggered serving step exactly as bench.py times it (encoder on the whole GPU at
+M = 64 x 1500 rows and 64 x 8 attention heads; the greedy decoder as a continuous batch of
+2 x 64 rows on its 16 CUs per XCD, 224 positions per call; YIN of 40 utterances after it;
+the vocoder on 64 x 2584 frames on the other half) — compared row by row
 with the oracle, as engine.py:510-552 would produce them one utterance at a time:
 
 * rows {0, 21, 42, 63}: encoder output within 1e-3 relative RMS of the fp32 oracle
@@ -47,11 +48,14 @@ def test_bench_workload_rows_match_oracle(gpu):
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
     # the bench's headline setting: T = 0, gates reported (bench.py without --fallback)
     pipe = JanusPipeline("base.en", max_length=448, temperatures=(0.0,))
-    pipe.keep_encoder_output = True
-    # the bench's step: the batch enters the overlapped pipeline, flush renders it
-    assert pipe.step_overlapped(pcm, offs, lengths, FRAMES, 16, timestamp=TS) == (None, None, None)
-    enc_gpu = pipe.last_encoder_output.float().cpu()
-    res, wav, pcm16 = pipe.flush(FRAMES)
+    # the bench's step (bench.py --stagger 1, the default): the batch enters the staggered
+    # pipeline (its encoder output lands in slot set 0, the decoder runs its first half
+    # beside an empty set), flush_staggered runs the second half and renders it
+    assert pipe.step_staggered(pcm, offs, lengths, FRAMES, 16, timestamp=TS) == (None, None, None)
+    enc_gpu = pipe._stag["enc"][:B].float().cpu()
+    done = pipe.flush_staggered(FRAMES)
+    assert len(done) == 1
+    res, wav, pcm16 = done[0]
     mel = pipe.whisper.logmel(pcm, offs, B, 3)
     torch.cuda.synchronize()
     assert enc_gpu.shape == (B, 1500, 512) and wav.shape == (B, FRAMES * 512)
