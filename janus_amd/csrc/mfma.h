@@ -86,12 +86,14 @@ __device__ __forceinline__ uint4 ld_act(const _Float16* p) {  // tile staging
 // loaded with the default policy so the neighbour (same XCD: tile_remap) finds it in L2;
 // rows only this tile reads stay non-temporal. `keep` must be wave-uniform (one load form
 // per wave, no exec-masked pair). JANUS_HALO_NT: every staging load non-temporal (r03).
-// JANUS_STAGE_PLAIN (A/B build): the callers keep EVERY staged row (the C = 64 / 32 units'
-// epilogues re-read their body rows as the residual).
-#ifdef JANUS_STAGE_PLAIN
-#define JANUS_STAGE_KEEP_ALL 1
-#else
+// Default since r04 (staggered step): the C = 64 / 32 callers keep EVERY staged row (their
+// epilogues re-read the body rows as the residual): traffic 1.26 / 1.36x -> 1.00 / 1.00x of
+// the algorithmic bytes, step level-to-better in two same-box pairs (266.2 / 266.9 vs 266.6
+// / 267.7 ms). JANUS_STAGE_HALO_ONLY (A/B build): only the halo rows kept, as r04 v2.
+#ifdef JANUS_STAGE_HALO_ONLY
 #define JANUS_STAGE_KEEP_ALL 0
+#else
+#define JANUS_STAGE_KEEP_ALL 1
 #endif
 __device__ __forceinline__ uint4 ld_act_halo(const _Float16* p, bool keep) {
 #if defined(JANUS_ACT_NT_LD) && !defined(JANUS_HALO_NT)

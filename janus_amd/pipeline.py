@@ -430,8 +430,11 @@ class JanusPipeline:
         dec = None
         if pcm is not None or cont is not None:
             with torch.cuda.stream(ds):
+                # cross-attention at 2 key splits: with 2 x 64 rows the grid fills the
+                # decoder's CUs without the split (4: decoder side 252.6-255.3 ms, 2:
+                # 246.7-248.6, 8: 264.7-266.7, one box)
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
-                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "2")),
                                   cu_count=self._dec_s.n_cus)
                 if n_dec > 0:
                     pres = (yin(0, n_dec), pres)

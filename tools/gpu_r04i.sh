@@ -15,4 +15,11 @@ for yd in 36 40 44 48; do
   python3 -c "
 import json; d=json.load(open('$out/yd$yd.json')); print('yd$yd', d['ms_per_step'], d['value'], d['step_ms'], d['side_ms'])"
 done
+for xs in 2 8 4; do
+  JANUS_XATTN_SPLITS=$xs timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --fallback-steps 0 --no-idle-latency \
+    > $out/xs$xs.log 2>&1 || { tail -20 $out/xs$xs.log; exit 1; }
+  tail -1 $out/xs$xs.log > $out/xs$xs.json
+  python3 -c "
+import json; d=json.load(open('$out/xs$xs.json')); print('xsplit$xs', d['ms_per_step'], d['value'], d['step_ms'], d['side_ms'])"
+done
 bash tools/gpu_ab.sh store default libjanus_hip_stplain.so libjanus_hip_wt.so libjanus_hip_stwt.so || exit 1
