@@ -53,7 +53,7 @@ def parse():
                     help="CUs per XCD (of 32) for the greedy decoder in the overlapped serving step "
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     ap.add_argument("--stagger", type=int, default=int(os.environ.get("JANUS_STAGGER", "1")),
                     help="1: continuous batching in the decoder (JanusPipeline.step_staggered): "
                          "each step's decoder call advances batch i from position 0 and batch "
