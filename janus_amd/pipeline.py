@@ -307,10 +307,23 @@ class JanusPipeline:
             dec_kw = dict(xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
                           cu_count=self._dec_s.n_cus)
             dec = w.decode_ex(enc, max_length=self.max_length, **dec_kw)
-            # the fallback's sampled re-decodes on the decoder's CUs (host-driven: reads
-            # the T = 0 gates); the settled texts go to _finish
-            dec.settled = (_texts_and_gates(w, dec, self.temperatures, enc, **dec_kw)
-                           if len(self.temperatures) > 1 else None)
+            # the fallback's sampled re-decodes (host-driven: reads the T = 0 gates); the
+            # settled texts go to _finish. They run on the WHOLE GPU (the high-priority
+            # stream, after the vocoder side and the T = 0 decode): the vocoder side ends
+            # with the T = 0 decode anyway, and the 320-row cross-attention streams scale
+            # with the CUs (JANUS_FB_FULL=0: on the decoder's CUs, as the T = 0 decode)
+            dec.settled = None
+            if len(self.temperatures) > 1:
+                if os.environ.get("JANUS_FB_FULL", "1") != "0":
+                    hi.wait_stream(ds)
+                    hi.wait_stream(vs)
+                    fb_kw = dict(xattn_splits=int(os.environ.get("JANUS_FB_XSPLITS", "4")),
+                                 cu_count=torch.cuda.get_device_properties(pcm.device).multi_processor_count)
+                    with torch.cuda.stream(hi):
+                        dec.settled = _texts_and_gates(w, dec, self.temperatures, enc, **fb_kw)
+                    ds.wait_stream(hi)
+                else:
+                    dec.settled = _texts_and_gates(w, dec, self.temperatures, enc, **dec_kw)
             if n_dec > 0:
                 pres = (yin(0, n_dec), pres)
         if record:
