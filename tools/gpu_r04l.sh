@@ -6,8 +6,7 @@ root=$(pwd)
 out=$root/gpurun_out/r04l
 mkdir -p $out
 export JANUS_YIN_DEC_UTTS=0
-for knob in base JANUS_LOGITS_BLOCKS=256 JANUS_LOGITS_BLOCKS=64 JANUS_SKINNY_NO_K1=1 JANUS_SKINNY_NO_NCT2=1 \
-            JANUS_DEC_MSPLIT_N=2048 JANUS_NO_CVP=1 JANUS_XATTN_SPLITS=1 base2; do
+for knob in ${KNOBS:-base}; do
   tag=${knob//=/_}
   if [ "${knob:0:4}" = base ]; then envs=""; else envs="$knob"; fi
   env $envs timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --fallback-steps 0 --no-idle-latency \
@@ -16,7 +15,7 @@ for knob in base JANUS_LOGITS_BLOCKS=256 JANUS_LOGITS_BLOCKS=64 JANUS_SKINNY_NO_
   python3 -c "
 import json; d=json.load(open('$out/$tag.json')); print('$tag', d['ms_per_step'], d['side_ms']['decoder'], d['roofline']['decoder']['us_per_position'])"
 done
-for xs in 8 2; do
+for xs in ${FBXS:-}; do
   JANUS_FB_XSPLITS=$xs timeout -k 10 400 python3 -u bench.py --no-cpu-baseline --steps 1 > $out/fb_xs$xs.log 2>&1 || { tail -20 $out/fb_xs$xs.log; exit 1; }
   tail -1 $out/fb_xs$xs.log > $out/fb_xs$xs.json
   python3 -c "
