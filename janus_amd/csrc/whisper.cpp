@@ -578,12 +578,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const bool rln = B <= 64 && !fused_ln && !ln_fuse && resid_ln_supported(d, d) &&
                    std::getenv("JANUS_RESID_LN") != nullptr;
   const bool rln2 = rln && !lnp2, rln3 = rln && !lnp3;
-  // cross-attention split merge + per-head value projection in one launch
-  // (xattn_combine_vproj_kernel, bit-identical; JANUS_NO_CVP restores the two launches)
   // the split merge fused into the per-head value projection (one launch) up to 64 rows;
   // above (the staggered 2 x 64 rows) the merge in the cross-attention's last split block
   // and a block-diagonal skinny projection measured faster (decoder side -1.5 / -2.9 ms
   // per step on two boxes, profiles/r04_decoder_knobs.json); bit-identical either way
+  // (xattn_combine_vproj_kernel; JANUS_NO_CVP / JANUS_CVP force either form)
   const bool cvp = xattn_cvp_supported(d, H) && xsplit <= 16 && std::getenv("JANUS_NO_CVP") == nullptr &&
                    (B <= 64 || ngroups > 0 || std::getenv("JANUS_CVP") != nullptr);
   Z.d_lncnt.ensure(sizeof(int) * 64);  // one arrival counter per 16-row block (JANUS_LN_FUSE)
