@@ -53,3 +53,19 @@ def test_split_cu_masks_balanced_per_xcd():
         assert not set(bits_a) & set(bits_b)
         for x in range(8):
             assert sum(1 for i in bits_a if i % 8 == x) == dec
+
+
+def test_group_cu_masks_three_lanes():
+    """The three-lane step's masks (decoder, encoder, vocoder): disjoint, balanced per XCD,
+    cover exactly the requested counts; two groups reproduce split_cu_masks."""
+    for per in ([12, 4, 16], [14, 2, 16], [16, 4, 12], [8, 8, 8]):
+        masks = _native.group_cu_masks(256, per)
+        seen = set()
+        for m, k in zip(masks, per):
+            bits = [i for i in range(256) if m[i // 32] >> (i % 32) & 1]
+            assert len(bits) == 8 * k and not seen & set(bits)
+            seen |= set(bits)
+            for x in range(8):
+                assert sum(1 for i in bits if i % 8 == x) == k
+    for dec in (4, 16, 28):
+        assert _native.group_cu_masks(256, [dec, 32 - dec]) == list(_native.split_cu_masks(256, dec))
