@@ -599,6 +599,7 @@ def main():
         dist.barrier()
     t_end = time.perf_counter()
     pipe.vocoder.set_timing(False)
+    yin_dec_utts = (getattr(pipe, "_stag", None) or {}).get("n_dec") if args.stagger == 1 else None
     sides = [(e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in (pipe.side_events or [])]
     enc_side = [e[4].elapsed_time(e[5]) for e in (pipe.side_events or []) if len(e) >= 6]
     pipe.side_events = None
@@ -715,6 +716,9 @@ def main():
                             **({"encoder": [round(x, 1) for x in enc_side]} if enc_side else {}))
             if sides else None,
             "enc_cus": args.enc_cus if args.stagger == 2 else None,
+            # staggered step: utterances whose YIN ran on the decoder side in the last timed
+            # step (self-balancing split, JanusPipeline._yin_split)
+            "yin_dec_utts": yin_dec_utts,
             "overlap": args.overlap,
             "step_ms": [round(t * 1000.0, 1) for t in times],
             "tokens_per_utt": round(float(np.mean(tok_counts)), 1),

@@ -403,18 +403,17 @@ class JanusPipeline:
         vs.wait_stream(hi)
         ds.wait_stream(hi)
         record = getattr(self, "side_events", None) is not None
-        if record:
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            ev[0].record(vs)
-            ev[2].record(ds)
+        # side events every step: the YIN split below reads the previous step's
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(vs)
+        ev[2].record(ds)
         wav = pcm16 = None
         pres = None
-        # YIN of the first JANUS_YIN_DEC_UTTS utterances (default 5B/8) runs on the decoder
-        # side after the decoder call, the rest behind the vocoder: with two batches per
-        # decoder call that side has the slack (64 x 30 s, one box: 0 / 24 / 32 / 40 of 64
-        # -> sides 275 / 242, 260 / 246, 256 / 249, 253 / 253 ms; step 287 -> 264 ms)
-        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", str(5 * B // 8))))
-                 if pcm is not None else 0)
+        # YIN of the first n_dec utterances runs on the decoder side after the decoder call,
+        # the rest behind the vocoder: with two batches per decoder call that side has the
+        # slack (64 x 30 s, one box: 0 / 24 / 32 / 40 of 64 -> sides 275 / 242, 260 / 246,
+        # 256 / 249, 253 / 253 ms; step 287 -> 264 ms)
+        n_dec = self._yin_split(st, B) if pcm is not None else 0
 
         def yin(u0, u1):
             try:
@@ -453,9 +452,12 @@ class JanusPipeline:
                     pres = (yin(0, n_dec), pres)
         st["sets"][f] = (None if pcm is None else {"pres": pres, "B": B, "mode": mode,
                                                   "override": override, "timestamp": timestamp})
+        ev[3].record(ds)
         if record:
-            ev[3].record(ds)
             self.side_events.append(ev)
+        # only full steps (a vocoder batch, both row sets decoding) steer the YIN split
+        if pcm is not None and res_prev is not None and cont is not None:
+            st["prev_ev"] = ev
         st["started"] = True
         main.wait_stream(ds)
         main.wait_stream(vs)
@@ -468,6 +470,28 @@ class JanusPipeline:
         st["sets"][c] = None
         st["parity"] = c
         return res_prev, wav, pcm16
+
+    # YIN of one 30 s utterance on a 16-CU-per-XCD partition (26 ms for 64, either side)
+    YIN_MS_PER_UTT = 0.4
+
+    def _yin_split(self, st, B):
+        """Utterances whose YIN runs on the decoder side in the staggered step. Fixed by
+        JANUS_YIN_DEC_UTTS; otherwise self-balancing: starts at 5B/8 and moves by the
+        previous step's side-time gap (vocoder side minus decoder side, HIP events on the
+        two CU-masked streams) over twice the per-utterance YIN time, at most 8 per step,
+        so the two partitions finish together whatever the box's vocoder / decoder speed
+        ratio (measured from box to box: vocoder side 253-265 ms at the same split)."""
+        env = os.environ.get("JANUS_YIN_DEC_UTTS")
+        if env is not None:
+            return max(0, min(B - 1, int(env)))
+        n = st.get("n_dec", 5 * B // 8)
+        prev = st.get("prev_ev")
+        if prev is not None and prev[1].query() and prev[3].query():
+            gap = prev[0].elapsed_time(prev[1]) - prev[2].elapsed_time(prev[3])
+            move = int(round(gap / (2.0 * self.YIN_MS_PER_UTT)))
+            n = max(0, min(B - 1, n + max(-8, min(8, move))))
+        st["n_dec"] = n
+        return n
 
     def flush_staggered(self, frames):
         """Drain the staggered pipeline: finish the batch still in the decoder and render
