@@ -426,8 +426,7 @@ class JanusPipeline:
                 wav, pcm16, _ = self.decode(res_prev.packets, frames)
             if pcm is not None:
                 pres = yin(n_dec, B)
-            if record:
-                ev[1].record(vs)
+            ev[1].record(vs)
         cont = st["sets"][c]
         # fresh rows start at 0, the continuing set at S. The first call starts every slot
         # fresh (no slot holds state yet); later, a slot set without a batch runs as
