@@ -557,9 +557,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // vs 47.3 + 5.1 — but the absorbed query projection 16.1 vs 9.2 + 5.1 us: its 256
   // 64-row blocks would each normalise all 64 rows. Beside the vocoder (overlapped
   // step, decoder side): mask 0 303.5-308.7, 13 305.1-306.8, 9 304.0-304.2, 5 306.6-306.9
-  // ms — within the box's noise; 9 (LN1 + final) is the default.
+  // ms — within the box's noise; 9 (LN1 + final) is the default up to 64 rows. Above (the
+  // staggered 2 x 64 rows) every LayerNorm is its own launch: decoder side 230-234 ms with
+  // mask 0 against 235-241 (9), 245-249 (13), 265-269 (15) on one box
+  // (profiles/r04_decoder_knobs.json): each prologue normalises its block's rows again.
   const int ln_pro_mask = (B <= kSkinnyMaxRows && d <= 512 && !fused_ln && !ln_fuse)
-                              ? (std::getenv("JANUS_LN_PROLOGUE") ? std::atoi(std::getenv("JANUS_LN_PROLOGUE")) : 9)
+                              ? (std::getenv("JANUS_LN_PROLOGUE") ? std::atoi(std::getenv("JANUS_LN_PROLOGUE"))
+                                                                  : (B <= 64 ? 9 : 0))
                               : 0;
   // the embedding kernel owns whole rows (one block per utterance): it also writes the
   // first layer's LayerNorm of its row, one launch fewer per position
