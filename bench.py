@@ -573,7 +573,12 @@ def main():
 
     # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
-    prime = (1 + int(args.stagger)) if args.overlap > 0 else 0
+    # decoder slot sets (staggered: JANUS_STAGGER_SETS batches per decoder call) and the
+    # pipeline depth (calls before the first batch comes out)
+    sets = (max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2"))) if args.stagger == 1
+            else 2 if args.stagger == 2 else 1)
+    depth = (sets if args.stagger == 1 else 3 if args.stagger == 2 else 1) if args.overlap > 0 else 0
+    prime = depth
     for _ in range(args.warmup + prime):
         enc = step()
     torch.cuda.synchronize()
@@ -699,14 +704,14 @@ def main():
             "xrt_per_gpu": round(value / world, 2),
             # overlapped: an utterance is encoded in one step and vocoded in the next
             # an utterance's steps: encode + decode, then vocoder (overlapped: 2 steps);
-            # staggered: encode + first half, second half, vocoder (3 steps); pipelined:
-            # encode, first half, second half, vocoder (4 steps)
+            # staggered: encode + the N decode chunks, then the vocoder (N + 1 steps);
+            # pipelined: encode, first half, second half, vocoder (4 steps)
             "p50_latency_ms": round(float(np.median(
-                [sum(times[i:i + 2 + int(args.stagger)])
-                 for i in range(len(times) - 1 - int(args.stagger))]
-                if args.overlap > 0 and len(times) > 1 + int(args.stagger)
+                [sum(times[i:i + depth + 1]) for i in range(len(times) - depth)]
+                if args.overlap > 0 and len(times) > depth
                 else times)) * 1000.0, 2),
             "stagger": int(args.stagger),
+            "stagger_sets": sets if args.stagger else None,
             # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
             "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
             # wall time of the two CU partitions per timed step (HIP events on each side's
@@ -762,11 +767,11 @@ def main():
                 # HBM roofline (algorithmic bytes per position / decoder-side time per
                 # position; launches per position from the captured decode graphs)
                 "decoder": decoder_roofline(
-                    pipe.whisper.cfg, (2 if args.stagger else 1) * B, dec_positions, dec_launches,
+                    pipe.whisper.cfg, sets * B, dec_positions, dec_launches,
                     float(np.mean([b for _, b in sides])) if sides else None,
                     round(1.0 - cu_share - (args.enc_cus * 8 / n_cus if args.stagger == 2 else 0), 4)
                     if args.overlap > 0 else 1.0,
-                    tkv_positions=(2 * dec_positions - 1) if args.stagger else None),
+                    tkv_positions=(sets * dec_positions - 1) if args.stagger else None),
             },
             "cpu_baseline": None,
         }

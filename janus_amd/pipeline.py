@@ -362,41 +362,47 @@ class JanusPipeline:
     # ------------------------------------------- staggered (continuous-batching) step
     def step_staggered(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
                        mode=JanusMode.SEMANTIC_VOICE, override="auto", timestamp=None):
-        """The overlapped serving step with the greedy decoder as a continuous batch of TWO
-        batches at different positions (janus_decode_rows.pos_offset): each call of the
-        decoder advances 2B rows by S = ceil((max_length - 1) / 2) positions — batch i's
-        rows (fresh, positions 0 .. S-1) and batch i-1's (continuing in their slots,
-        positions S .. 2S-1), so every step still completes exactly one batch's decode, but
-        the decoder's latency-bound launches serve twice the rows. Per step: mel + encoder of
-        batch i (whole GPU), then decoder (batch i, batch i-1) on the decoder's CUs beside
-        the vocoder of batch i-2 + YIN of batch i on the vocoder's CUs. Returns (EncodeResult,
-        wav, pcm16) of batch i-2, (None, None, None) for the first two calls;
-        ``flush_staggered`` drains. Greedy (T = 0) only; per-row results are bit-identical to
-        the one-batch decode (rows are independent of their neighbours' positions)."""
+        """The overlapped serving step with the greedy decoder as a continuous batch of N
+        batches at different positions (janus_decode_rows.pos_offset; N =
+        JANUS_STAGGER_SETS, default 2): each call of the decoder advances N·B rows by
+        S = max_length // N positions — batch i's rows fresh (positions 0 .. S-1) and
+        batch i-m's, m = 1 .. N-1, continuing in their slot set (positions mS .. (m+1)S-1),
+        so every step still completes exactly one batch's decode, but the decoder's
+        latency-bound launches serve N times the rows. Per step: mel + encoder of batch i
+        (whole GPU), then the decoder call on the decoder's CUs beside the vocoder of batch
+        i-N + YIN of batch i on the vocoder's CUs. Returns (EncodeResult, wav, pcm16) of
+        batch i-N, (None, None, None) for the first N calls; ``flush_staggered`` drains.
+        Greedy (T = 0) only; per-row results are bit-identical to the one-batch decode
+        (rows are independent of their neighbours' positions)."""
         if tuple(self.temperatures) != (0.0,):
             raise NotImplementedError("staggered decode runs at temperature 0 only")
         B = len(lengths)
         w = self.whisper
         L = self.max_length
-        S = L // 2
         dev = pcm.device if pcm is not None else self.device
         main = torch.cuda.current_stream(dev)
         hi = self._hi_stream(dev)
         ds, vs = self._split_streams(dev, dec_per_xcd)
         st = getattr(self, "_stag", None)
         if st is None or st["B"] != B:
+            n = max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2")))
             d = w.cfg.d_model
-            st = self._stag = {"B": B, "parity": 0, "sets": [None, None], "done": None,
-                               "enc": torch.zeros(2 * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
+            st = self._stag = {"B": B, "n": n, "k": 0, "sets": [None] * n, "done": None,
+                               "enc": torch.zeros(n * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
                                                   device=dev)}
-        f = st["parity"]
-        c = 1 - f
+        n, k = st["n"], st["k"]
+        # S positions per call cover the full decode's L - 1 steps in N calls; the last set's
+        # chunk may overrun by a position (a no-op past the row's end) but not past L
+        S = -(-(L - 1) // n)
+        if n * S > L:
+            raise ValueError(f"JANUS_STAGGER_SETS={n} does not tile max_length {L}")
+        f = k % n   # this call's fresh slot set (its last batch completed in the previous call)
         hi.wait_stream(main)
         with torch.cuda.stream(hi):
             if pcm is not None:
                 mel = w.logmel(pcm, offsets, B, 3)
                 st["enc"][f * B:(f + 1) * B].copy_(w.encode(mel))
-        # batch i-2 (completed by the previous call) on the host while the encoder runs
+        # batch i-N (completed by the previous call) on the host while the encoder runs
         prev = st["done"]
         st["done"] = None
         res_prev = self._finish(*prev) if prev is not None else None
@@ -427,19 +433,23 @@ class JanusPipeline:
             if pcm is not None:
                 pres = yin(n_dec, B)
             ev[1].record(vs)
-        cont = st["sets"][c]
-        # fresh rows start at 0, the continuing set at S. The first call starts every slot
-        # fresh (no slot holds state yet); later, a slot set without a batch runs as
-        # continuing rows over the finished state it holds (its output is not read)
-        if not st.get("started"):
-            offs = [0] * (2 * B)
-        else:
-            offs = [0] * (2 * B)
-            for k in range(2 * B):
-                if k // B == c or pcm is None:
-                    offs[k] = S if k // B == c else L - S
+        # each set's first position: the fresh set 0, a set holding the batch that entered at
+        # call b (k - b) S; the first call starts every set fresh (no set holds state yet);
+        # later a set without a batch runs as continuing rows over the finished state it
+        # holds, at (N-1) S (its output is not read)
+        offs = [0] * (n * B)
+        if st.get("started"):
+            for j in range(n):
+                sj = st["sets"][j]
+                o = 0 if (j == f and pcm is not None) else \
+                    (k - sj["born"]) * S if sj is not None else (n - 1) * S
+                offs[j * B:(j + 1) * B] = [o] * B
+        # the batch that completes in this call: entered N-1 calls ago
+        jc = (k - (n - 1)) % n
+        cont = st["sets"][jc] if (st["sets"][jc] is not None
+                                  and k - st["sets"][jc]["born"] == n - 1) else None
         dec = None
-        if pcm is not None or cont is not None:
+        if pcm is not None or any(x is not None for x in st["sets"]):
             with torch.cuda.stream(ds):
                 # cross-attention at 2 key splits: with 2 x 64 rows the grid fills the
                 # decoder's CUs without the split (4: decoder side 252.6-255.3 ms, 2:
@@ -449,25 +459,26 @@ class JanusPipeline:
                                   cu_count=self._dec_s.n_cus)
                 if n_dec > 0:
                     pres = (yin(0, n_dec), pres)
-        st["sets"][f] = (None if pcm is None else {"pres": pres, "B": B, "mode": mode,
-                                                  "override": override, "timestamp": timestamp})
+            st["started"] = True
+        if pcm is not None:
+            st["sets"][f] = {"pres": pres, "B": B, "mode": mode, "override": override,
+                             "timestamp": timestamp, "born": k}
         ev[3].record(ds)
         if record:
             self.side_events.append(ev)
-        # only full steps (a vocoder batch, both row sets decoding) steer the YIN split
+        # only full steps (a vocoder batch, a batch completing) steer the YIN split
         if pcm is not None and res_prev is not None and cont is not None:
             st["prev_ev"] = ev
-        st["started"] = True
         main.wait_stream(ds)
         main.wait_stream(vs)
         if cont is not None:
-            sl = slice(c * B, (c + 1) * B)
+            sl = slice(jc * B, (jc + 1) * B)
             from .whisper import DecodeOut
             part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
                              dec.no_speech_prob[sl], dec.prompt_lens[sl])
             st["done"] = (part, cont["pres"], B, cont["mode"], cont["override"], cont["timestamp"])
-        st["sets"][c] = None
-        st["parity"] = c
+            st["sets"][jc] = None
+        st["k"] = k + 1
         return res_prev, wav, pcm16
 
     # YIN of one 30 s utterance on a 16-CU-per-XCD partition (26 ms for 64, either side)
@@ -493,14 +504,13 @@ class JanusPipeline:
         return n
 
     def flush_staggered(self, frames):
-        """Drain the staggered pipeline: finish the batch still in the decoder and render
-        the last two batches. Returns a list of (EncodeResult, wav, pcm16)."""
+        """Drain the staggered pipeline: finish the batches still in the decoder and render
+        them. Returns a list of (EncodeResult, wav, pcm16), in order."""
         out = []
         st = getattr(self, "_stag", None)
         if st is None:
             return out
-        dev = st["enc"].device
-        for _ in range(2):
+        while any(x is not None for x in st["sets"]):
             r = self.step_staggered(None, None, [0] * st["B"], frames)
             if r[0] is not None:
                 out.append(r)

@@ -102,11 +102,13 @@ def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
         assert torch.equal(pcm16, seq[i][2])
 
 
-def test_staggered_step_matches_sequential(gpu):
+@pytest.mark.parametrize("sets", ["2", "3", "4"])
+def test_staggered_step_matches_sequential(gpu, monkeypatch, sets):
     """The continuous-batching serving step (step_staggered: the decoder advances batch i's
-    rows from position 0 and batch i-1's from position S in one call, 2B rows) produces,
-    per batch and two steps later, the same packets and waveforms as the back-to-back step
-    of that batch alone; flush_staggered drains the last two."""
+    rows from position 0 and batch i-m's from position mS, m < N, in one call, N·B rows;
+    N = JANUS_STAGGER_SETS) produces, per batch and N steps later, the same packets and
+    waveforms as the back-to-back step of that batch alone; flush_staggered drains."""
+    monkeypatch.setenv("JANUS_STAGGER_SETS", sets)
     pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,))
     batches = []
     for i in range(3):
@@ -123,8 +125,9 @@ def test_staggered_step_matches_sequential(gpu):
         seq.append((enc.packets, wav, pcm16, enc.tokens.cpu()))
     outs = [pipe.step_staggered(pcm, offs, lengths, frames, 16, timestamp=5.0)
             for pcm, offs, lengths in batches]
-    assert outs[0] == (None, None, None) and outs[1] == (None, None, None)
-    done = [outs[2]] + pipe.flush_staggered(frames)
+    n = int(sets)
+    assert all(o == (None, None, None) for o in outs[:n])
+    done = [o for o in outs if o[0] is not None] + pipe.flush_staggered(frames)
     assert len(done) == 3
     for i, (res, wav, pcm16) in enumerate(done):
         assert res.packets == seq[i][0], i
