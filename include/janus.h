@@ -280,8 +280,10 @@ typedef struct {
    * runs positions [pos_offset[b], pos_offset[b] + steps) (steps 0 = max_length - 1). A row
    * with an offset > 0 CONTINUES the previous call's row in the same slot of this context
    * (its tokens, KV cache, counters and rule state are kept; pass its encoder output again);
-   * rows with offset 0 start fresh and must be one contiguous range. Greedy only, no
-   * enc_index; pos_offset + steps <= max_length. NULL = every row fresh. */
+   * rows with offset 0 start fresh and must be one contiguous range. A continuing row's
+   * offset must not exceed the position its previous calls reached (its tokens and KV rows
+   * below the offset must have been written). Greedy only, no enc_index; pos_offset + steps
+   * <= max_length. NULL = every row fresh. */
   const int32_t* pos_offset;
   int steps;
 } janus_decode_rows;

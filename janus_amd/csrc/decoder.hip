@@ -64,6 +64,9 @@ __device__ __forceinline__ void embed_row(const _Float16* __restrict__ tok_emb,
                                           const float* __restrict__ ln_b,
                                           _Float16* __restrict__ ln_out) {
   __shared__ float red[2][4];
+  // defence in depth: a row continued past the tokens it has written (a pos_offset beyond
+  // where the row stands) reads the -1 fill; embed token 0 rather than read before the table
+  tok = tok < 0 ? 0 : tok;
   float v0 = 0.f, v1 = 0.f;
   for (int base = 0; base < d; base += 512) {
     const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece

@@ -435,14 +435,16 @@ class JanusPipeline:
             ev[1].record(vs)
         # each set's first position: the fresh set 0, a set holding the batch that entered at
         # call b (k - b) S; the first call starts every set fresh (no set holds state yet);
-        # later a set without a batch runs as continuing rows over the finished state it
-        # holds, at (N-1) S (its output is not read)
+        # later a set without a batch runs as continuing rows over the state it holds, from
+        # where its rows stand (at most (N-1) S: a finished set re-runs its last chunk), so
+        # every token and KV-cache row it reads was written (its output is not read)
         offs = [0] * (n * B)
+        pos = st.setdefault("pos", [0] * n)
         if st.get("started"):
             for j in range(n):
                 sj = st["sets"][j]
                 o = 0 if (j == f and pcm is not None) else \
-                    (k - sj["born"]) * S if sj is not None else (n - 1) * S
+                    (k - sj["born"]) * S if sj is not None else min(pos[j], (n - 1) * S)
                 offs[j * B:(j + 1) * B] = [o] * B
         # the batch that completes in this call: entered N-1 calls ago
         jc = (k - (n - 1)) % n
@@ -460,6 +462,8 @@ class JanusPipeline:
                 if n_dec > 0:
                     pres = (yin(0, n_dec), pres)
             st["started"] = True
+            for j in range(n):
+                pos[j] = offs[j * B] + S
         if pcm is not None:
             st["sets"][f] = {"pres": pres, "B": B, "mode": mode, "override": override,
                              "timestamp": timestamp, "born": k}
