@@ -84,6 +84,31 @@ def _prosody_stats(parts, B, device):
     return torch.full((B, 3), float("nan"), dtype=torch.float32, device=device)
 
 
+def stagger_plan(sets, pos, started, k, S, fresh):
+    """One staggered decoder call's plan (JanusPipeline.step_staggered), host-only: the
+    first position of every slot set and the set whose batch completes in this call.
+    sets[j]: None or {"born": call index the batch entered}; pos[j]: where set j's rows
+    stand after the previous calls; k: this call's index (fresh set k % N); fresh: a new
+    batch enters. Returns ([offset per set], completing set or None). A set holding a
+    batch continues at (k - born) S; a set without one continues from where its rows stand,
+    at most (N-1) S, so it reads only tokens and KV rows it wrote; before the first call
+    every set starts fresh."""
+    n = len(sets)
+    f = k % n
+    offs = [0] * n
+    if started:
+        for j in range(n):
+            if j == f and fresh:
+                offs[j] = 0
+            elif sets[j] is not None:
+                offs[j] = (k - sets[j]["born"]) * S
+            else:
+                offs[j] = min(pos[j], (n - 1) * S)
+    jc = (k - (n - 1)) % n
+    done = jc if (sets[jc] is not None and k - sets[jc]["born"] == n - 1) else None
+    return offs, done
+
+
 class JanusPipeline:
     def __init__(self, model: str = "base.en", whisper_seed: int = 0, vocoder_seed: int = 0,
                  max_length: int = 448, vocoder_cfg: FireflyConfig = FireflyConfig(),
@@ -438,18 +463,10 @@ class JanusPipeline:
         # later a set without a batch runs as continuing rows over the state it holds, from
         # where its rows stand (at most (N-1) S: a finished set re-runs its last chunk), so
         # every token and KV-cache row it reads was written (its output is not read)
-        offs = [0] * (n * B)
         pos = st.setdefault("pos", [0] * n)
-        if st.get("started"):
-            for j in range(n):
-                sj = st["sets"][j]
-                o = 0 if (j == f and pcm is not None) else \
-                    (k - sj["born"]) * S if sj is not None else min(pos[j], (n - 1) * S)
-                offs[j * B:(j + 1) * B] = [o] * B
-        # the batch that completes in this call: entered N-1 calls ago
-        jc = (k - (n - 1)) % n
-        cont = st["sets"][jc] if (st["sets"][jc] is not None
-                                  and k - st["sets"][jc]["born"] == n - 1) else None
+        set_offs, jc = stagger_plan(st["sets"], pos, bool(st.get("started")), k, S, pcm is not None)
+        offs = [o for o in set_offs for _ in range(B)]
+        cont = st["sets"][jc] if jc is not None else None
         dec = None
         if pcm is not None or any(x is not None for x in st["sets"]):
             with torch.cuda.stream(ds):
@@ -463,7 +480,7 @@ class JanusPipeline:
                     pres = (yin(0, n_dec), pres)
             st["started"] = True
             for j in range(n):
-                pos[j] = offs[j * B] + S
+                pos[j] = set_offs[j] + S
         if pcm is not None:
             st["sets"][f] = {"pres": pres, "B": B, "mode": mode, "override": override,
                              "timestamp": timestamp, "born": k}
