@@ -575,6 +575,9 @@ def main():
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
     # decoder slot sets (staggered: JANUS_STAGGER_SETS batches per decoder call) and the
     # pipeline depth (calls before the first batch comes out)
+    # (the staggered steps are greedy-only: with --fallback the overlapped step runs)
+    if args.fallback:
+        args.stagger = 0
     sets = (max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2"))) if args.stagger == 1
             else 2 if args.stagger == 2 else 1)
     depth = (sets if args.stagger == 1 else 3 if args.stagger == 2 else 1) if args.overlap > 0 else 0
