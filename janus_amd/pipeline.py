@@ -473,10 +473,25 @@ class JanusPipeline:
                 # cross-attention at 2 key splits: with 2 x 64 rows the grid fills the
                 # decoder's CUs without the split (4: decoder side 252.6-255.3 ms, 2:
                 # 246.7-248.6, 8: 264.7-266.7, one box)
+                beside = os.environ.get("JANUS_YIN_BESIDE") is not None and n_dec > 0
+                if beside:
+                    # opt-in: the decoder side's YIN concurrently with the decode call, on a
+                    # second stream over the decoder's CUs with a capped grid
+                    ys = self._yin_s.stream
+                    ys.wait_stream(ds)
+                    with torch.cuda.stream(ys):
+                        try:
+                            pd = prosody_launch(pcm, offsets[0:n_dec + 1], lengths[0:n_dec], CAPTURE_RATE,
+                                                512, max_blocks=int(os.environ.get("JANUS_YIN_BESIDE", "64")))
+                        except Exception:  # engine.py:520-525
+                            pd = None
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
                                   xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "2")),
                                   cu_count=self._dec_s.n_cus)
-                if n_dec > 0:
+                if beside:
+                    ds.wait_stream(ys)
+                    pres = (pd, pres)
+                elif n_dec > 0:
                     pres = (yin(0, n_dec), pres)
             st["started"] = True
             for j in range(n):
