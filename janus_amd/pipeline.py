@@ -522,20 +522,21 @@ class JanusPipeline:
 
     def _yin_split(self, st, B):
         """Utterances whose YIN runs on the decoder side in the staggered step. Fixed by
-        JANUS_YIN_DEC_UTTS; otherwise self-balancing: starts at 5B/8 and moves by the
-        previous step's side-time gap (vocoder side minus decoder side, HIP events on the
-        two CU-masked streams) over twice the per-utterance YIN time, at most 8 per step,
+        JANUS_YIN_DEC_UTTS; otherwise self-balancing: starts at 7B/8 (where it settled on
+        the r04 boxes: 52-59 of 64) and moves by the previous full step's side-time gap
+        (vocoder side minus decoder side, HIP events on the two CU-masked streams) over
+        twice the per-utterance YIN time, at most 16 per step,
         so the two partitions finish together whatever the box's vocoder / decoder speed
         ratio (measured from box to box: vocoder side 253-265 ms at the same split)."""
         env = os.environ.get("JANUS_YIN_DEC_UTTS")
         if env is not None:
             return max(0, min(B - 1, int(env)))
-        n = st.get("n_dec", 5 * B // 8)
+        n = st.get("n_dec", 7 * B // 8)
         prev = st.get("prev_ev")
         if prev is not None and prev[1].query() and prev[3].query():
             gap = prev[0].elapsed_time(prev[1]) - prev[2].elapsed_time(prev[3])
             move = int(round(gap / (2.0 * self.YIN_MS_PER_UTT)))
-            n = max(0, min(B - 1, n + max(-8, min(8, move))))
+            n = max(0, min(B - 1, n + max(-16, min(16, move))))
         st["n_dec"] = n
         return n
 
