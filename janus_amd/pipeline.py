@@ -473,16 +473,21 @@ class JanusPipeline:
                 # cross-attention at 2 key splits: with 2 x 64 rows the grid fills the
                 # decoder's CUs without the split (4: decoder side 252.6-255.3 ms, 2:
                 # 246.7-248.6, 8: 264.7-266.7, one box)
-                beside = os.environ.get("JANUS_YIN_BESIDE") is not None and n_dec > 0
+                # the decoder side's YIN runs concurrently with the decode call, on a second
+                # stream over the decoder's CUs with its grid capped at JANUS_YIN_BESIDE
+                # blocks (default 128; 0: after the call): the latency-bound decoder leaves
+                # issue slots free. Same box, two rounds of 5 steps: 259.4 / 258.4 ms at 128
+                # against 261.7 / 262.3 after the call and 263.0 / 262.3 at 256
+                # (profiles/r04_yin_beside_ab.json)
+                yb = int(os.environ.get("JANUS_YIN_BESIDE", "128"))
+                beside = yb > 0 and n_dec > 0
                 if beside:
-                    # opt-in: the decoder side's YIN concurrently with the decode call, on a
-                    # second stream over the decoder's CUs with a capped grid
                     ys = self._yin_s.stream
                     ys.wait_stream(ds)
                     with torch.cuda.stream(ys):
                         try:
                             pd = prosody_launch(pcm, offsets[0:n_dec + 1], lengths[0:n_dec], CAPTURE_RATE,
-                                                512, max_blocks=int(os.environ.get("JANUS_YIN_BESIDE", "64")))
+                                                512, max_blocks=yb)
                         except Exception:  # engine.py:520-525
                             pd = None
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
