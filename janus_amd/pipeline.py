@@ -394,8 +394,9 @@ class JanusPipeline:
         batch i-m's, m = 1 .. N-1, continuing in their slot set (positions mS .. (m+1)S-1),
         so every step still completes exactly one batch's decode, but the decoder's
         latency-bound launches serve N times the rows. Per step: mel + encoder of batch i
-        (whole GPU), then the decoder call on the decoder's CUs beside the vocoder of batch
-        i-N + YIN of batch i on the vocoder's CUs. Returns (EncodeResult, wav, pcm16) of
+        (whole GPU), then the decoder call on the decoder's CUs (with the YIN of the first
+        n_dec utterances of batch i beside it, _yin_split) beside the vocoder of batch i-N
+        + the rest of batch i's YIN on the vocoder's CUs. Returns (EncodeResult, wav, pcm16) of
         batch i-N, (None, None, None) for the first N calls; ``flush_staggered`` drains.
         Greedy (T = 0) only; per-row results are bit-identical to the one-batch decode
         (rows are independent of their neighbours' positions)."""
@@ -440,10 +441,10 @@ class JanusPipeline:
         ev[2].record(ds)
         wav = pcm16 = None
         pres = None
-        # YIN of the first n_dec utterances runs on the decoder side after the decoder call,
-        # the rest behind the vocoder: with two batches per decoder call that side has the
-        # slack (64 x 30 s, one box: 0 / 24 / 32 / 40 of 64 -> sides 275 / 242, 260 / 246,
-        # 256 / 249, 253 / 253 ms; step 287 -> 264 ms)
+        # YIN of the first n_dec utterances runs on the decoder side (beside the decoder call,
+        # below), the rest behind the vocoder: with two batches per decoder call that side has
+        # the slack (64 x 30 s, one box, YIN after the call: 0 / 24 / 32 / 40 of 64 -> sides
+        # 275 / 242, 260 / 246, 256 / 249, 253 / 253 ms; step 287 -> 264 ms)
         n_dec = self._yin_split(st, B) if pcm is not None else 0
 
         def yin(u0, u1):
