@@ -66,11 +66,23 @@ def parse():
                     help="skip the flush and the three idle-pipeline latency steps after the timed "
                          "region (profiling runs: only priming, warm-up and timed overlapped steps "
                          "then reach the kernel trace)")
-    ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4),
+    ap.add_argument("--config", type=int, default=4, choices=(1, 2, 3, 4, 5),
                     help="BASELINE.json config: 4 (default) = the headline, its per-GPU share "
                          "(64 x 30 s end to end); 1 = the 5 s WAV through the drop-in "
                          "Transcriber + prosody + packet; 2 = tiny.en + vocoder on one 30 s "
-                         "utterance (latency); 3 = base.en encode-only, 64 x 30 s")
+                         "utterance (latency); 3 = base.en encode-only, 64 x 30 s; 5 = "
+                         "streaming duplex, --streams channels per GPU in real time")
+    ap.add_argument("--streams", type=int, default=16,
+                    help="config 5: capture channels per GPU (128 / 8)")
+    ap.add_argument("--block-ms", type=int, default=320, help="config 5: block length")
+    ap.add_argument("--stream-async", type=int, default=1,
+                    help="config 5: 1 = encode + render on a worker stream while the next "
+                         "blocks are ingested (StreamingEncoder(asynchronous=True))")
+    ap.add_argument("--duplex", type=int, default=1,
+                    help="config 5: render every packet through the receiver's vocoder")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="no GPU: spawn / join the ranks over gloo and print each rank's shard "
+                         "(tests of the launcher)")
     ap.add_argument("--fallback-steps", type=int, default=1,
                     help="after the headline (T = 0) line, time this many overlapped steps with "
                          "faster-whisper's temperature fallback on and report them as "
@@ -515,21 +527,167 @@ def cpu_encoder_baseline(model):
             "cpu_model": _cpu_model()}
 
 
+def run_config5(args, rank, world, use_dist, dev):
+    """BASELINE config 5: 16 concurrent 48 kHz capture channels per GPU (128 over 8 GPUs)
+    arriving in real time as 320 ms blocks (10 x 1536-sample chunks); channel s on rank
+    s mod N. Per block every chunk is gated and phrases are segmented per channel
+    (engine.py:438-506); completed phrases are encoded as one GPU batch (Whisper + YIN with
+    per-channel detector state + packet, engine.py:510-552) on a worker stream and, in
+    duplex mode, rendered by the receiver leg (engine.py:220-286: prompt -> vocoder at the
+    phrase's duration). After the run every rank's per-block push latencies and
+    per-phrase duplex latencies (phrase complete -> packet + rendered audio) are
+    all-gathered (RCCL), so rank 0 reports the node's p50 / p99 and whether every block
+    and phrase stayed inside the 320 ms block."""
+    from janus_amd.streaming import CHUNK, StreamingEncoder
+    from janus_amd.whisper import CONFIGS, WhisperEngine
+    from janus_amd.workload import channel_audio, synth_speech
+    from janus_amd.services.transcriber import TEMPERATURES
+    per_block = int(round(args.block_ms / 32.0))          # 1536 samples = 32 ms
+    n_blocks = int(args.seconds * 1000 / args.block_ms)
+    total = n_blocks * per_block * CHUNK
+    n_total = args.streams * world
+    mine = [s for s in range(n_total) if s % world == rank]
+    audio = np.stack([channel_audio(s, total) for s in mine])
+    S = len(mine)
+    w = WhisperEngine(CONFIGS[args.model], seed=0)
+    temps = TEMPERATURES if args.fallback else (0.0,)
+    rx = None
+    if args.duplex:
+        from janus_amd.pipeline import JanusPipeline
+        rx = JanusPipeline(args.model, max_length=8)   # its vocoder renders the far end
+    enc = StreamingEncoder(S, w, max_length=args.max_length, asynchronous=bool(args.stream_async),
+                           receiver=rx, temperatures=temps)
+    # warm-up: one block of speech + silence on a scratch encoder (graph capture, allocations)
+    warm = StreamingEncoder(S, w, max_length=args.max_length, receiver=rx, temperatures=temps)
+    z = np.zeros((S, per_block * CHUNK), np.float32)
+    sp = np.tile(synth_speech(1, per_block * CHUNK / 48000.0)[None, :per_block * CHUNK], (S, 1))
+    warm.push(sp)
+    for _ in range(3):
+        warm.push(z)
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    phrases = 0
+    t_start = time.perf_counter()
+    for b in range(n_blocks):
+        # blocks arrive in real time: block b is complete at t_start + (b + 1) * block
+        wait = t_start + (b + 1) * args.block_ms / 1000.0 - time.perf_counter()
+        if wait > 0:
+            time.sleep(wait)
+        out = enc.push(audio[:, b * per_block * CHUNK:(b + 1) * per_block * CHUNK])
+        phrases += len(out)
+    phrases += len(enc.flush())
+    t_total = time.perf_counter() - t_start
+    enc.close()
+    lat, plat = list(enc.latencies), list(enc.phrase_latencies)
+    counts = [phrases, enc.max_queue, enc.extra_windows]
+    if use_dist:
+        from janus_amd.dist import gather_values
+        lat, plat = gather_values(lat, dev), gather_values(plat, dev)
+        per_rank = gather_values(counts, dev)
+        counts = [sum(per_rank[0::3]), max(per_rank[1::3]), sum(per_rank[2::3])]
+        wall = torch.tensor([t_total], dtype=torch.float64, device=dev)
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        t_total = float(wall.item())
+    if rank != 0:
+        return
+    lat = np.array(lat) * 1000.0
+    plat = np.array(plat) * 1000.0 if len(plat) else np.zeros(1)
+    p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+    pp50, pp99 = float(np.percentile(plat, 50)), float(np.percentile(plat, 99))
+    out = {"metric": "config 5: streaming duplex, 16 kHz channels x 320 ms chunks, per-phrase "
+                     "encode+decode p50 latency (phrase complete -> packet + rendered audio)",
+           "value": round(pp50, 2), "unit": "ms", "n_gpus": world, "steps": n_blocks, "warmup": 4,
+           "ms_per_step": round(p50, 3), "higher_is_better": False, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp16",
+           "data": "synthetic seeded speech phrases with silences per channel; energy speech "
+                   "gate; seeded synthetic weights",
+           "config": {"workload": f"{n_total} channels ({args.streams} per GPU, channel s on "
+                                  f"rank s mod {world}), {args.seconds:g} s of {args.block_ms} ms "
+                                  "blocks in real time", "model": args.model,
+                      "streams_total": n_total, "parallelism": f"dp{world}",
+                      "max_length": args.max_length},
+           "streams_total": n_total, "streams_per_gpu": args.streams, "block_ms": args.block_ms,
+           "blocks": n_blocks, "phrases": int(counts[0]),
+           "asynchronous": bool(args.stream_async), "duplex": bool(args.duplex),
+           # per-block push latency (gate + segmentation of every channel's 320 ms block)
+           "p50_ms": round(p50, 2), "p99_ms": round(p99, 2), "max_ms": round(float(lat.max()), 2),
+           # per-phrase duplex latency (phrase complete -> packet + rendered audio)
+           "phrase_p50_ms": round(pp50, 2), "phrase_p99_ms": round(pp99, 2),
+           "phrase_max_ms": round(float(plat.max()), 2),
+           "worker_max_queue": int(counts[1]), "wall_s": round(t_total, 2),
+           "audio_s": round(n_blocks * args.block_ms / 1000.0, 2),
+           "realtime": bool(p99 < args.block_ms and pp99 < args.block_ms),
+           "fallback": bool(args.fallback), "extra_seek_windows": int(counts[2]),
+           "roofline": None,
+           "roofline_note": "real-time arrival: per-phrase batches of a few 1.5-6 s phrases, "
+                            "latency-bound; the kernels' rooflines are the config-4 line's",
+           "cpu_baseline": None}
+    print(json.dumps(out), flush=True)
+
+
+def run_launch_check(args, rank, world):
+    """--launch-check: the multi-process plumbing without a GPU (gloo): every rank reports
+    (rank, world, its utterance shard of world x batch, its config-5 channels) and rank 0
+    prints them gathered, one JSON line. tests/test_distributed.py drives it through
+    ``bench.py --gpus 2`` (the spawning launcher) on the CPU."""
+    from janus_amd.dist import gather_values, shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    u0, u1 = shard(rank, world, world * args.batch)
+    chans = [s for s in range(args.streams * world) if s % world == rank]
+    mine = [rank, world, u0, u1, len(chans), chans[0] if chans else -1]
+    allv = gather_values(mine, torch.device("cpu")) if world > 1 else mine
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        ranks = [allv[i:i + 6] for i in range(0, len(allv), 6)]
+        print(json.dumps({"launch_check": True, "world": world,
+                          "ranks": [{"rank": int(r[0]), "world": int(r[1]),
+                                     "shard": [int(r[2]), int(r[3])], "channels": int(r[4]),
+                                     "first_channel": int(r[5])} for r in ranks],
+                          "pid": os.getpid()}), flush=True)
+
+
 def main():
     args = parse()
+    from janus_amd import launch
+    launched = os.environ.get("WORLD_SIZE") is not None
+    if args.config in (1, 2, 3) and args.gpus != 1:
+        print(f"bench.py: config {args.config} is a single-GPU configuration (--gpus 1)",
+              file=sys.stderr)
+        sys.exit(2)
+    # --gpus N without a launcher: N fresh rank processes of this script, started before
+    # this process makes any HIP call; with a launcher, --gpus must match WORLD_SIZE
+    err = None if args.launch_check else launch.check_world(args.gpus)
+    if err is not None:
+        print(f"bench.py: {err}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if not launched and args.gpus > 1:
+        sys.exit(launch.spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        run_launch_check(args, rank, world)
+        return
     if args.config in (1, 2, 3):
         torch.cuda.set_device(0)
         {1: run_config1, 2: run_config2, 3: run_config3}[args.config](args)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     # JANUS_DIST_FORCE=1: the RCCL path (process group, barriers, max-over-ranks all-reduce,
     # result gather) at world size 1 too — exercises it on a one-GPU box
     use_dist = world > 1 or os.environ.get("JANUS_DIST_FORCE") == "1"
     if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.config == 5:
+        run_config5(args, rank, world, use_dist, torch.device("cuda", local))
+        if use_dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from janus_amd.dist import gather_results, shard
     from janus_amd.pipeline import JanusPipeline

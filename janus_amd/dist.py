@@ -73,6 +73,14 @@ def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
 
+def gather_values(values, device, group=None):
+    """All-gather a variable-length list of floats from every rank (config 5's per-block
+    and per-phrase latencies) -> one flat list in rank order, on every rank."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64).reshape(-1, 1)
+    g = gather_stats(t.to(device), group)   # float32 keeps µs at these magnitudes
+    return [float(v) for v in g.reshape(-1).cpu().tolist()]
+
+
 def gather_results(packets, stats: torch.Tensor, device, group=None):
     """The result gather of SURVEY §8(e): packet bytes and per-utterance stats."""
     return gather_packets(packets, device, group), gather_stats(stats, group)

@@ -76,6 +76,24 @@ def utterance_batch(config: int, count: int, seconds: float = 30.0, sr: int = 48
     return [synth_speech(1000 * config + i, seconds, sr) for i in range(count)]
 
 
+def channel_audio(channel: int, n_samples: int, sr: int = 48000) -> np.ndarray:
+    """One capture channel of BASELINE config 5 (48 kHz): phrases of 1.5-6 s separated by
+    0.6-2 s of silence, the first starting within 1 s. Seeded per GLOBAL channel index
+    (5000 + channel), so a rank generates only the channels it owns and every world size
+    sees the same channels."""
+    rng = np.random.default_rng(5000 + channel)
+    out = np.zeros(n_samples, np.float32)
+    t = int(rng.integers(0, sr))
+    k = 0
+    while t < n_samples:
+        ph = synth_speech(5000 + 97 * channel + k, float(rng.uniform(1.5, 6.0)), sr)
+        n = min(len(ph), n_samples - t)
+        out[t:t + n] = ph[:n]
+        t += n + int(rng.uniform(0.6, 2.0) * sr)
+        k += 1
+    return out
+
+
 def sine(frequency=440.0, duration=1.0, sample_rate=48000, amplitude=0.5) -> np.ndarray:
     """Same construction as the reference's generate_sine_wave
     (backend/tests/test_input_processing.py:30-45)."""
