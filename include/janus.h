@@ -282,8 +282,12 @@ typedef struct {
    * (its tokens, KV cache, counters and rule state are kept; pass its encoder output again);
    * rows with offset 0 start fresh and must be one contiguous range. A continuing row's
    * offset must not exceed the position its previous calls reached (its tokens and KV rows
-   * below the offset must have been written). Greedy only, no enc_index; pos_offset + steps
-   * <= max_length. NULL = every row fresh. */
+   * below the offset must have been written): the context records where every slot stands
+   * after each call (janus_whisper_decode_stand) and REJECTS (non-zero status,
+   * janus_last_error) a continuing row past it, or a continuing call whose batch size /
+   * max_length differ from the previous call's. When every row finishes early (check_every
+   * polls), all rows stand at offset + the positions actually run. Greedy only, no
+   * enc_index; steps >= 0; pos_offset + steps <= max_length. NULL = every row fresh. */
   const int32_t* pos_offset;
   int steps;
 } janus_decode_rows;
@@ -324,6 +328,16 @@ int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* enc, int ba
  * launches per position beside bytes per position); the reference has no counterpart.
  */
 int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* launches);
+
+/*
+ * Where each of the `batch` row slots stands after the last completed decode call (the
+ * first position a staggered call may continue it from: tokens and KV rows below it are
+ * written). Fails when the last call had another batch size or failed. The continuous-
+ * batching plan of the serving step (janus_amd/pipeline.py stagger_plan) continues from
+ * here; the reference has no counterpart (its decode is one faster-whisper call per
+ * window, transcriber.py:53-57).
+ */
+int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch);
 
 /* ------------------------------------------------------------ vocoder --- */
 /*

@@ -9,6 +9,9 @@
 // chosen token's log-probability (avg_logprob).
 #include <cfloat>
 #include <cstdlib>
+#ifdef JANUS_DEBUG_ASSERT
+#include <cassert>
+#endif
 #include "mfma.h"
 #include "kernels.h"
 #include "decoder.h"
@@ -64,9 +67,12 @@ __device__ __forceinline__ void embed_row(const _Float16* __restrict__ tok_emb,
                                           const float* __restrict__ ln_b,
                                           _Float16* __restrict__ ln_out) {
   __shared__ float red[2][4];
-  // defence in depth: a row continued past the tokens it has written (a pos_offset beyond
-  // where the row stands) reads the -1 fill; embed token 0 rather than read before the table
-  tok = tok < 0 ? 0 : tok;
+  // every token read here was written by a selection or the prompt: the context rejects a
+  // staggered row continued past where its slot stands (janus_whisper_decode_stand), so
+  // the -1 fill is never embedded (JANUS_DEBUG_ASSERT builds check it)
+#ifdef JANUS_DEBUG_ASSERT
+  assert(tok >= 0);
+#endif
   float v0 = 0.f, v1 = 0.f;
   for (int base = 0; base < d; base += 512) {
     const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece

@@ -69,6 +69,12 @@ struct DecLane {
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
   int64_t last_launches = 0;     // kernel launches those positions issued (graph nodes)
+  // where each row slot stands after the last call (positions whose KV rows and next
+  // tokens are written): a staggered call may continue row b only from an offset <=
+  // stand[b], with the same batch size and max_length. Empty: nothing to continue (no call
+  // yet, or the last one failed).
+  std::vector<int32_t> stand;
+  int stand_maxlen = 0;
   hipStream_t stream = nullptr;  // graph capture needs a non-null stream
   std::vector<uint32_t> stream_mask;  // CU mask the lane stream was created with (empty: none)
   hipEvent_t ev_done = nullptr;
@@ -407,8 +413,23 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     if (f1 <= f0) f0 = f1 = 0;
     for (int b = f0; b < f1; ++b) JANUS_CHECK(h_roff[b] == 0, "decode: fresh rows must be contiguous");
   }
+  JANUS_CHECK(!stagger || rows->steps >= 0, "decode: steps must be >= 0");
   const int steps = (stagger && rows->steps > 0) ? rows->steps : maxlen - 1;
   JANUS_CHECK(!stagger || max_roff + steps <= maxlen, "decode: pos_offset + steps > max_length");
+  // a continuing row reads the tokens and KV rows its slot holds: only up to where the
+  // previous calls left it (a larger offset would read unwritten tokens / KV rows)
+  if (stagger) {
+    for (int b = 0; b < B; ++b) {
+      if (h_roff[b] == 0) continue;
+      JANUS_CHECK((int)Z.stand.size() == B && Z.stand_maxlen == maxlen,
+                  "decode: continuing rows need the previous call's batch size and max_length");
+      JANUS_CHECK(h_roff[b] <= Z.stand[b],
+                  "decode: row " + std::to_string(b) + " continues at pos_offset " + std::to_string(h_roff[b]) +
+                      " but its slot stands at " + std::to_string(Z.stand[b]));
+    }
+  }
+  // until this call completes, nothing may be continued (a failed call leaves stand empty)
+  Z.stand.clear();
   const int min_plen = f1 > f0 ? *std::min_element(h_plen.begin() + f0, h_plen.begin() + f1) : 1;
   const int max_plen = f1 > f0 ? *std::max_element(h_plen.begin() + f0, h_plen.begin() + f1) : 1;
   JANUS_CHECK(min_plen >= 1 && max_plen < maxlen && maxlen <= NC,
@@ -786,6 +807,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       if (all) break;  // remaining positions keep -1; callers stop at the first eot
     }
   }
+  // every row ran Z.last_positions positions from its offset (the early exit stops all rows
+  // together); janus_whisper_decode_stand reports it, stagger plans continue from there
+  Z.stand.assign(B, 0);
+  for (int b = 0; b < B; ++b) Z.stand[b] = (stagger ? h_roff[b] : 0) + Z.last_positions;
+  Z.stand_maxlen = maxlen;
   JANUS_HIP(hipMemcpyAsync(tokens_out, tokens, sizeof(int32_t) * (int64_t)B * maxlen,
                            hipMemcpyDeviceToDevice, s));
   JANUS_HIP(hipMemcpyAsync(n_tokens_out, n_tokens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
@@ -911,6 +937,16 @@ extern "C" int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* 
   const DecodeSampling smp{temperature, seeds};
   return decode_entry(w, enc, batch, opt, rows, tokens, n_tokens, sum_logprob, no_speech_prob, stream,
                       &smp);
+}
+
+extern "C" int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch) {
+  return guarded([&] {
+    JANUS_CHECK(w && stand, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    JANUS_CHECK(!w->lanes.empty() && (int)w->lanes[0]->stand.size() == batch,
+                "decode_stand: no completed decode of this batch size");
+    std::copy(w->lanes[0]->stand.begin(), w->lanes[0]->stand.end(), stand);
+  });
 }
 
 extern "C" int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* launches) {

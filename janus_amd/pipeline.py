@@ -90,9 +90,11 @@ def stagger_plan(sets, pos, started, k, S, fresh):
     sets[j]: None or {"born": call index the batch entered}; pos[j]: where set j's rows
     stand after the previous calls; k: this call's index (fresh set k % N); fresh: a new
     batch enters. Returns ([offset per set], completing set or None). A set holding a
-    batch continues at (k - born) S; a set without one continues from where its rows stand,
+    batch continues at (k - born) S (at most where its rows stand: the early exit stops a
+    call whose rows all finished); a set without one continues from where its rows stand,
     at most (N-1) S, so it reads only tokens and KV rows it wrote; before the first call
-    every set starts fresh."""
+    every set starts fresh. pos comes from the context (janus_whisper_decode_stand), which
+    rejects any offset past it."""
     n = len(sets)
     f = k % n
     offs = [0] * n
@@ -101,7 +103,9 @@ def stagger_plan(sets, pos, started, k, S, fresh):
             if j == f and fresh:
                 offs[j] = 0
             elif sets[j] is not None:
-                offs[j] = (k - sets[j]["born"]) * S
+                # (k - born) S, or less where every row finished early and the previous
+                # call stopped short (its rows stand at pos[j]; the context rejects more)
+                offs[j] = min((k - sets[j]["born"]) * S, pos[j])
             else:
                 offs[j] = min(pos[j], (n - 1) * S)
     jc = (k - (n - 1)) % n
@@ -410,7 +414,14 @@ class JanusPipeline:
         hi = self._hi_stream(dev)
         ds, vs = self._split_streams(dev, dec_per_xcd)
         st = getattr(self, "_stag", None)
-        if st is None or st["B"] != B:
+        if st is not None and st["B"] != B:
+            # the slot layout (and every KV / token row in it) is sized by B: batches still
+            # in the decoder would be lost
+            if any(x is not None for x in st["sets"]) or st["done"] is not None:
+                raise ValueError(f"step_staggered: batch size {B} != {st['B']} while batches are "
+                                 "in flight; call flush_staggered() first (or pad the batch)")
+            st = None
+        if st is None:
             n = max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2")))
             d = w.cfg.d_model
             st = self._stag = {"B": B, "n": n, "k": 0, "sets": [None] * n, "done": None,
@@ -500,8 +511,11 @@ class JanusPipeline:
                 elif n_dec > 0:
                     pres = (yin(0, n_dec), pres)
             st["started"] = True
+            # where each set's rows stand now (offset + S, or fewer when every row
+            # finished and the call stopped early), as the context recorded it
+            stand = w.decode_stand(n * B)
             for j in range(n):
-                pos[j] = set_offs[j] + S
+                pos[j] = stand[j * B]
         if pcm is not None:
             st["sets"][f] = {"pres": pres, "B": B, "mode": mode, "override": override,
                              "timestamp": timestamp, "born": k}
@@ -612,10 +626,16 @@ class JanusPipeline:
         main = torch.cuda.current_stream(dev)
         ds, es, vs = self._lane_streams(dev, dec_per_xcd, enc_per_xcd)
         st = getattr(self, "_lanes", None)
-        if st is None or st["B"] != B:
+        if st is not None and st["B"] != B:
+            if (st["staged"] is not None or st["vocode"] is not None
+                    or any(x is not None for x in st["sets"])):
+                raise ValueError(f"step_pipelined: batch size {B} != {st['B']} while batches are "
+                                 "in flight; call flush_pipelined() first (or pad the batch)")
+            st = None
+        if st is None:
             d = w.cfg.d_model
             st = self._lanes = {"B": B, "parity": 0, "sets": [None, None], "staged": None,
-                                "vocode": None, "started": False,
+                                "vocode": None, "started": False, "pos": [0, 0],
                                 "enc": torch.zeros(2 * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
                                                    device=dev),
                                 "stage": torch.zeros(B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
@@ -681,10 +701,14 @@ class JanusPipeline:
                     offs[k] = 0 if staged is not None or not started else L - S
                 else:
                     offs[k] = S if cont is not None else (L - S if started else 0)
+                if offs[k] > 0:   # never past where the slot stands (early-exit calls)
+                    offs[k] = min(offs[k], st["pos"][k // B])
             with torch.cuda.stream(ds):
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
                                   xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
                                   cu_count=self._dec_s.n_cus)
+            stand = w.decode_stand(2 * B)
+            st["pos"] = [stand[0], stand[B]]
             st["started"] = True
         pres = rest
         with torch.cuda.stream(ds):

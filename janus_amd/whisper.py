@@ -325,6 +325,10 @@ class WhisperEngine:
         same row (pass the same batch size and their encoder output again), rows with 0
         start fresh (one contiguous range)."""
         B = enc.shape[0] if enc_index is None else len(enc_index)
+        if steps < 0:
+            raise ValueError("steps must be >= 0")
+        if steps and pos_offset is None:
+            raise ValueError("steps applies to a staggered call (pos_offset) only")
         if temperature > 0:
             if seeds is None or len(seeds) != B:
                 raise ValueError("sampling needs one uint32 seed per row")
@@ -373,6 +377,13 @@ class WhisperEngine:
                      nsp.data_ptr(), nat.stream_ptr())
         del keep, pr, ei, po
         return DecodeOut(tokens, ntok, slp, nsp, plens)
+
+    def decode_stand(self, batch: int):
+        """Where each of the last decode call's ``batch`` row slots stands (the largest
+        pos_offset a staggered call may continue it from; janus_whisper_decode_stand)."""
+        out = np.zeros(batch, np.int32)
+        nat.call("janus_whisper_decode_stand", self._h, out.ctypes.data, int(batch))
+        return [int(v) for v in out]
 
     def decode_info(self):
         """(positions stepped, kernel launches issued) by the last decode call

@@ -283,6 +283,48 @@ def test_staggered_decode_matches_full(engine, gpu, L):
         assert int(n.min()) >= min(16, L - plen - 1)
 
 
+def test_staggered_offset_past_stand_is_rejected(engine, gpu):
+    """The context records where every row slot stands after each call
+    (janus_whisper_decode_stand) and rejects a continuing row whose pos_offset lies past it
+    — it would read tokens and KV rows never written — with a non-zero status and
+    janus_last_error, as it rejects continuing after a call of another batch size. The
+    valid plan right after the rejected one is still bit-identical to the full decode (a
+    call rejected by the checks runs nothing and keeps the slots' state)."""
+    from janus_amd import _native as nat
+    eng, _ = engine
+    N, L, S = 2, 40, 20
+    utts = [synth_speech(400 + j, 2.0) for j in range(N)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, N, 3))
+    ref = eng.decode_ex(enc, max_length=L)
+    two = torch.cat([enc, enc])
+    eng.decode_ex(two, max_length=L, pos_offset=[0] * (2 * N), steps=S)
+    assert eng.decode_stand(2 * N) == [S] * (2 * N)
+    # continuing one position past the stand: rejected before anything runs (the slots
+    # keep their state)
+    with pytest.raises(nat.JanusNativeError, match="stands at"):
+        eng.decode_ex(two, max_length=L, pos_offset=[0] * N + [S + 1] * N, steps=S - 1)
+    assert eng.decode_stand(2 * N) == [S] * (2 * N)
+    # negative steps are refused on the Python side, a stray steps without offsets too
+    with pytest.raises(ValueError):
+        eng.decode_ex(two, max_length=L, pos_offset=[0] * (2 * N), steps=-1)
+    with pytest.raises(ValueError):
+        eng.decode_ex(two, max_length=L, steps=S)
+    # the good plan: continue at S, bit-identical to the one-call decode
+    out = eng.decode_ex(two, max_length=L, pos_offset=[0] * N + [S] * N, steps=L - 1 - S)
+    assert eng.decode_stand(2 * N) == [L - 1 - S] * N + [L - 1] * N
+    sl = slice(N, 2 * N)
+    assert torch.equal(out.n_tokens[sl].cpu(), ref.n_tokens.cpu())
+    assert torch.equal(out.sum_logprob[sl].cpu(), ref.sum_logprob.cpu())
+    plen = len(eng.tokenizer.sot_sequence)
+    for j in range(N):
+        k = plen + int(ref.n_tokens[j])
+        assert torch.equal(out.tokens[N + j, :k].cpu(), ref.tokens[j, :k].cpu())
+    # another batch size cannot continue these slots
+    with pytest.raises(nat.JanusNativeError, match="batch size"):
+        eng.decode_ex(enc[:1].repeat(3, 1, 1), max_length=L, pos_offset=[0, 5, 5], steps=5)
+
+
 def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
     """Opt-in decoder lanes (JANUS_DEC_LANES: the batch split over concurrent streams and
     host threads) decode every utterance exactly as the single-lane decoder does: rows
