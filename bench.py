@@ -83,8 +83,8 @@ def parse():
     ap.add_argument("--launch-check", action="store_true",
                     help="no GPU: spawn / join the ranks over gloo and print each rank's shard "
                          "(tests of the launcher)")
-    ap.add_argument("--fallback-steps", type=int, default=1,
-                    help="after the headline (T = 0) line, time this many overlapped steps with "
+    ap.add_argument("--fallback-steps", type=int, default=3,
+                    help="after the headline (T = 0) line, time this many steps of the same serving step with "
                          "faster-whisper's temperature fallback on and report them as "
                          "xrt_with_fallback (0: skip)")
     ap.add_argument("--fallback", action="store_true",
@@ -715,9 +715,10 @@ def main():
             # three lanes: encoder of batch i, decoder of batches i-1 / i-2, vocoder of i-3
             enc, wav, pcm16 = pipe.step_pipelined(pcm, offs, lengths, frames, args.overlap,
                                                   args.enc_cus)
-        elif args.overlap > 0 and args.stagger and len(pipe.temperatures) == 1:
+        elif args.overlap > 0 and args.stagger:
             # continuous batching: batch i's first half and batch i-1's second half of the
-            # decode in one decoder call, the vocoder of batch i-2 beside it
+            # decode in one decoder call, the vocoder of batch i-2 beside it (with the
+            # fallback on, the completing batch's failing windows re-decode after it)
             enc, wav, pcm16 = pipe.step_staggered(pcm, offs, lengths, frames, args.overlap)
         elif args.overlap > 0:
             # steady-state serving pipeline: batch i through mel / encoder / decoder / YIN,
@@ -733,9 +734,9 @@ def main():
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
     # decoder slot sets (staggered: JANUS_STAGGER_SETS batches per decoder call) and the
     # pipeline depth (calls before the first batch comes out)
-    # (the staggered steps are greedy-only: with --fallback the overlapped step runs)
-    if args.fallback:
-        args.stagger = 0
+    # (the three-lane step is greedy-only: with --fallback --stagger 2 the staggered step runs)
+    if args.fallback and args.stagger == 2:
+        args.stagger = 1
     sets = (max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2"))) if args.stagger == 1
             else 2 if args.stagger == 2 else 1)
     depth = (sets if args.stagger == 1 else 3 if args.stagger == 2 else 1) if args.overlap > 0 else 0
@@ -773,17 +774,41 @@ def main():
     tok_counts = [float(n.float().mean().item()) for n in tok_counts]
     fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
+    # faster-whisper's seek loop would decode a second window of every clip whose first
+    # window's seek (the last timestamp pair) stops short of its content (gate 7); the
+    # pipeline decodes first windows only, so these are counted, not decoded
+    content = [(n + 2) // 3 // 160 for n in lengths]
+    seek_extra = int(sum(1 for g, c in zip(enc.gates or [], content) if len(g) > 7 and g[7] < c))
+    flush = {0: pipe.flush, 1: pipe.flush_staggered, 2: pipe.flush_pipelined}
     # latency of one batch through an IDLE pipeline (encode then decode back to back, nothing
     # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
     idle = []
     if args.overlap > 0 and not args.no_idle_latency:
-        {0: pipe.flush, 1: pipe.flush_staggered, 2: pipe.flush_pipelined}[args.stagger](frames)
+        flush[args.stagger](frames)
     for _ in range(0 if args.no_idle_latency else 3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         pipe.step(pcm, offs, lengths, frames)
         torch.cuda.synchronize()
         idle.append(time.perf_counter() - t0)
+    # the latency operating point: the overlapped step (--stagger 0: an utterance's encode +
+    # decode step, then its vocoder step) timed right after, beside the staggered headline
+    # (three steps per utterance): p50 of consecutive step pairs
+    ov = None
+    if args.overlap > 0 and args.stagger != 0 and not args.no_idle_latency and not args.fallback:
+        ov_t = []
+        for i in range(2 + 5):   # priming + warm-up, then 5 timed
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pipe.step_overlapped(pcm, offs, lengths, frames, args.overlap)
+            torch.cuda.synchronize()
+            if i >= 2:
+                ov_t.append(time.perf_counter() - t0)
+        pipe.flush(frames)
+        ov = {"p50_latency_ms": round(float(np.median([ov_t[i] + ov_t[i + 1]
+                                                        for i in range(len(ov_t) - 1)])) * 1000.0, 2),
+              "step_ms": [round(v * 1000.0, 1) for v in ov_t],
+              "xrt": round(B * args.seconds / float(np.mean(ov_t)), 2)}
     # the same serving step with faster-whisper's temperature fallback on (the library
     # default; every window of the seeded synthetic model fails its gates, so each runs all
     # five sampled temperatures x best_of 5): reported beside the T = 0 headline
@@ -791,7 +816,9 @@ def main():
     if (args.fallback_steps > 0 and not args.fallback and not args.no_idle_latency
             and args.overlap > 0):
         pipe.temperatures = TEMPERATURES
-        for _ in range(2):   # priming (encode only) + one warm step (B = 320 decode graphs)
+        # the pipeline's depth in priming calls (the first output needs depth + 1 calls),
+        # plus one warm step (B = 320 sampled-decode graphs)
+        for _ in range(depth + 1):
             step()
         fb_t = []
         for _ in range(args.fallback_steps):
@@ -800,9 +827,10 @@ def main():
             fenc = step()
             torch.cuda.synchronize()
             fb_t.append(time.perf_counter() - t0)
-        pipe.flush(frames)
+        flush[min(args.stagger, 1)](frames)
         pipe.temperatures = (0.0,)
         fb = {"xrt": round(B * args.seconds / float(np.mean(fb_t)), 2),
+              "step": {0: "overlapped", 1: "staggered", 2: "staggered"}[args.stagger],
               "step_ms": [round(v * 1000.0, 1) for v in fb_t],
               "sampled_decodes": int(sum(g[6] for g in fenc.gates or [])),
               "windows_failing_t0": int(sum(g[0] for g in fenc.gates or []))}
@@ -871,8 +899,16 @@ def main():
                 [sum(times[i:i + depth + 1]) for i in range(len(times) - depth)]
                 if args.overlap > 0 and len(times) > depth
                 else times)) * 1000.0, 2),
+            # the latency operating point: the overlapped step (--stagger 0), timed after the
+            # headline on the same pipeline (an utterance's encode + decode step, then its
+            # vocoder step); the staggered headline trades one more step of latency for xRT
+            "p50_latency_ms_overlapped": ov["p50_latency_ms"] if ov else None,
+            "overlapped": ov,
             "stagger": int(args.stagger),
             "stagger_sets": sets if args.stagger else None,
+            # the headline decodes at T = 0 only (faster-whisper's fallback temperatures are
+            # the xrt_with_fallback leg below, or --fallback)
+            "temperatures": list(pipe.temperatures) if args.fallback else [0.0],
             # one batch's encode + decode through an idle pipeline (sequential step), p50 of 3
             "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
             # wall time of the two CU partitions per timed step (HIP events on each side's
@@ -899,6 +935,10 @@ def main():
                       "fallback_run": bool(args.fallback),
                       "sampled_decodes": int(sum(g[6] for g in enc.gates or []))},
             "stats_gathered": n_stats,
+            # second windows faster-whisper's seek loop would run on the last timed batch
+            # (the first window's seek stops at a timestamp pair short of the clip's
+            # content); counted, not decoded: the pipeline decodes first windows only
+            "seek_windows_extra": seek_extra,
             # the overlapped step with the temperature fallback on (5 temperatures x best_of
             # 5 re-decodes of every failing window; rank 0's figure, per GPU)
             "xrt_with_fallback": fb["xrt"] if fb else None,

@@ -241,6 +241,14 @@ typedef struct {
                               stream's CU mask), e.g. 128 on a half-GPU partition: one
                               vocabulary-projection block per CU, and at <= 128 the skinny
                               projections split rows from N <= 1024 */
+  int state_slot;          /* decoder state slot of the context (0 = default): the KV caches,
+                              tokens and rule state a call leaves behind for staggered
+                              continuation live in this slot, so a sampled re-decode between
+                              two staggered calls runs in another slot without disturbing
+                              them (0 .. 7) */
+  int logits_blocks;       /* vocabulary-projection blocks (0 = cu_count) */
+  int msplit_rows_n;       /* skinny projections split rows over blocks up to this N
+                              (0 = auto: 1024 on <= 128 CUs, else none; -1 = never) */
 } janus_decode_options;
 
 /*
@@ -338,6 +346,8 @@ int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* lau
  * window, transcriber.py:53-57).
  */
 int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch);
+/* The same for decoder state slot `slot` (janus_decode_options.state_slot). */
+int janus_whisper_decode_stand_slot(janus_whisper* w, int slot, int32_t* stand, int batch);
 
 /* ------------------------------------------------------------ vocoder --- */
 /*

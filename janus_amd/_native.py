@@ -80,6 +80,7 @@ SIGNATURES = {
     "janus_whisper_decode_sample_ex": [_P, _P, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P],
     "janus_whisper_decode_info": [_P, _P, _P],
     "janus_whisper_decode_stand": [_P, _P, _I32],
+    "janus_whisper_decode_stand_slot": [_P, _I32, _P, _I32],
     "janus_vocoder_create": [_P, _P],
     "janus_vocoder_destroy": [_P],
     "janus_vocoder_set_tensor": [_P, ctypes.c_char_p, _P, _I64],

@@ -103,6 +103,7 @@ struct janus_whisper {
   janus::DevMem ws_x1, ws_x2, ws_r, ws_a, ws_qkv, ws_o, ws_f, ws_logmel, ws_maxkey;
   // decoder lanes: each owns the workspaces, captured graphs and stream of one batch slice
   std::vector<std::unique_ptr<janus::DecLane>> lanes;
+  int last_slot = 0;  // state slot of the last decode call (decode_info reports it)
   hipEvent_t ev_in = nullptr;
   ~janus_whisper() {
     if (ev_in) (void)hipEventDestroy(ev_in);
@@ -452,10 +453,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // cu_count: the CUs the caller's stream may use (a CU-masked partition); 0 = read it
   // from the stream's CU mask
   const int cus = opt->cu_count > 0 ? opt->cu_count : stream_cu_count(s);
-  const int lg_cap = std::getenv("JANUS_LOGITS_BLOCKS") ? std::atoi(std::getenv("JANUS_LOGITS_BLOCKS"))
-                                                        : cus;
-  const int msplit_n = std::getenv("JANUS_DEC_MSPLIT_N") ? std::atoi(std::getenv("JANUS_DEC_MSPLIT_N"))
-                                                         : (cus <= 128 ? 1024 : 0);
+  // launch geometry from the options (janus_decode_options.logits_blocks / msplit_rows_n;
+  // measured defaults: DESIGN.md §5b / §5d)
+  const int lg_cap = opt->logits_blocks > 0 ? opt->logits_blocks : cus;
+  const int msplit_n = opt->msplit_rows_n > 0 ? opt->msplit_rows_n
+                       : opt->msplit_rows_n < 0 ? 0 : (cus <= 128 ? 1024 : 0);
   auto dgargs = [&](auto&&... args) {
     GemmArgs g = gargs(args...);
     g.msplit_n = msplit_n;
@@ -939,22 +941,27 @@ extern "C" int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* 
                       &smp);
 }
 
-extern "C" int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch) {
+extern "C" int janus_whisper_decode_stand_slot(janus_whisper* w, int slot, int32_t* stand, int batch) {
   return guarded([&] {
     JANUS_CHECK(w && stand, "null argument");
     std::lock_guard<std::mutex> lk(w->mu);
-    JANUS_CHECK(!w->lanes.empty() && (int)w->lanes[0]->stand.size() == batch,
-                "decode_stand: no completed decode of this batch size");
-    std::copy(w->lanes[0]->stand.begin(), w->lanes[0]->stand.end(), stand);
+    JANUS_CHECK(slot >= 0 && slot < (int)w->lanes.size() && (int)w->lanes[slot]->stand.size() == batch,
+                "decode_stand: no completed decode of this batch size in this slot");
+    std::copy(w->lanes[slot]->stand.begin(), w->lanes[slot]->stand.end(), stand);
   });
+}
+
+extern "C" int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch) {
+  return janus_whisper_decode_stand_slot(w, 0, stand, batch);
 }
 
 extern "C" int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* launches) {
   return guarded([&] {
     JANUS_CHECK(w && positions && launches, "null argument");
     std::lock_guard<std::mutex> lk(w->mu);
-    *positions = w->lanes.empty() ? 0 : w->lanes[0]->last_positions;
-    *launches = w->lanes.empty() ? 0 : w->lanes[0]->last_launches;
+    const int sl = w->last_slot < (int)w->lanes.size() ? w->last_slot : 0;
+    *positions = w->lanes.empty() ? 0 : w->lanes[sl]->last_positions;
+    *launches = w->lanes.empty() ? 0 : w->lanes[sl]->last_launches;
   });
 }
 
@@ -978,9 +985,15 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
     // shared encoder rows / staggered rows: one lane holds them all (and its slots' state)
     if (rows && (rows->enc_index || rows->pos_offset)) nlanes = 1;
-    while ((int)w->lanes.size() < nlanes) w->lanes.emplace_back(new DecLane());
-    if (nlanes == 1 && s != nullptr) {
-      decode_greedy(w, *w->lanes[0], e, batch, opt, rows, tokens, n_tokens, sum_logprob,
+    // a state slot other than 0 (janus_decode_options.state_slot) is one lane of its own
+    JANUS_CHECK(opt->state_slot >= 0 && opt->state_slot < 8, "decode: state_slot must be 0 .. 7");
+    const int slot = opt->state_slot;
+    if (slot > 0) nlanes = 1;
+    while ((int)w->lanes.size() < std::max(nlanes, slot + 1)) w->lanes.emplace_back(new DecLane());
+    w->last_slot = slot;
+    if (nlanes == 1 && (s != nullptr || slot > 0)) {
+      JANUS_CHECK(s != nullptr, "decode: a state slot > 0 needs a non-null stream");
+      decode_greedy(w, *w->lanes[slot], e, batch, opt, rows, tokens, n_tokens, sum_logprob,
                     no_speech_prob, s, nullptr, smp);
       return;
     }

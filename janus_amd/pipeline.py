@@ -53,8 +53,11 @@ def _texts_and_gates(w, dec, temperatures=(0.0,), enc=None, **dec_kw):
     encoder output ``enc``, on the caller's stream, ``dec_kw`` to decode_ex) and the
     settled result gives the text. Gates per utterance: (needs_fallback at T = 0,
     no_speech_skip, avg_logprob, compression_ratio, no_speech_prob, temperature, sampled
-    decodes) of the settled result."""
-    from .services.transcriber import BEST_OF, _fallback, candidate
+    decodes, seek after the window) of the settled result — the seek faster-whisper's
+    generate_segments moves to (split_window: the window end, or the last timestamp pair);
+    a seek short of the clip's content frames means the reference's loop decodes a second
+    window from there (counted by bench.py as seek_windows_extra)."""
+    from .services.transcriber import BEST_OF, N_FRAMES, _fallback, candidate, split_window
     tk = w.tokenizer
     first = [candidate(tk, toks, avg, nsp, 0.0) for (toks, avg, nsp) in dec.rows()]
     if len(temperatures) > 1:
@@ -69,8 +72,9 @@ def _texts_and_gates(w, dec, temperatures=(0.0,), enc=None, **dec_kw):
     for t, c0, c, nd in zip(texts, first, final, ndec):
         skip = c.no_speech_prob > 0.6 and not c.avg_logprob > -1.0
         out_t.append("" if skip else t)
+        seek = N_FRAMES if skip else split_window(tk, c.tokens, 0, N_FRAMES)[1]
         out_g.append((c0.needs_fallback, skip, c.avg_logprob, c.compression_ratio, c.no_speech_prob,
-                      c.temperature, nd))
+                      c.temperature, nd, seek))
     return out_t, out_g
 
 
@@ -402,10 +406,14 @@ class JanusPipeline:
         n_dec utterances of batch i beside it, _yin_split) beside the vocoder of batch i-N
         + the rest of batch i's YIN on the vocoder's CUs. Returns (EncodeResult, wav, pcm16) of
         batch i-N, (None, None, None) for the first N calls; ``flush_staggered`` drains.
-        Greedy (T = 0) only; per-row results are bit-identical to the one-batch decode
-        (rows are independent of their neighbours' positions)."""
-        if tuple(self.temperatures) != (0.0,):
-            raise NotImplementedError("staggered decode runs at temperature 0 only")
+        The continuous batch decodes at T = 0; per-row results are bit-identical to the
+        one-batch decode (rows are independent of their neighbours' positions). With the
+        temperature fallback on (``temperatures`` beyond (0.0,), faster-whisper's default),
+        the windows of the completing batch that fail their gates leave the continuous
+        batch: their sampled best_of re-decodes (generate_with_fallback) run at the end of
+        the call on the whole GPU, from the batch's encoder output still in its slot set,
+        in decoder state slot 1 (the continuous batch's slots stay untouched in slot 0), as
+        step_overlapped runs them."""
         B = len(lengths)
         w = self.whisper
         L = self.max_length
@@ -532,6 +540,18 @@ class JanusPipeline:
             from .whisper import DecodeOut
             part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
                              dec.no_speech_prob[sl], dec.prompt_lens[sl])
+            part.settled = None
+            if len(self.temperatures) > 1:
+                # the fallback of the completing batch's failing windows, on the whole GPU
+                # after both sides (its encoder output stays in slot set jc until the next
+                # call's encoder, later on the same stream, overwrites it)
+                hi.wait_stream(main)
+                fb_kw = dict(xattn_splits=int(os.environ.get("JANUS_FB_XSPLITS", "4")),
+                             cu_count=torch.cuda.get_device_properties(dev).multi_processor_count,
+                             state_slot=1)
+                with torch.cuda.stream(hi):
+                    part.settled = _texts_and_gates(w, part, self.temperatures, st["enc"][sl], **fb_kw)
+                main.wait_stream(hi)
             st["done"] = (part, cont["pres"], B, cont["mode"], cont["override"], cont["timestamp"])
             st["sets"][jc] = None
         st["k"] = k + 1

@@ -69,6 +69,7 @@ PROMPT_RESET_ON_TEMPERATURE = 0.5
 FALLBACK_ROWS = 320      # hypotheses per sampling decode (64 windows x 5: one decode per
                          # temperature for a 64-window round; the windows' encoder outputs are
                          # shared by their hypotheses through enc_index)
+FALLBACK_ROWS_GATHER = 60  # the same for models past the PAIR path's H <= 8, d <= 512
 
 
 def _mix32(h: int) -> int:
@@ -252,7 +253,12 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
     (chunks of FALLBACK_ROWS rows)."""
     results = [[c] for c in first]
     final = [settle(r, temperatures) if not r[0].needs_fallback else None for r in results]
-    per = max(1, FALLBACK_ROWS // best_of)
+    # the shared-encoder PAIR path (H <= 8, d <= 512) reads each window's output in place;
+    # wider models gather one encoder copy per hypothesis row (0.74 GB per 320 rows at
+    # d = 768), so their sampled decodes stay at FALLBACK_ROWS_GATHER rows
+    cfg = getattr(engine, "cfg", None)
+    pair = cfg is None or (cfg.n_heads <= 8 and cfg.d_model <= 512)
+    per = max(1, (FALLBACK_ROWS if pair else FALLBACK_ROWS_GATHER) // best_of)
     for ti in range(1, len(temperatures)):
         T = float(temperatures[ti])
         pend = [j for j in range(len(first)) if final[j] is None]

@@ -56,7 +56,9 @@ class janus_decode_options(ctypes.Structure):
                 ("suppress_blank", ctypes.c_int), ("blank_token", ctypes.c_int),
                 ("timestamp_begin", ctypes.c_int), ("no_timestamps", ctypes.c_int),
                 ("max_initial_timestamp_index", ctypes.c_int), ("check_every", ctypes.c_int),
-                ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int)]
+                ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int),
+                ("state_slot", ctypes.c_int), ("logits_blocks", ctypes.c_int),
+                ("msplit_rows_n", ctypes.c_int)]
 
 
 class janus_decode_rows(ctypes.Structure):
@@ -276,7 +278,8 @@ class WhisperEngine:
         return enc
 
     def decode_options(self, max_length: int = 448, check_every: int = 16,
-                       timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0):
+                       timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0,
+                       state_slot: int = 0, logits_blocks: int = 0, msplit_rows_n: int = 0):
         t = self.tokenizer
         prompt = np.array(t.sot_sequence, np.int32)
         supp = np.array(t.suppress_tokens(), np.int32)
@@ -295,6 +298,9 @@ class WhisperEngine:
         opt.check_every = check_every
         opt.xattn_splits = xattn_splits
         opt.cu_count = cu_count
+        opt.state_slot = state_slot
+        opt.logits_blocks = logits_blocks
+        opt.msplit_rows_n = msplit_rows_n
         return opt, (prompt, supp)
 
     def decode(self, enc: torch.Tensor, max_length: int = 448, check_every: int = 16,
@@ -313,7 +319,8 @@ class WhisperEngine:
     def decode_ex(self, enc: torch.Tensor, prompts=None, max_length: int = 448,
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
                   cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None,
-                  pos_offset=None, steps: int = 0):
+                  pos_offset=None, steps: int = 0, state_slot: int = 0, logits_blocks: int = 0,
+                  msplit_rows_n: int = 0):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
@@ -323,7 +330,10 @@ class WhisperEngine:
         ``steps`` (greedy): a staggered call — row b runs ``steps`` positions from
         pos_offset[b]; rows with an offset > 0 continue this context's previous call in the
         same row (pass the same batch size and their encoder output again), rows with 0
-        start fresh (one contiguous range)."""
+        start fresh (one contiguous range). ``state_slot``: the context's decoder state slot
+        the call runs in (a sampled re-decode between two staggered calls takes another
+        slot); ``logits_blocks`` / ``msplit_rows_n``: launch geometry (0 = measured
+        defaults, janus_decode_options)."""
         B = enc.shape[0] if enc_index is None else len(enc_index)
         if steps < 0:
             raise ValueError("steps must be >= 0")
@@ -333,7 +343,8 @@ class WhisperEngine:
             if seeds is None or len(seeds) != B:
                 raise ValueError("sampling needs one uint32 seed per row")
             sd = np.ascontiguousarray(np.asarray(seeds, np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
-        opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count)
+        opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count,
+                                        state_slot, logits_blocks, msplit_rows_n)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
         po = None
@@ -378,11 +389,13 @@ class WhisperEngine:
         del keep, pr, ei, po
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 
-    def decode_stand(self, batch: int):
-        """Where each of the last decode call's ``batch`` row slots stands (the largest
-        pos_offset a staggered call may continue it from; janus_whisper_decode_stand)."""
+    def decode_stand(self, batch: int, state_slot: int = 0):
+        """Where each of the last decode call's ``batch`` row slots stands in decoder state
+        slot ``state_slot`` (the largest pos_offset a staggered call may continue it from;
+        janus_whisper_decode_stand_slot)."""
         out = np.zeros(batch, np.int32)
-        nat.call("janus_whisper_decode_stand", self._h, out.ctypes.data, int(batch))
+        nat.call("janus_whisper_decode_stand_slot", self._h, int(state_slot), out.ctypes.data,
+                 int(batch))
         return [int(v) for v in out]
 
     def decode_info(self):

@@ -183,8 +183,11 @@ def test_pipeline_fallback_matches_seek_loop(gpu):
     """The batched pipeline with faster-whisper's fallback (temperatures 0 ... 1.0, best_of
     5: every window of the seeded synthetic model fails at T = 0) settles each utterance
     exactly as the drop-in seek loop (generate_segments) does on the same 16 kHz audio:
-    same avg_logprob, temperature and number of sampled decodes; the overlapped serving
-    step, whose re-decodes run on the decoder's CU partition, gives the same packets."""
+    same avg_logprob, temperature, number of sampled decodes and seek after the window;
+    the overlapped serving step (re-decodes on the decoder's CU partition) and the
+    staggered (continuous-batching) step — whose failing windows leave the continuous
+    batch and re-decode on the whole GPU in decoder state slot 1 — give the same
+    packets, batch after batch."""
     from janus_amd.services.transcriber import TEMPERATURES, generate_segments
     pipe = JanusPipeline("tiny.en", max_length=12, temperatures=TEMPERATURES)
     utts = [synth_speech(500 + k, 2.0 + 3 * k) for k in range(3)]
@@ -195,8 +198,9 @@ def test_pipeline_fallback_matches_seek_loop(gpu):
     streams = generate_segments(pipe.whisper, [np.ascontiguousarray(u[::3]) for u in utts],
                                 max_length=12)
     for b, st in enumerate(streams):
-        needs0, skip, avg, cr, nsp, temp, ndec = res.gates[b]
+        needs0, skip, avg, cr, nsp, temp, ndec, seek = res.gates[b]
         assert st.windows == 1 and needs0 and ndec == st.fallback_decodes == 5
+        assert seek >= min(3000, len(utts[b][::3]) // 160)   # one window: its seek ends the clip
         if st.segments:
             assert st.segments[0].avg_logprob == avg and st.segments[0].temperature == temp == 1.0
     outs = [pipe.step_overlapped(pcm, offs, lengths, 16, 16, timestamp=5.0)]
@@ -205,5 +209,18 @@ def test_pipeline_fallback_matches_seek_loop(gpu):
     # flags, settled temperature and decode counts identical; the log-prob sums differ in
     # the last bits (the overlapped decoder runs 4 cross-attention key splits on 128 CUs)
     for g, r in zip(outs[1][0].gates, res.gates):
-        assert (g[0], g[1], g[3], g[5], g[6]) == (r[0], r[1], r[3], r[5], r[6])
+        assert (g[0], g[1], g[3], g[5], g[6], g[7]) == (r[0], r[1], r[3], r[5], r[6], r[7])
         assert abs(g[2] - r[2]) <= 1e-4 * abs(r[2]) and abs(g[4] - r[4]) <= 5e-3 * r[4] + 1e-9
+    # the staggered step: three batches in, each settled like the seek loop
+    got = []
+    for _ in range(3):
+        r = pipe.step_staggered(pcm, offs, lengths, 16, 16, timestamp=5.0)
+        if r[0] is not None:
+            got.append(r)
+    got += pipe.flush_staggered(16)
+    assert len(got) == 3
+    for r in got:
+        assert r[0].packets == res.packets
+        for g, q in zip(r[0].gates, res.gates):
+            assert (g[0], g[1], g[3], g[5], g[6], g[7]) == (q[0], q[1], q[3], q[5], q[6], q[7])
+            assert abs(g[2] - q[2]) <= 1e-4 * abs(q[2]) and abs(g[4] - q[4]) <= 5e-3 * q[4] + 1e-9

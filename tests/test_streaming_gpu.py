@@ -61,10 +61,13 @@ def tiny(gpu):
     return WhisperEngine(CONFIGS["tiny.en"], seed=0)
 
 
-def _streaming_case(gpu, w, S, ticks, per_tick, mode=None, gap_s=1.0, seed0=300, min_phrases=1):
+def _streaming_case(gpu, w, S, ticks, per_tick, mode=None, gap_s=1.0, seed0=300, min_phrases=1,
+                    max_length=8, temperatures=None, refs=None):
     from janus_amd.common.protocol import JanusMode
+    from janus_amd.services.transcriber import TEMPERATURES
     mode = JanusMode.SEMANTIC_VOICE if mode is None else mode
-    enc = StreamingEncoder(S, w, max_length=8, mode=mode)
+    enc = StreamingEncoder(S, w, max_length=max_length, mode=mode,
+                           temperatures=TEMPERATURES if temperatures is None else temperatures)
     total = ticks * per_tick * CHUNK
     audio = np.zeros((S, total), np.float32)
     for s in range(S):  # speech / silence / speech so phrases complete mid-run
@@ -86,6 +89,8 @@ def _streaming_case(gpu, w, S, ticks, per_tick, mode=None, gap_s=1.0, seed0=300,
         ref = segment(chunks, list(dec[s]), non_vad=[non_vad] * len(chunks))
         mine = [r for _, r in got if r["stream"] == s]
         assert len(mine) == len(ref), (s, len(mine), len(ref))
+        if refs is not None:
+            refs[s] = [ph for _, ph in ref]
         n_ph += len(ref)
         op = OracleProsody(48000)  # one stateful detector per channel
         for r, (_, ph) in zip(mine, ref):
@@ -108,6 +113,50 @@ def test_streaming_encoder_matches_oracle(gpu, tiny):
 def test_streaming_encoder_16_channels(gpu, tiny):
     """Config 5's per-GPU share: 16 channels of 320 ms blocks."""
     _streaming_case(gpu, tiny, S=16, ticks=14, per_tick=10, seed0=700, min_phrases=16)
+
+
+def test_streaming_16_channels_base_448(gpu):
+    """Config 5's per-GPU share at its real decode setting: base.en, max_length 448 (the
+    reference's default), 16 channels, T = 0. For channels 0 and 9: every phrase's text
+    equals the seek loop (generate_segments) on the oracle segmenter's phrase audio, and
+    the first window of every phrase decodes to the oracle's tokens (KV-cached fp32
+    decoder on the same encoder output) or diverges first at an oracle near-tie."""
+    from janus_amd.services.transcriber import generate_segments
+    from janus_amd.whisper import synthetic_weights
+    from oracle import whisper as ow
+    cfg = CONFIGS["base.en"]
+    w = WhisperEngine(cfg, seed=0)
+    refs = {}
+    got = _streaming_case(gpu, w, S=16, ticks=14, per_tick=10, seed0=900, min_phrases=16,
+                          max_length=448, temperatures=(0.0,), refs=refs)
+    W = synthetic_weights(cfg, 0)
+    tk = w.tokenizer
+    plen = len(tk.sot_sequence)
+    checked = 0
+    for s in (0, 9):
+        mine = [r for _, r in got if r["stream"] == s]
+        phrases = refs[s]
+        auds = [np.ascontiguousarray(ph[::3]) for ph in phrases]
+        sts = generate_segments(w, auds, max_length=448, temperatures=(0.0,))
+        for r, st in zip(mine, sts):
+            assert r["text"] == " ".join(sg.text.strip() for sg in st.segments).strip()
+        # first windows: the GPU decoder vs the oracle decoder on the GPU encoder output
+        pcm = torch.from_numpy(np.concatenate(phrases + [np.zeros(1, np.float32)])).to(gpu)
+        offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in phrases])]),
+                            dtype=torch.int64, device=gpu)
+        enc = w.encode(w.logmel(pcm, offs, len(phrases), 3))
+        dec = w.decode_ex(enc, max_length=448)
+        toks, nt = dec.tokens.cpu().numpy(), dec.n_tokens.cpu().numpy()
+        ref = ow.greedy_cached(enc.float().cpu(), W, cfg, tk, 448, no_speech=50361)
+        for b, rr in enumerate(ref):
+            g = [int(t) for t in toks[b][plen:plen + int(nt[b])]]
+            if g != rr["tokens"]:
+                first = next((i for i in range(min(len(g), len(rr["tokens"])))
+                              if g[i] != rr["tokens"][i]), min(len(g), len(rr["tokens"])))
+                margin = rr["margins"][first] if first < len(rr["margins"]) else 0.0
+                assert margin < 2e-3, (s, b, first, margin)
+            checked += 1
+    assert checked >= 4
 
 
 def test_streaming_two_phrases_one_push(gpu, tiny):
