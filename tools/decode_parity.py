@@ -5,6 +5,13 @@ Prints one JSON line: per utterance the GPU / oracle token counts, whether the w
 sequence matches, the first divergence and the oracle's top-2 margin there, and whether
 the MessagePack packet built from each transcript matches. Usage (GPU box):
   python tools/decode_parity.py [--model base.en] [--n 6] [--max-length 448]
+  python tools/decode_parity.py --bench 32     # the bench's own rows through its decode
+--bench N: the first N utterances of bench.py's config-4 workload (30 s, seeds 4000 + i,
+weights seed 0) decoded exactly as the headline step decodes them — JanusPipeline.
+step_staggered (two slot sets, 224 positions per call, the decoder's CU-masked stream) —
+against the oracle on the same encoder output; adds the token-agreement rate (positions
+before the first divergence / tokens) and the packets (oracle detokeniser + packer on
+each side's tokens).
 """
 import argparse
 import json
@@ -51,8 +58,67 @@ def compare(eng, W, cfg, enc, max_length):
     return rows, t_oracle
 
 
+def bench_rows(n, max_length):
+    """--bench: the headline step's decode of the bench's first n utterances vs the oracle."""
+    from janus_amd.pipeline import JanusPipeline
+    cfg = CONFIGS["base.en"]
+    W = synthetic_weights(cfg, 0)
+    pipe = JanusPipeline("base.en", max_length=max_length, temperatures=(0.0,))
+    dev = pipe.device
+    utts = [synth_speech(4000 + i, 30.0) for i in range(n)]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=dev)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
+    frames = 64
+    outs = []
+    for _ in range(2):   # the same batch twice: the second batch enters beside the first
+        r = pipe.step_staggered(pcm, offs, lengths, frames)
+        if r[0] is not None:
+            outs.append(r[0])
+    outs += [r[0] for r in pipe.flush_staggered(frames)]
+    res = outs[0]
+    w = pipe.whisper
+    enc = w.encode(w.logmel(pcm, offs, n, 3))
+    tk = w.tokenizer
+    plen = len(tk.sot_sequence)
+    toks, nt = res.tokens.cpu().numpy(), res.n_tokens.cpu().numpy()
+    t0 = time.time()
+    ref = ow.greedy_cached(enc.float().cpu(), W, cfg, tk, max_length)
+    t_oracle = time.time() - t0
+    tags = {"energy": "Normal", "pitch": "High"}
+    rows = []
+    agree = total = 0
+    for b in range(n):
+        g = [int(t) for t in toks[b][plen:plen + int(nt[b])]]
+        r = ref[b]["tokens"]
+        first = next((i for i in range(min(len(g), len(r))) if g[i] != r[i]),
+                     None if len(g) == len(r) else min(len(g), len(r)))
+        agree += len(r) if first is None else first
+        total += len(r)
+        rows.append(dict(gpu_len=len(g), ref_len=len(r), match=g == r, first_diff=first,
+                         margin_at_diff=(ref[b]["margins"][first] if first is not None and
+                                         first < len(ref[b]["margins"]) else None),
+                         min_margin=float(min(ref[b]["margins"])) if ref[b]["margins"] else None,
+                         packet_match=opk.serialize(tk.transcript(g), 0, tags, "auto", 1.0) ==
+                         opk.serialize(tk.transcript(r), 0, tags, "auto", 1.0),
+                         # the transcript the pipeline packed is the GPU tokens' transcript
+                         text_is_tokens=res.texts[b] == tk.transcript(g)))
+    same_twice = all(np.array_equal(outs[0].tokens.cpu().numpy(), o.tokens.cpu().numpy()) for o in outs[1:])
+    margins = [r["margin_at_diff"] for r in rows if r["margin_at_diff"] is not None]
+    return dict(model="base.en", n=n, max_length=max_length, path="JanusPipeline.step_staggered",
+                oracle_s=round(t_oracle, 1),
+                seq_match_rate=float(np.mean([r["match"] for r in rows])),
+                packet_match_rate=float(np.mean([r["packet_match"] for r in rows])),
+                token_agreement_rate=agree / max(total, 1),
+                first_divergence_margins=margins,
+                max_margin_at_divergence=max(margins) if margins else None,
+                batches_identical=bool(same_twice), rows=rows)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--bench", type=int, default=0,
+                    help="N > 0: the bench's first N utterances through the headline step")
     ap.add_argument("--model", default="base.en")
     ap.add_argument("--n", type=int, default=6)
     ap.add_argument("--max-length", type=int, default=448)
@@ -60,6 +126,9 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also oracle front end + encoder")
     a = ap.parse_args()
     torch.set_num_threads(min(16, os.cpu_count() or 1))
+    if a.bench > 0:
+        print(json.dumps(bench_rows(a.bench, a.max_length)), flush=True)
+        return
     cfg = CONFIGS[a.model]
     W = synthetic_weights(cfg, a.seed)
     eng = WhisperEngine(cfg, W)

@@ -1,10 +1,14 @@
 #!/bin/bash
-# bench A/B over env settings / builds: tools/gpu_ab_env.sh tag default env:A=1,B=2 lib:libx.so ...
-# (env: comma-separated NAME=VALUE pairs applied to the in-tree lib)
+# bench A/B over env settings / builds, timed steps only (--no-idle-latency):
+#   tools/gpu_ab_env.sh tag default env:A=1,B=2 lib:libx.so ...
+# (env: comma-separated NAME=VALUE pairs; lib: an alternative in-tree build, JANUS_LIB)
+# AB_REPS rounds (default 2), AB_STEPS timed steps (default 5). One line per run:
+# variant, ms/step, mean vocoder / decoder side, conv avg launch ms.
 set -o pipefail
 mkdir -p gpurun_out
 tag=$1; shift
 reps=${AB_REPS:-2}
+steps=${AB_STEPS:-5}
 for rep in $(seq $reps); do
 for v in "$@"; do
   unset JANUS_LIB
@@ -15,8 +19,13 @@ for v in "$@"; do
     lib:*) export JANUS_LIB="${v#lib:}" ;;
   esac
   name=$(echo "$v" | tr -c 'A-Za-z0-9_=.\n' '_')
-  env $envs JANUS_OVERLAP_TIMING=1 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline \
-    > gpurun_out/ab_${tag}_$name.json 2> gpurun_out/ab_${tag}_$name.err || { tail -5 gpurun_out/ab_${tag}_$name.err; exit 1; }
-  echo "$v $(python -c "import json;d=json.load(open('gpurun_out/ab_${tag}_$name.json'));print(d['ms_per_step'], d['step_ms'], d['roofline']['avg_launch_ms'])") $(grep overlap gpurun_out/ab_${tag}_$name.err | tail -1)"
+  out=gpurun_out/ab_${tag}_${name}_$rep
+  env $envs timeout -k 10 300 python -u bench.py --steps $steps --warmup 2 --no-cpu-baseline --no-idle-latency \
+    > $out.json 2> $out.err || { tail -5 $out.err; exit 1; }
+  echo "$v $(python3 -c "
+import json; d=json.load(open('$out.json'))
+s=d['side_ms'] or {}
+m=lambda k: round(sum(s.get(k,[0]))/max(len(s.get(k,[1])),1),1)
+print(d['ms_per_step'], 'voc', m('vocoder'), 'dec', m('decoder'), 'conv', d['roofline']['avg_launch_ms'], 'yin', d.get('yin_dec_utts'), 'lpp', (d['roofline'].get('decoder') or {}).get('launches_per_position'))")"
 done
 done
