@@ -101,10 +101,14 @@ struct XGeo {
 // window): rows 0-7 are row b0's heads, rows 8-15 row b1's (H <= 8; b1 < 0: none), and
 // the block reads encoder row e once for both — where the one-row form pads 8 heads to 16
 // MFMA rows and reads E once per decoder row. pairs[blockIdx.y] = {b0, b1, e, -}.
-template <int D, int CH, bool PAIR = false>
+// DIRECT (one key split, r05): the block holds the whole softmax of its row, so it writes
+// c[b][h*D + j] = C / l in fp16 itself (the merge's arithmetic at one split: weight
+// exp2(m - m) = 1, L = l, c = C * (1 / L)) and no merge launch follows.
+template <int D, int CH, bool PAIR = false, bool DIRECT = false>
 __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
-    float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs) {
+    float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
+    _Float16* __restrict__ out = nullptr) {
   using G = XGeo<D, CH>;
   constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT, NW = G::NW,
                 NKT = G::NKT, HPW = G::HPW;
@@ -240,6 +244,27 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
     __syncthreads();  // sE / sS / sP are rewritten by the next chunk
   }
 
+  if constexpr (DIRECT) {
+    // 1 / l per head through LDS (the softmax waves own the heads), then c = C * (1 / l)
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < HPW; ++i) {
+        const int h = w + NW * i;
+        if (h < H) sA[h] = 1.0f / fmaf(1.0f, l_run[i], 0.0f);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * lg + r;
+      if (row >= H) continue;
+      const float il = sA[row];
+      _Float16* o = out + ((int64_t)b * H + row) * D;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) o[w * (D / NW) + 16 * n + lr] = (_Float16)(fmaf(1.0f, accc[n][r], 0.0f) * il);
+    }
+    return;
+  }
   // ---- per-split partials: C of the valid rows (fp32), (m, l) per head
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -720,18 +745,22 @@ int xattn_split_count(int Te, int requested) {
 
 template <int D, int CH>
 static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
-                      float* part_c, float* part_ml, hipStream_t s, const int4* pairs, int npairs) {
+                      float* part_c, float* part_ml, hipStream_t s, const int4* pairs, int npairs,
+                      _Float16* out = nullptr) {
   const int chunks = (Te + CH - 1) / CH;
   const int kps = (chunks + nsplit - 1) / nsplit * CH;
-  auto kern = pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
-  static bool attr[2] = {false, false};
-  if (!attr[pairs != nullptr]) {
+  const bool direct = out != nullptr;
+  auto kern = direct ? xattn_kernel<D, CH, false, true>
+              : pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
+  const int ai = direct ? 2 : pairs != nullptr;
+  static bool attr[3] = {false, false, false};
+  if (!attr[ai]) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
-    attr[pairs != nullptr] = true;
+    attr[ai] = true;
   }
   kern<<<dim3(nsplit, pairs ? npairs : B), CH * 8, XGeo<D, CH>::LDS, s>>>(qk, enc, Te, H, kps, part_c,
-                                                                         part_ml, pairs);
+                                                                         part_ml, pairs, out);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -748,6 +777,12 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   JANUS_CHECK(!pairs || (H <= 8 && npairs >= 1 && D <= 512), "xattn: row pairs need H <= 8, D <= 512");
   // 64-key chunks (8 waves) unless JANUS_XATTN_CH32
   static const bool ch32 = std::getenv("JANUS_XATTN_CH32") != nullptr;
+  // one key split with the merge requested: the kernel writes c itself (DIRECT), no merge
+  if (combine && nsplit == 1 && !pairs && !ch32 && D <= 512) {
+    if (D == 384) xattn_cfg<384, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out);
+    else xattn_cfg<512, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out);
+    return;
+  }
   if (D == 384) {
     if (ch32) xattn_cfg<384, 32>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);
     else xattn_cfg<384, 64>(qk, enc, B, Te, H, nsplit, part_c, part_ml, s, pairs, npairs);

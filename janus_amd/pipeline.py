@@ -490,9 +490,12 @@ class JanusPipeline:
         dec = None
         if pcm is not None or any(x is not None for x in st["sets"]):
             with torch.cuda.stream(ds):
-                # cross-attention at 2 key splits: with 2 x 64 rows the grid fills the
-                # decoder's CUs without the split (4: decoder side 252.6-255.3 ms, 2:
-                # 246.7-248.6, 8: 264.7-266.7, one box)
+                # cross-attention at ONE key split (r05): with 2 x 64 rows the grid fills the
+                # decoder's CUs without splitting the keys, and at one split the kernel writes
+                # its output itself (no merge launch: 81 -> 75 launches per position; decoder
+                # side 246.2 / 244.4 -> 243.8 / 242.0 ms in two same-box rounds,
+                # profiles/r05_xattn_split1_ab.txt; r04: 4 splits 252.6-255.3, 2 246.7-248.6,
+                # 8 264.7-266.7 ms)
                 # the decoder side's YIN runs concurrently with the decode call, on a second
                 # stream over the decoder's CUs with its grid capped at JANUS_YIN_BESIDE
                 # blocks (default 128; 0: after the call): the latency-bound decoder leaves
@@ -511,7 +514,7 @@ class JanusPipeline:
                         except Exception:  # engine.py:520-525
                             pd = None
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
-                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "2")),
+                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "1")),
                                   cu_count=self._dec_s.n_cus)
                 if beside:
                     ds.wait_stream(ys)

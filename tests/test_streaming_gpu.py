@@ -127,7 +127,9 @@ def test_streaming_16_channels_base_448(gpu):
     cfg = CONFIGS["base.en"]
     w = WhisperEngine(cfg, seed=0)
     refs = {}
-    got = _streaming_case(gpu, w, S=16, ticks=14, per_tick=10, seed0=900, min_phrases=16,
+    # 20 ticks of 320 ms: both phrases of every channel complete (the second needs 15 silent
+    # chunks after it)
+    got = _streaming_case(gpu, w, S=16, ticks=20, per_tick=10, seed0=900, min_phrases=32,
                           max_length=448, temperatures=(0.0,), refs=refs)
     W = synthetic_weights(cfg, 0)
     tk = w.tokenizer
