@@ -249,6 +249,12 @@ typedef struct {
   int logits_blocks;       /* vocabulary-projection blocks (0 = cu_count) */
   int msplit_rows_n;       /* skinny projections split rows over blocks up to this N
                               (0 = auto: 1024 on <= 128 CUs, else none; -1 = never) */
+  int persistent;          /* 1: the launches between a layer's self- and cross-attention
+                              run as two resident-grid launches with in-launch barriers
+                              (d_model 512, 8 heads, <= 128 rows, >= 16 CUs per 16 rows; the
+                              other shapes keep the launch path): 29 launches per position
+                              at base.en instead of 75. Same arithmetic per row except the
+                              GEMMs' k order (fp32-rounding level, not bit-identical to 0) */
 } janus_decode_options;
 
 /*

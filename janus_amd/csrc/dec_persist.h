@@ -1,0 +1,39 @@
+// Persistent decoder segments (dec_persist.hip): the launches between a layer's self- and
+// cross-attention (segment A) and between its cross-attention and the next layer's
+// self-attention (segment B) as resident grids with in-launch barriers.
+#pragma once
+#include "common.h"
+
+namespace janus {
+
+struct DecSegArgs {
+  int B, MT;                 // rows (<= 128), 16-row tiles (power of two >= B / 16)
+  float* x;                  // [B][512] fp32 residual stream (read-modify-write)
+  // segment A: x += o Wo^T + bo; xqk = LN2(x) Wqk^T + bqk
+  const _Float16* o; const _Float16* wo; const float* bo;
+  const float* ln2g; const float* ln2b;
+  const _Float16* wqk; const float* bqk; _Float16* xqk;     // xqk [B][8 * 512]
+  // segment B: o' = c_h Wv_h^T + bv; x += o' Wo_c^T + bo_c; f = gelu(LN3(x) W1^T + b1);
+  // x += f W2^T + b2; [wqkv != null] q, K/V = LN1'(x) Wqkv'^T + bqkv'
+  const _Float16* xc;                                        // [B][8 * 512] (cross-attention)
+  const _Float16* wv; const float* bv; _Float16* omid;       // omid [B][512] scratch
+  const _Float16* woc; const float* boc;
+  const float* ln3g; const float* ln3b;
+  const _Float16* w1; const float* b1; _Float16* f;          // f [B][2048] scratch
+  const _Float16* w2; const float* b2;
+  const float* ln1g; const float* ln1b;                      // the NEXT layer's
+  const _Float16* wqkv; const float* bqkv; _Float16* qkv;    // qkv [B][1536] (q part)
+  _Float16* kc; _Float16* vc; int pos, n_ctx; const int32_t* roff;  // the next layer's cache
+  unsigned* bar;             // 160 zeroed words (barrier counters, self-cleaning)
+  unsigned* err;             // timeout flag (host-checked)
+};
+
+// 16-row tiles for B rows (0: unsupported, B > 128)
+int dec_seg_mtiles(int B);
+// blocks of the resident grid on a partition of `cus` CUs (0: unsupported)
+int dec_seg_grid(int B, int cus);
+bool dec_seg_supported(int d, int H, int B, int cus);
+void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s);
+void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s);
+
+}  // namespace janus

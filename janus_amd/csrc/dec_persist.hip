@@ -1,0 +1,496 @@
+// Persistent decoder segments (r05): the greedy decoder's small launches between the two
+// attention kernels of a layer, as two resident-grid launches with grid barriers.
+//
+// Whisper's decoder layer (faster-whisper / CTranslate2 greedy step, transcriber.py:53-57;
+// the absorbed cross-attention of xattn.hip) per position, rows = the decode batch:
+//   self-attention launch -> o
+//   SEGMENT A:  x += o Wo^T + bo                      (split-K GEMM, residual epilogue)
+//               | grid barrier
+//               xqk = LN2(x) Wqk^T + bqk              (LayerNorm in the block + GEMM)
+//   cross-attention launch (one key split: writes c = softmax(qk enc^T) enc itself)
+//   SEGMENT B:  o' = c_h Wv_h^T + bv  (per head)      (split-K, block-diagonal A)
+//               | x += o' Wo_c^T + bo_c               (split-K, residual)
+//               | f = gelu(LN3(x) W1^T + b1)          (LayerNorm + GEMM)
+//               | x += f W2^T + b2                    (split-K, K = 4d)
+//               | [next layer] q, K/V[pos] = LN1(x) Wqkv^T + bqkv   (LayerNorm + GEMM)
+// which replaces ten launches per layer (O, LN2, qk, value projection, cross O, LN3, fc1,
+// fc2, LN1, QKV) by two: 75 -> 29 launches per position at base.en.
+//
+// What a resident grid buys over launch boundaries (MI355X_MICROARCH.md price list,
+// phase-in-launch / prefetch-credit): no per-launch fill and drain, and each phase's WEIGHT
+// fragments (independent of the activations) are loaded into registers while the previous
+// phase finishes, so after the barrier a phase waits only for its (small, L2/MALL-served)
+// activation rows. Hand-offs follow the guide's R1 form (cdna_hip_programming.md §6
+// Guideline 16): every handed-off byte is stored write-through (sc1 buffer stores), every
+// storing wave drains (s_waitcnt vmcnt(0)) before its block arrives at the barrier, and
+// every load of a handed-off byte is an sc1 load. The barrier is two-level (one arrival
+// counter per XCD group on its own 64-byte line, the group's last arriver bumps the top
+// counter; one lane polls the top counter relaxed with s_sleep), spins are bounded (a
+// timeout sets the error word and the kernel runs to its end), and the last block to leave
+// zeroes every counter for the next launch (self-cleaning: nothing to memset per call).
+//
+// Numerics: LayerNorm with layernorm_kernel's arithmetic (ln_sum4 / ln_sq4 / ln_norm4);
+// split-K partials summed in a fixed order ((k0 + k1) + k2) + k3 independent of the grid
+// and of the rows' neighbours, so a row's result does not depend on the batch it rides in
+// (the staggered decode's bit-identity). The GEMMs' k order differs from the launch path's
+// 16-wave split (gemm_skinny_kernel), so the two paths agree to fp32 rounding, not bits.
+#include "mfma.h"
+#include "kernels.h"
+#include "dec_persist.h"
+
+namespace janus {
+
+namespace {
+
+constexpr int kD = 512;            // d_model (base.en); LayerNorm / residual width
+constexpr int kNT = 512;           // threads per block: 8 waves
+constexpr int kAP = frag_pitch(kD);  // LDS row pitch of the normalised A tile (halves)
+constexpr unsigned kSpinLimit = 1u << 22;  // ~0.5 s of s_sleep polls before giving up
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  // raw buffer: out-of-range loads return 0 and out-of-range stores are dropped, so rows
+  // past the batch need no guards
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+// sc1: agent-coherent, L1-bypassing (write-through stores) — the R1 hand-off flavour
+__device__ __forceinline__ u32x4v ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ void st_sc1(u32x4v v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void st_sc1_8(u32x2v v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 16);
+}
+__device__ __forceinline__ half8 as_h8(u32x4v v) { return __builtin_bit_cast(half8, v); }
+// an opaque copy of a value: the compiler cannot prove two phases' copies equal, so it
+// recomputes per-phase addresses instead of keeping them live across the whole launch
+template <class T>
+__device__ __forceinline__ T opaque(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ float4 as_f4(u32x4v v) { return __builtin_bit_cast(float4, v); }
+
+// Grid barrier `epoch` (1, 2, ... within the launch). Every wave drains its stores first
+// (the sc1 payload is in memory), then lane 0 of the block arrives on its XCD group's
+// counter; the group's last arriver bumps the top counter; lane 0 polls the top counter.
+// bar: [0] top, [16 * (1 + g)] group g (g < 8), [16 * 9] exit — 64-byte lines.
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned epoch, unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x, g = blockIdx.x & 7;
+    const unsigned ng = G < 8 ? G : 8;
+    const unsigned gsz = G / 8 + (g < G % 8 ? 1u : 0u);
+    const unsigned old = __hip_atomic_fetch_add(bar + 16 * (1 + g), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == epoch * gsz - 1)
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch * ng) {
+      __builtin_amdgcn_s_sleep(2);
+      // a block never arrived: give up and flag it; once flagged (this launch or an
+      // earlier one of the call) nobody waits again, so a broken call ends quickly
+      if (++spins > kSpinLimit ||
+          ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// The last block to leave zeroes the counters (every block has passed every wait by then).
+__device__ __forceinline__ void grid_exit(unsigned* bar) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(bar + 16 * 9, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int g = 0; g < 8; ++g)
+        __hip_atomic_store(bar + 16 * (1 + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 16 * 9, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ split-K phase
+// out[R][512] from A[R][K] . W[512][K]^T: tiles of 16 rows x 16 columns, each over K in
+// four quarters (one wave per quarter), two tiles per block (8 waves); pair p of the
+// phase: tiles 2p, 2p + 1, tile t -> (m = t % MT, n = t / MT). KSW = k-steps per quarter.
+// GROUP: block-diagonal A (output columns [64h, 64h + 64) read A columns [512h, 512h + 512):
+// the per-head value projection).
+template <int KSW>
+struct SplitW {
+  half8 w[KSW];
+};
+
+template <int KSW>
+__device__ __forceinline__ void splitk_prefetch(SplitW<KSW>& W, const _Float16* wt, int K,
+                                                int pair, int MT, int lane, int wv) {
+  const int t = 2 * pair + (wv >> 2), kp = wv & 3;
+  const int n = t / MT;
+  const _Float16* wr = wt + (int64_t)(16 * n + (lane & 15)) * K + kp * (K / 4) + 8 * (lane >> 4);
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) W.w[s] = *reinterpret_cast<const half8*>(wr + 32 * s);
+}
+
+enum SegEpi { SE_RESID = 0, SE_F16_SC1 = 1 };
+
+// one pair of tiles: the waves' products, the fixed-order reduction, the epilogue. pre():
+// the NEXT phase's weight loads, issued right after this pair's MFMAs so they are in
+// flight during the reduction and the epilogue (the barrier's drain then finds them done)
+template <int KSW, int EPI, bool GROUP, class Pre>
+__device__ __forceinline__ void splitk_pair(const SplitW<KSW>& W, int pair, int MT, int K,
+                                            __amdgpu_buffer_rsrc_t ra, int lda,
+                                            const float* bias,
+                                            __amdgpu_buffer_rsrc_t rx,  // SE_RESID: x [B][512] f32
+                                            __amdgpu_buffer_rsrc_t ro,  // SE_F16_SC1: out [B][512]
+                                            float* red, int lane, int wv, bool last, Pre&& pre) {
+  const int tsub = wv >> 2, kp = wv & 3;
+  const int t = 2 * pair + tsub;
+  const int m = t % MT, n = t / MT;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const int acol = (GROUP ? (16 * n / 64) * kD : 0) + kp * (K / 4) + kc8;
+  const uint32_t abase = (uint32_t)(((16 * m + lr) * lda + acol) * 2);
+  f32x4 acc = zero_f32x4();
+  // A in halves of at most 8 k-steps (K = 4d: 64 + 32 registers, not 64 + 64)
+  constexpr int H = KSW > 8 ? 8 : KSW;
+#pragma unroll
+  for (int h0 = 0; h0 < KSW; h0 += H) {
+    half8 a[H];
+#pragma unroll
+    for (int s = 0; s < H; ++s) a[s] = as_h8(ld_sc1(ra, abase + 64 * (h0 + s)));
+#pragma unroll
+    for (int s = 0; s < H; ++s) acc = mfma16(a[s], W.w[h0 + s], acc);
+    // the second half's loads stay below the first half's MFMAs (hoisted, all 16 A
+    // fragments plus the 16 weight fragments would need 128 registers)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the next phase's loads below the MFMAs
+  if (last) pre();
+  __builtin_amdgcn_sched_barrier(0);
+  // red[tsub][kp][16][17]
+  float* rp = red + (tsub * 4 + kp) * 16 * 17;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rp[(4 * (lane >> 4) + r) * 17 + lr] = acc[r];
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < 128) {
+    const int es = tid >> 6, q = tid & 63;
+    const int et = 2 * pair + es;
+    const int em = et % MT, en = et / MT;
+    const int row = q >> 2, c4 = 4 * (q & 3);
+    const float* r0 = red + (es * 4) * 16 * 17 + row * 17 + c4;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s = r0[i] + r0[16 * 17 + i];
+      s += r0[2 * 16 * 17 + i];
+      s += r0[3 * 16 * 17 + i];
+      v[i] = s + bias[16 * en + c4 + i];
+    }
+    const uint32_t eoff = (uint32_t)((16 * em + row) * kD + 16 * en + c4);
+    if constexpr (EPI == SE_RESID) {
+      const float4 xv = as_f4(ld_sc1(rx, eoff * 4));
+      const float4 y = make_float4(xv.x + v[0], xv.y + v[1], xv.z + v[2], xv.w + v[3]);
+      st_sc1(__builtin_bit_cast(u32x4v, y), rx, eoff * 4);
+    } else {
+      const half4 h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      st_sc1_8(__builtin_bit_cast(u32x2v, h), ro, eoff * 2);
+    }
+  }
+  __syncthreads();  // red is reused by the next pair
+}
+
+// ------------------------------------------------------------ LayerNorm + GEMM phase
+// out[R][N] = epi(LN(x) W[N][512]^T + b): block -> (m-tile, group of NPG 16-column tiles);
+// the block normalises its 16 rows into LDS (layernorm_kernel's arithmetic), each wave
+// computes whole-K tiles of the group (up to two prefetched).
+struct LngW {
+  half8 w[16];
+};
+
+__device__ __forceinline__ void lng_tiles(int N, int MT, int& m, int& nt0, int& npg) {
+  const int b = blockIdx.x, G = gridDim.x;
+  const int j = b >> 3, xcd = b & 7;
+  const int NG = G / MT;
+  m = j % MT;
+  const int g = xcd + 8 * (j / MT);
+  npg = (N / 16) / NG;
+  nt0 = g * npg;
+}
+
+__device__ __forceinline__ void lng_load(half8 (&w)[16], const _Float16* wt, int nt, int lane) {
+  const _Float16* wr = wt + (int64_t)(16 * nt + (lane & 15)) * kD + 8 * (lane >> 4);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) w[s] = *reinterpret_cast<const half8*>(wr + 32 * s);
+}
+
+// the wave's first tile of the phase (the rest are loaded during the phase)
+__device__ __forceinline__ void lng_prefetch(LngW& W, const _Float16* wt, int N, int MT,
+                                             int lane, int wv) {
+  int m, nt0, npg;
+  lng_tiles(N, MT, m, nt0, npg);
+  if (wv < npg) lng_load(W.w, wt, nt0 + wv, lane);  // wave-uniform
+}
+
+enum LngEpi { LE_F16 = 0, LE_GELU_SC1 = 1, LE_QKV = 2 };
+
+struct LngOut {
+  _Float16* out; int ldo;                  // LE_F16 / LE_GELU_SC1 / q part of LE_QKV
+  _Float16* kc; _Float16* vc; int pos, n_ctx; const int32_t* roff;  // LE_QKV
+};
+
+template <int EPI, class Pre>
+__device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, int MT,
+                                          int B, __amdgpu_buffer_rsrc_t rx, const float* g,
+                                          const float* bt, const float* bias,
+                                          const LngOut& o, _Float16* sA, float* patch_all, int lane,
+                                          int wv, Pre&& pre) {
+  int m, nt0, npg;
+  lng_tiles(N, MT, m, nt0, npg);
+  // ---- LayerNorm of rows 16m + 2wv, 16m + 2wv + 1 (sc1 loads: x was just handed off),
+  // one row at a time and gamma / beta loaded at their use: the phase's weight fragments
+  // are in flight in 64 registers meanwhile
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int lrow = 2 * wv + j;
+    float4 v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      v[k] = as_f4(ld_sc1(rx, (uint32_t)(((16 * m + lrow) * kD + 4 * (lane + 64 * k)) * 4)));
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) s += ln_sum4(v[k]);
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    const float mean = s / kD;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) q += ln_sq4(v[k], mean);
+    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+    const float rstd = rsqrtf(q / kD + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float4 gg = reinterpret_cast<const float4*>(g)[lane + 64 * k];
+      const float4 bb = reinterpret_cast<const float4*>(bt)[lane + 64 * k];
+      *reinterpret_cast<half4*>(sA + lrow * kAP + 4 * (lane + 64 * k)) = ln_norm4(v[k], mean, rstd, gg, bb);
+    }
+  }
+  __syncthreads();
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  float* patch = patch_all + wv * 16 * 17;
+  // the wave's tiles li = wv, wv + 8, ...; the last one peeled so pre() (the next phase's
+  // weights) sits after the loop in straight-line code: inside it, its registers would be
+  // live across every iteration
+  const int ntile = wv < npg ? (npg - wv + 7) / 8 : 0;
+  auto tile = [&](int li, bool last) __attribute__((always_inline)) {
+    const int nt = nt0 + li;
+    f32x4 acc = zero_f32x4();
+    half8 a[2];
+    a[0] = *reinterpret_cast<const half8*>(sA + lr * kAP + kc8);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s + 1 < 16) a[(s + 1) & 1] = *reinterpret_cast<const half8*>(sA + lr * kAP + 32 * (s + 1) + kc8);
+      acc = mfma16(a[s & 1], W.w[s], acc);
+    }
+    // the next tile's weights (or the next phase's) in flight during this epilogue
+    // (scheduling barriers: hoisted above the MFMAs, the loads' registers would overlap
+    // this tile's weights)
+    __builtin_amdgcn_sched_barrier(0);
+    if (!last) lng_load(W.w, wt, nt + 8, lane);
+    else pre();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) patch[(4 * (lane >> 4) + r) * 17 + lr] = acc[r];
+    // wave-private patch: own stores visible to own loads in order
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    const int row = lane >> 2, c4 = 4 * (lane & 3);
+    const int grow = 16 * m + row, col = 16 * nt + c4;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = patch[row * 17 + c4 + i] + bias[col + i];
+    if (grow < B) {
+      if constexpr (EPI == LE_GELU_SC1) {
+        const half4 h = {(_Float16)gelu_erf(v[0]), (_Float16)gelu_erf(v[1]), (_Float16)gelu_erf(v[2]),
+                         (_Float16)gelu_erf(v[3])};
+        st_sc1_8(__builtin_bit_cast(u32x2v, h), rsrc(o.out, (uint32_t)B * o.ldo * 2),
+                 (uint32_t)((grow * o.ldo + col) * 2));
+      } else {
+        const half4 h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        _Float16* dst;
+        if constexpr (EPI == LE_QKV) {
+          if (col < kD) {
+            dst = o.out + (int64_t)grow * o.ldo + col;
+          } else {
+            _Float16* cache = col < 2 * kD ? o.kc : o.vc;
+            const int cpos = o.pos + (o.roff ? o.roff[grow] : 0);
+            dst = cache + ((int64_t)grow * o.n_ctx + cpos) * kD + (col % kD);
+          }
+        } else {
+          dst = o.out + (int64_t)grow * o.ldo + col;
+        }
+        *reinterpret_cast<half4*>(dst) = h;
+      }
+    }
+    // the patch is rewritten by the next tile: LDS operations of one wave run in order
+  };
+  for (int i = 0; i + 1 < ntile; ++i) tile(wv + 8 * i, false);
+  if (ntile > 0) tile(wv + 8 * (ntile - 1), true);
+  else pre();  // no tile for this wave
+  (void)N;
+}
+
+// one pair per block: the grid always has at least 16 * MT blocks (dec_seg_grid)
+template <int KSW, int EPI, bool GROUP, class Pre>
+__device__ __forceinline__ void splitk_phase(const SplitW<KSW>& W, const _Float16* wt, int K,
+                                             int MT, __amdgpu_buffer_rsrc_t ra, int lda,
+                                             const float* bias, __amdgpu_buffer_rsrc_t rx,
+                                             __amdgpu_buffer_rsrc_t ro, float* red, int lane, int wv,
+                                             Pre&& pre) {
+  const int p0 = blockIdx.x;
+  if (p0 >= 16 * MT) { pre(); return; }  // 32 column tiles x MT row tiles / 2
+  splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre);
+  (void)wt;
+}
+
+}  // namespace
+
+// LDS: split-K reduction [2][4][16][17] f32 | LN tile [16][kAP] f16 | wave patches [8][16][17]
+constexpr int kRedF = 2 * 4 * 16 * 17;
+constexpr int kPatchF = 8 * 16 * 17;
+constexpr size_t kSegLds = (size_t)kRedF * 4 + (size_t)16 * kAP * 2 + (size_t)kPatchF * 4;
+
+// 128 VGPRs (four waves per SIMD): two blocks fit a CU, so a CU already holding other
+// blocks (the YIN grid beside the decoder) still takes one and the grid stays co-resident.
+// Each phase issues its weight loads first, right after the barrier, so they are in flight
+// together with the phase's activation loads (sc1) — carrying them ACROSS the barrier in
+// registers measured no faster in this shape (the activation round trip follows the
+// barrier anyway) and cost the register budget.
+__global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  float* red = seg_smem;
+  _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
+  float* patch = reinterpret_cast<float*>(sA + 16 * kAP);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  const int B = a.B, MT = a.MT;
+  const auto rx = rsrc(a.x, (uint32_t)B * kD * 4);
+  const bool first = (int)blockIdx.x < 16 * MT;
+  // phase 1: x += o Wo^T + bo (o from the self-attention launch)
+  {
+    SplitW<4> w;
+    if (first) splitk_prefetch<4>(w, a.wo, kD, blockIdx.x, MT, lane, wv);
+    splitk_phase<4, SE_RESID, false>(w, a.wo, kD, MT, rsrc(a.o, (uint32_t)B * kD * 2), kD, a.bo, rx, rx,
+                                     red, lane, wv, [] {});
+  }
+  grid_barrier(a.bar, 1, a.err);
+  // phase 2: xqk = LN2(x) Wqk^T + bqk (read by the cross-attention launch)
+  {
+    LngW w;
+    lng_prefetch(w, a.wqk, 8 * kD, MT, lane, wv);
+    LngOut o{a.xqk, 8 * kD, nullptr, nullptr, 0, 0, nullptr};
+    lng_phase<LE_F16>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {});
+  }
+  grid_exit(a.bar);
+}
+
+__global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  float* red = seg_smem;
+  _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
+  float* patch = reinterpret_cast<float*>(sA + 16 * kAP);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  const int B = a.B, MT = a.MT;
+  const auto rx = rsrc(a.x, (uint32_t)B * kD * 4);
+  const auto rom = rsrc(a.omid, (uint32_t)B * kD * 2);
+  const bool first = (int)blockIdx.x < 16 * MT;
+  // phase 1: o' = c_h Wv_h^T + bv (c from the cross-attention launch), sc1 out
+  {
+    SplitW<4> w;
+    if (first) splitk_prefetch<4>(w, a.wv, kD, blockIdx.x, MT, lane, wv);
+    splitk_phase<4, SE_F16_SC1, true>(w, a.wv, kD, MT, rsrc(a.xc, (uint32_t)B * 8 * kD * 2), 8 * kD, a.bv,
+                                      rx, rom, red, lane, wv, [] {});
+  }
+  grid_barrier(a.bar, 1, a.err);
+  // phase 2: x += o' Wo_c^T + bo_c
+  {
+    SplitW<4> w;
+    if (first) splitk_prefetch<4>(w, a.woc, kD, blockIdx.x, MT, lane, wv);
+    splitk_phase<4, SE_RESID, false>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {});
+  }
+  grid_barrier(a.bar, 2, a.err);
+  // phase 3: f = gelu(LN3(x) W1^T + b1), sc1 out
+  {
+    LngW w;
+    lng_prefetch(w, a.w1, 4 * kD, MT, lane, wv);
+    LngOut o{a.f, 4 * kD, nullptr, nullptr, 0, 0, nullptr};
+    lng_phase<LE_GELU_SC1>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {});
+  }
+  grid_barrier(a.bar, 3, a.err);
+  // phase 4: x += f W2^T + b2 (K = 4d: 16 k-steps per quarter)
+  {
+    SplitW<16> w;
+    if (first) splitk_prefetch<16>(w, a.w2, 4 * kD, blockIdx.x, MT, lane, wv);
+    splitk_phase<16, SE_RESID, false>(w, a.w2, 4 * kD, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), 4 * kD, a.b2,
+                                      rx, rx, red, lane, wv, [] {});
+  }
+  // phase 5 (all but the last layer): the next layer's q and K/V cache rows
+  if (a.wqkv) {
+    grid_barrier(a.bar, 4, a.err);
+    LngW w;
+    lng_prefetch(w, a.wqkv, 3 * kD, MT, lane, wv);
+    LngOut o{a.qkv, 3 * kD, a.kc, a.vc, a.pos, a.n_ctx, a.roff};
+    lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {});
+  }
+  grid_exit(a.bar);
+}
+
+int dec_seg_grid(int B, int cus) {
+  // rows in 16-row tiles, rounded to a power of two (<= 8); groups of 16-column tiles per
+  // m-tile NG in {32, 16} (a divisor of 96, 128 and 256 tiles: QKV, fc1, qk) with
+  // MT * NG <= the partition's CUs: one block per CU, every block co-resident
+  const int MT = dec_seg_mtiles(B);
+  if (MT <= 0) return 0;
+  // NG >= 16: at least 16 * MT blocks, one split-K tile pair each
+  for (int ng : {32, 16})
+    if (MT * ng <= cus) return MT * ng;
+  return 0;
+}
+
+int dec_seg_mtiles(int B) {
+  if (B <= 0 || B > 128) return 0;
+  int mt = 1;
+  while (mt * 16 < B) mt *= 2;
+  return mt;
+}
+
+bool dec_seg_supported(int d, int H, int B, int cus) {
+  return d == kD && H == 8 && dec_seg_grid(B, cus) > 0;
+}
+
+static void seg_attr(const void* k) {
+  JANUS_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds));
+}
+
+void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_seg_a_kernel); attr = true; }
+  dec_seg_a_kernel<<<grid, kNT, kSegLds, s>>>(a);
+  JANUS_LAUNCH_CHECK();
+}
+
+void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_seg_b_kernel); attr = true; }
+  dec_seg_b_kernel<<<grid, kNT, kSegLds, s>>>(a);
+  JANUS_LAUNCH_CHECK();
+}
+
+}  // namespace janus

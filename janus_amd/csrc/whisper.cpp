@@ -17,6 +17,7 @@
 #include "devmem.h"
 #include "kernels.h"
 #include "decoder.h"
+#include "dec_persist.h"
 #include "../../include/janus.h"
 
 namespace janus {
@@ -64,7 +65,7 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups, d_roff;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups, d_roff, d_omid, d_segbar, d_segerr;
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
@@ -637,6 +638,46 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const bool fuse_se = std::getenv("JANUS_NO_SEL_EMBED") == nullptr;
   JANUS_CHECK(!stagger || (!fused_ln && !ln_fuse && !rln && xabs),
               "decode: staggered rows run the default decoder kernels only");
+  // persistent segments (dec_persist.hip, janus_decode_options.persistent): per layer the
+  // launches between the self-attention and the cross-attention (O + residual, LN2, the
+  // absorbed query projection) and between the cross-attention and the next layer's
+  // self-attention (value projection, cross O + residual, LN3, fc1, fc2 + residual, LN1,
+  // QKV) as two resident grids; the cross-attention then runs at one key split (its
+  // output written directly). Shapes it does not cover keep the launch path.
+  const int seg_grid = opt->persistent ? dec_seg_grid(B, cus) : 0;
+  const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && xabs && !shared && !fused_ln &&
+                       !ln_fuse && !rln && ngroups == 0 && npairs == 0;
+  if (persist) {
+    Z.d_omid.ensure(sizeof(_Float16) * B * d);
+    if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed
+      Z.d_segbar.ensure(sizeof(unsigned) * 256);
+      JANUS_HIP(hipMemsetAsync(Z.d_segbar.p, 0, sizeof(unsigned) * 256, s));
+    }
+    if (!Z.d_segerr.p) {
+      Z.d_segerr.ensure(256);
+      JANUS_HIP(hipMemsetAsync(Z.d_segerr.p, 0, 256, s));
+    }
+  }
+  auto seg_args = [&](int l, int pos) {
+    DecLayer& L = w->dec[l];
+    DecSegArgs g{};
+    g.B = B; g.MT = dec_seg_mtiles(B); g.x = x;
+    g.o = o; g.wo = L.wo.as<_Float16>(); g.bo = L.bo; g.ln2g = L.ln2g; g.ln2b = L.ln2b;
+    g.wqk = L.wqk.as<_Float16>(); g.bqk = L.bqk.as<float>(); g.xqk = Z.d_xqk.as<_Float16>();
+    g.xc = Z.d_xc.as<_Float16>(); g.wv = L.wv_c.as<_Float16>(); g.bv = L.bv_c; g.omid = Z.d_omid.as<_Float16>();
+    g.woc = L.wo_c.as<_Float16>(); g.boc = L.bo_c; g.ln3g = L.ln3g; g.ln3b = L.ln3b;
+    g.w1 = L.w1.as<_Float16>(); g.b1 = L.b1; g.f = f; g.w2 = L.w2.as<_Float16>(); g.b2 = L.b2;
+    if (l + 1 < nl) {
+      DecLayer& N = w->dec[l + 1];
+      g.ln1g = N.ln1g; g.ln1b = N.ln1b; g.wqkv = N.wqkv.as<_Float16>(); g.bqkv = N.bqkv.as<float>();
+      g.qkv = qkv;
+      g.kc = Z.d_kc.as<_Float16>() + (int64_t)(l + 1) * B * NC * d;
+      g.vc = Z.d_vc.as<_Float16>() + (int64_t)(l + 1) * B * NC * d;
+    }
+    g.pos = pos; g.n_ctx = NC; g.roff = roff;
+    g.bar = Z.d_segbar.as<unsigned>(); g.err = Z.d_segerr.as<unsigned>();
+    return g;
+  };
   auto step = [&](int pos) {
     if (!(fuse_se && pos >= sample_begin && pos > 0))
       embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
@@ -648,7 +689,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       _Float16* vc = Z.d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
       _Float16* ck = Z.d_ck.as<_Float16>() + (int64_t)l * Me * d;
       _Float16* cv = Z.d_cv.as<_Float16>() + (int64_t)l * Me * d;
-      if (fused_ln) {
+      if (persist && l > 0) {
+        // q and this layer's K/V cache row came from the previous layer's segment B
+      } else if (fused_ln) {
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
       } else {
@@ -670,6 +713,14 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       }
       decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                     part_o, part_ml, s, roff, max_roff);
+      if (persist) {
+        const DecSegArgs g = seg_args(l, pos);
+        dec_seg_a_launch(g, seg_grid, s);
+        xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
+                     s, true, nullptr, 0);
+        dec_seg_b_launch(g, seg_grid, s);
+        continue;
+      }
       if (rln2) resid_ln(o, L.wo, L.bo, L.ln2g, L.ln2b);
       else resid(o, d, L.wo, L.bo, L.ln2g, L.ln2b);
       if (xabs) {
@@ -759,7 +810,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
       (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
       (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows, (int64_t)roff,
-      (int64_t)max_roff};
+      (int64_t)max_roff, (int64_t)persist, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
+      (int64_t)Z.d_segerr.p};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {
     for (auto& kv : Z.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -807,6 +859,17 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       bool all = true;
       for (int b = 0; b < B; ++b) all = all && h_done[b];
       if (all) break;  // remaining positions keep -1; callers stop at the first eot
+    }
+  }
+  if (persist) {  // a segment whose grid never became co-resident gave up at a barrier
+    uint32_t herr = 0;
+    JANUS_HIP(hipMemcpyAsync(&herr, Z.d_segerr.p, sizeof(herr), hipMemcpyDeviceToHost, s));
+    JANUS_HIP(hipStreamSynchronize(s));
+    if (herr) {
+      JANUS_HIP(hipMemsetAsync(Z.d_segbar.p, 0, sizeof(unsigned) * 256, s));
+      JANUS_HIP(hipMemsetAsync(Z.d_segerr.p, 0, 256, s));
+      JANUS_HIP(hipStreamSynchronize(s));
+      throw Error("decode: a persistent decoder segment timed out at a grid barrier (grid not co-resident)");
     }
   }
   // every row ran Z.last_positions positions from its offset (the early exit stops all rows

@@ -134,6 +134,8 @@ class JanusPipeline:
         # ~98 MB alive between calls at base.en, batch 64)
         self.keep_encoder_output = False
         self.last_encoder_output = None
+        # the staggered step's decoder: persistent segments (janus_decode_options.persistent)
+        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "0"))
 
     # ------------------------------------------------------------------ encode
     def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
@@ -515,7 +517,7 @@ class JanusPipeline:
                             pd = None
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
                                   xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "1")),
-                                  cu_count=self._dec_s.n_cus)
+                                  cu_count=self._dec_s.n_cus, persistent=self.persistent)
                 if beside:
                     ds.wait_stream(ys)
                     pres = (pd, pres)

@@ -58,7 +58,7 @@ class janus_decode_options(ctypes.Structure):
                 ("max_initial_timestamp_index", ctypes.c_int), ("check_every", ctypes.c_int),
                 ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int),
                 ("state_slot", ctypes.c_int), ("logits_blocks", ctypes.c_int),
-                ("msplit_rows_n", ctypes.c_int)]
+                ("msplit_rows_n", ctypes.c_int), ("persistent", ctypes.c_int)]
 
 
 class janus_decode_rows(ctypes.Structure):
@@ -279,7 +279,8 @@ class WhisperEngine:
 
     def decode_options(self, max_length: int = 448, check_every: int = 16,
                        timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0,
-                       state_slot: int = 0, logits_blocks: int = 0, msplit_rows_n: int = 0):
+                       state_slot: int = 0, logits_blocks: int = 0, msplit_rows_n: int = 0,
+                       persistent: int = 0):
         t = self.tokenizer
         prompt = np.array(t.sot_sequence, np.int32)
         supp = np.array(t.suppress_tokens(), np.int32)
@@ -301,6 +302,7 @@ class WhisperEngine:
         opt.state_slot = state_slot
         opt.logits_blocks = logits_blocks
         opt.msplit_rows_n = msplit_rows_n
+        opt.persistent = persistent
         return opt, (prompt, supp)
 
     def decode(self, enc: torch.Tensor, max_length: int = 448, check_every: int = 16,
@@ -320,7 +322,7 @@ class WhisperEngine:
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
                   cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None,
                   pos_offset=None, steps: int = 0, state_slot: int = 0, logits_blocks: int = 0,
-                  msplit_rows_n: int = 0):
+                  msplit_rows_n: int = 0, persistent: int = 0):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
@@ -333,7 +335,8 @@ class WhisperEngine:
         start fresh (one contiguous range). ``state_slot``: the context's decoder state slot
         the call runs in (a sampled re-decode between two staggered calls takes another
         slot); ``logits_blocks`` / ``msplit_rows_n``: launch geometry (0 = measured
-        defaults, janus_decode_options)."""
+        defaults, janus_decode_options); ``persistent``: the persistent decoder segments
+        (dec_persist.hip) where the shape allows."""
         B = enc.shape[0] if enc_index is None else len(enc_index)
         if steps < 0:
             raise ValueError("steps must be >= 0")
@@ -344,7 +347,7 @@ class WhisperEngine:
                 raise ValueError("sampling needs one uint32 seed per row")
             sd = np.ascontiguousarray(np.asarray(seeds, np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count,
-                                        state_slot, logits_blocks, msplit_rows_n)
+                                        state_slot, logits_blocks, msplit_rows_n, persistent)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
         po = None

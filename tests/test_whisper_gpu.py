@@ -504,3 +504,85 @@ def test_layernorm_placements_bit_identical(base_engine, gpu, monkeypatch, env):
     t2, n2, s2 = eng.decode(enc, 40)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
+
+
+def test_persistent_segments_vs_oracle(base_engine, gpu):
+    """The persistent decoder segments (janus_decode_options.persistent: per layer two
+    resident-grid launches with in-launch barriers instead of ten launches) decode base.en
+    free-running to 448 tokens like the oracle — identical, or first divergence at an
+    oracle near-tie — and agree with the launch path on the gate inputs (sum of chosen
+    log-probs within 1e-3 where the sequences match, no-speech probability within 0.5 %)."""
+    eng, W = base_engine
+    secs = [30.0, 17.0, 8.0, 3.0, 1.0, 0.3, 24.0, 12.0]
+    utts = [synth_speech(140 + k, s) for k, s in enumerate(secs)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    per = eng.decode_ex(enc, max_length=448, persistent=1)
+    lau = eng.decode_ex(enc, max_length=448, persistent=0)
+    torch.cuda.synchronize()
+    tk = eng.tokenizer
+    plen = len(tk.sot_sequence)
+    nt = per.n_tokens.cpu().numpy()
+    assert (nt >= 128).all()
+    ref = ow.greedy_cached(enc.float().cpu(), W, BASE, tk, 448, no_speech=50361)
+    seq, pk = _check_free_running(per.tokens.cpu().numpy(), ref, tk, plen, nt)
+    print(f"persistent segments, base.en free-running: sequences identical {seq:.3f}, packets {pk:.3f}")
+    assert seq >= 0.75 and pk >= 0.75
+    pt, lt = per.tokens.cpu(), lau.tokens.cpu()
+    for b in range(len(utts)):
+        if torch.equal(pt[b], lt[b]):
+            a, c = float(per.sum_logprob[b]), float(lau.sum_logprob[b])
+            assert abs(a - c) <= 1e-3 * abs(c), (b, a, c)
+        a, c = float(per.no_speech_prob[b]), float(lau.no_speech_prob[b])
+        assert abs(a - c) <= 5e-3 * c + 1e-12, (b, a, c)
+
+
+@pytest.mark.parametrize("rows", [40, 64])
+def test_persistent_staggered_bit_identical(base_engine, gpu, rows):
+    """Continuous batching through the persistent segments: two slot sets of `rows` rows
+    (2 x 64 = the bench's decoder call), each batch started fresh in one call and continued
+    in the next, equal a full persistent decode of that batch alone bit for bit — a row's
+    arithmetic in the segments does not depend on the rows beside it or on the grid."""
+    eng, _ = base_engine
+    L, S = 40, 20
+    batches = []
+    for k in range(3):
+        utts = [synth_speech(600 + 10 * k + j, 1.0 + (j % 5)) for j in range(rows)]
+        pcm, offs = pack(utts, gpu)
+        batches.append(eng.encode(eng.logmel(pcm, offs, rows, 3)))
+    ref = [eng.decode_ex(e, max_length=L, persistent=1) for e in batches]
+    sets = [None, None]
+    got = {}
+    for call in range(4):
+        fresh, cont = call % 2, 1 - call % 2
+        sets[fresh] = call if call < 3 else None
+        rows_enc, offs = [], []
+        for st in (0, 1):
+            bi = sets[st]
+            if bi is None:
+                rows_enc.append(torch.zeros_like(batches[0]))
+                offs += [L - S] * rows if st == cont or call == 3 else [0] * rows
+            else:
+                rows_enc.append(batches[bi])
+                offs += [0 if st == fresh else S] * rows
+        if call == 0:
+            offs = [0] * (2 * rows)
+        out = eng.decode_ex(torch.cat(rows_enc), max_length=L, pos_offset=offs, steps=S, persistent=1,
+                            cu_count=128)
+        if call > 0 and sets[cont] is not None:
+            bi = sets[cont]
+            sl = slice(cont * rows, cont * rows + rows)
+            got[bi] = (out.tokens[sl].cpu(), out.n_tokens[sl].cpu(), out.sum_logprob[sl].cpu(),
+                       out.no_speech_prob[sl].cpu())
+            sets[cont] = None
+    torch.cuda.synchronize()
+    assert sorted(got) == [0, 1, 2]
+    plen = len(eng.tokenizer.sot_sequence)
+    for bi, r in enumerate(ref):
+        t, n, lp, ns = got[bi]
+        assert torch.equal(n, r.n_tokens.cpu()) and torch.equal(lp, r.sum_logprob.cpu())
+        assert torch.equal(ns, r.no_speech_prob.cpu())
+        rt = r.tokens.cpu()
+        for j in range(rows):
+            k = plen + int(n[j])
+            assert torch.equal(t[j, :k], rt[j, :k]), (bi, j)
