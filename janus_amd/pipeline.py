@@ -128,6 +128,7 @@ class JanusPipeline:
         self.device = nat.require_gpu()
         self.whisper = WhisperEngine(CONFIGS[model], seed=whisper_seed)
         self.vocoder = VocoderEngine(vocoder_cfg, seed=vocoder_seed)
+        self._vocoder_seed = vocoder_seed
         self.max_length = max_length
         self.temperatures = tuple(float(t) for t in temperatures)
         # parity tests set this to read the encoder output back (it would otherwise keep
@@ -135,7 +136,7 @@ class JanusPipeline:
         self.keep_encoder_output = False
         self.last_encoder_output = None
         # the staggered step's decoder: persistent segments (janus_decode_options.persistent)
-        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "0"))
+        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "1"))
 
     # ------------------------------------------------------------------ encode
     def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
@@ -202,10 +203,13 @@ class JanusPipeline:
         return torch.stack([self._stock_voice if m == JanusMode.SEMANTIC_VOICE else zero
                             for m in modes])
 
-    def decode(self, packets, frames: int):
+    def decode(self, packets, frames: int, vocoder=None):
         """packets: MessagePack bytes (None entries skipped). Returns (wav, pcm, prompts)
         for the SEMANTIC / TEXT_ONLY packets, all rendered to `frames` latent frames, in
-        the voice the Synthesizer would request (set_reference_audio)."""
+        the voice the Synthesizer would request (set_reference_audio). ``vocoder``: another
+        VocoderEngine with the same weights (its own workspaces: a second batch renders
+        concurrently on another stream)."""
+        voc = vocoder if vocoder is not None else self.vocoder
         prompts, emos, modes = [], [], []
         for p in packets:
             if p is None:
@@ -224,9 +228,16 @@ class JanusPipeline:
             modes.append(pkt.mode)
         if not prompts:
             return None, None, []
-        lat = self.vocoder.frontend(prompts, emos, frames, self._voices(modes))
-        wav, pcm = self.vocoder.forward(lat)
+        lat = voc.frontend(prompts, emos, frames, self._voices(modes))
+        wav, pcm = voc.forward(lat)
         return wav, pcm, prompts
+
+    def _vocoder_dec(self):
+        """The second vocoder context (same seeded weights, own workspaces) that renders the
+        decoder side's share of a staggered step's batch."""
+        if getattr(self, "_voc2", None) is None:
+            self._voc2 = VocoderEngine(self.vocoder.cfg, seed=self._vocoder_seed)
+        return self._voc2
 
     def step(self, pcm, offsets, lengths, frames):
         enc = self.encode(pcm, offsets, lengths)
@@ -474,9 +485,18 @@ class JanusPipeline:
                                       max_blocks=0)
             except Exception:  # engine.py:520-525
                 return None
+        # the last kv packets of the batch render on the decoder's CUs after its call (a
+        # second vocoder context), the rest here: a decoder side that finishes early takes
+        # vocoder work the way the vocoder side takes YIN (JANUS_VOC_DEC_UTTS)
+        kv = 0
+        pk_dec = []
+        wav_b = pcm_b = None
         with torch.cuda.stream(vs):
             if res_prev is not None:
-                wav, pcm16, _ = self.decode(res_prev.packets, frames)
+                pk = res_prev.packets
+                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "0"))))
+                pk_dec = pk[len(pk) - kv:] if kv else []
+                wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
             if pcm is not None:
                 pres = yin(n_dec, B)
             ev[1].record(vs)
@@ -529,6 +549,9 @@ class JanusPipeline:
             stand = w.decode_stand(n * B)
             for j in range(n):
                 pos[j] = stand[j * B]
+        if pk_dec:
+            with torch.cuda.stream(ds):
+                wav_b, pcm_b, _ = self.decode(pk_dec, frames, vocoder=self._vocoder_dec())
         if pcm is not None:
             st["sets"][f] = {"pres": pres, "B": B, "mode": mode, "override": override,
                              "timestamp": timestamp, "born": k}
@@ -540,6 +563,9 @@ class JanusPipeline:
             st["prev_ev"] = ev
         main.wait_stream(ds)
         main.wait_stream(vs)
+        if wav_b is not None:   # the batch back in packet order
+            wav = wav_b if wav is None else torch.cat([wav, wav_b])
+            pcm16 = pcm_b if pcm16 is None else torch.cat([pcm16, pcm_b])
         if cont is not None:
             sl = slice(jc * B, (jc + 1) * B)
             from .whisper import DecodeOut

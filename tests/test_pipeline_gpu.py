@@ -102,13 +102,16 @@ def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
         assert torch.equal(pcm16, seq[i][2])
 
 
-@pytest.mark.parametrize("sets", ["2", "3", "4"])
-def test_staggered_step_matches_sequential(gpu, monkeypatch, sets):
+@pytest.mark.parametrize("sets,voc_dec", [("2", "0"), ("3", "0"), ("4", "0"), ("2", "1"), ("2", "3")])
+def test_staggered_step_matches_sequential(gpu, monkeypatch, sets, voc_dec):
     """The continuous-batching serving step (step_staggered: the decoder advances batch i's
     rows from position 0 and batch i-m's from position mS, m < N, in one call, N·B rows;
     N = JANUS_STAGGER_SETS) produces, per batch and N steps later, the same packets and
-    waveforms as the back-to-back step of that batch alone; flush_staggered drains."""
+    waveforms as the back-to-back step of that batch alone; flush_staggered drains. With
+    JANUS_VOC_DEC_UTTS = k the batch's last k packets render on the decoder's CUs through a
+    second vocoder context: the waveforms are still bit-identical, in packet order."""
     monkeypatch.setenv("JANUS_STAGGER_SETS", sets)
+    monkeypatch.setenv("JANUS_VOC_DEC_UTTS", voc_dec)
     pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,))
     batches = []
     for i in range(3):

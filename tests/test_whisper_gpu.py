@@ -550,7 +550,9 @@ def test_persistent_staggered_bit_identical(base_engine, gpu, rows):
         utts = [synth_speech(600 + 10 * k + j, 1.0 + (j % 5)) for j in range(rows)]
         pcm, offs = pack(utts, gpu)
         batches.append(eng.encode(eng.logmel(pcm, offs, rows, 3)))
-    ref = [eng.decode_ex(e, max_length=L, persistent=1) for e in batches]
+    # the same launch geometry on both sides (cu_count sets the vocabulary projection's
+    # block count, whose partial merge order reaches the log-prob sums' last bits)
+    ref = [eng.decode_ex(e, max_length=L, persistent=1, cu_count=128) for e in batches]
     sets = [None, None]
     got = {}
     for call in range(4):
