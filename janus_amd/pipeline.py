@@ -494,7 +494,7 @@ class JanusPipeline:
         with torch.cuda.stream(vs):
             if res_prev is not None:
                 pk = res_prev.packets
-                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "0"))))
+                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "2"))))
                 pk_dec = pk[len(pk) - kv:] if kv else []
                 wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
             if pcm is not None:
