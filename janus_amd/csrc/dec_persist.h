@@ -26,6 +26,7 @@ struct DecSegArgs {
   _Float16* kc; _Float16* vc; int pos, n_ctx; const int32_t* roff;  // the next layer's cache
   unsigned* bar;             // 160 zeroed words (barrier counters, self-cleaning)
   unsigned* err;             // timeout flag (host-checked)
+  long long* prof;           // phase stamps (JANUS_PHASE_PROF builds, tools/seg_prof.py); null
 };
 
 // 16-row tiles for B rows (0: unsupported, B > 128)
@@ -35,5 +36,7 @@ int dec_seg_grid(int B, int cus);
 bool dec_seg_supported(int d, int H, int B, int cus);
 void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s);
 void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s);
+// JANUS_PHASE_PROF builds: the stamp buffer for layer l when JANUS_SEG_PROF=l, else null
+long long* dec_seg_prof_target(int l);
 
 }  // namespace janus

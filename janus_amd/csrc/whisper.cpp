@@ -676,6 +676,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     }
     g.pos = pos; g.n_ctx = NC; g.roff = roff;
     g.bar = Z.d_segbar.as<unsigned>(); g.err = Z.d_segerr.as<unsigned>();
+    g.prof = dec_seg_prof_target(l);
     return g;
   };
   auto step = [&](int pos) {

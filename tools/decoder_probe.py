@@ -3,7 +3,8 @@
 vocoder (batch 64 x 30 s on the complementary CUs), to separate the decoder's own latency
 floor from interference. Prints one JSON line per configuration.
 
-python tools/decoder_probe.py [--per-xcd 8,12,16,24] [--beside 1]
+python tools/decoder_probe.py [--per-xcd 8,12,16,24] [--beside 1] [--rows 128] [--persistent 1]
+(--rows 128: the headline step's two slot sets, the 64 encoder rows twice)
 """
 import argparse
 import json
@@ -19,6 +20,9 @@ def main():
     ap.add_argument("--beside", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--max-length", type=int, default=448)
+    ap.add_argument("--rows", type=int, default=64)
+    ap.add_argument("--persistent", type=int, default=0)
+    ap.add_argument("--xsplits", type=int, default=4)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -33,6 +37,8 @@ def main():
     pipe = JanusPipeline("base.en", max_length=448, temperatures=(0.0,))
     w = pipe.whisper
     enc = w.encode(w.logmel(pcm, offs, B, 3))
+    if a.rows > B:
+        enc = torch.cat([enc] * ((a.rows + B - 1) // B))[:a.rows].contiguous()
     frames = 2584
     lat = None
     if a.beside:
@@ -52,13 +58,15 @@ def main():
                         pipe.vocoder.forward(lat, want_pcm=True)
                 e[3].record(vs.stream)
                 with torch.cuda.stream(ds.stream):
-                    out = w.decode_ex(enc, max_length=a.max_length, xattn_splits=4, cu_count=ds.n_cus)
+                    out = w.decode_ex(enc, max_length=a.max_length, xattn_splits=a.xsplits, cu_count=ds.n_cus,
+                                      persistent=a.persistent)
                 e[1].record(ds.stream)
                 torch.cuda.synchronize()
                 print(json.dumps({"dec_per_xcd": per, "beside_vocoder": beside, "rep": rep,
                                   "decoder_ms": round(e[0].elapsed_time(e[1]), 1),
                                   "vocoder_ms": round(e[2].elapsed_time(e[3]), 1) if beside else None,
-                                  "tokens": int(out.n_tokens.float().mean().item())}), flush=True)
+                                  "tokens": int(out.n_tokens.float().mean().item()), "rows": int(enc.shape[0]),
+                                  "persistent": a.persistent, "xsplits": a.xsplits}), flush=True)
 
 
 if __name__ == "__main__":

@@ -187,7 +187,8 @@ def _time_cold(fn, reps, flush):
     torch.cuda.synchronize()
     tot = 0.0
     for _ in range(reps):
-        flush.fill_(1.0)
+        if flush is not None:
+            flush.fill_(1.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         fn()
@@ -201,13 +202,18 @@ def xattn_bench(reps=20):
     """Absorbed cross-attention at the bench shape (64 x 1500 x 512, 8 heads) per split
     count, caches flushed before every call (the decoder reads enc once per layer)."""
     dev = torch.device("cuda", 0)
+    if os.environ.get("XMASK"):  # on a CU-masked stream: XMASK CUs per XCD (the decoder's share)
+        n = torch.cuda.get_device_properties(0).multi_processor_count
+        ms = nat.MaskedStream(nat.split_cu_masks(n, int(os.environ["XMASK"]))[0])
+        torch.cuda.set_stream(ms.stream)
+        print(f"masked stream: {ms.n_cus} CUs", flush=True)
     s = torch.cuda.current_stream().cuda_stream
     B, Te, D, H = 64, 1500, 512, 8
     enc = torch.randn(B, Te, D, device=dev).half()
     qk = (torch.randn(B, H, D, device=dev) * 0.1).half()
     out = torch.empty(B, H * D, device=dev, dtype=torch.float16)
     flush = torch.empty(128 << 20, device=dev)
-    for ns in (8, 12, 16, 24):
+    for ns in [int(v) for v in os.environ.get("XSPLITS", "1,2,4,8,12,16,24").split(",")]:
         pc = torch.empty(B * ns * H * D, device=dev)
         pml = torch.empty(B * ns * H * 2, device=dev)
 
@@ -216,6 +222,9 @@ def xattn_bench(reps=20):
                      pc.data_ptr(), pml.data_ptr(), out.data_ptr(), s)
         ms = _time_cold(run, reps, flush)
         print(f"xattn nsplit={ns:3d} {ms * 1000:8.1f} us  {B * Te * D * 2 / ms / 1e6:8.1f} GB/s (enc, cold)",
+              flush=True)
+        ms = _time_cold(run, reps, None)
+        print(f"xattn nsplit={ns:3d} {ms * 1000:8.1f} us  {B * Te * D * 2 / ms / 1e6:8.1f} GB/s (enc, warm)",
               flush=True)
 
 
