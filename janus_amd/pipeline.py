@@ -21,7 +21,7 @@ import torch
 
 from . import _native as nat
 from .common.protocol import JanusMode, JanusPacket
-from .services.prosody import prosody_launch
+from .services.prosody import ProsodyResult, prosody_launch
 from .services.synthesizer import emotion_prompt
 from .services.transcriber import TEMPERATURES
 from .vocoder import DEFAULT_REFERENCE_ID, FireflyConfig, VocoderEngine, emotion_id
@@ -321,6 +321,8 @@ class JanusPipeline:
         prev = getattr(self, "_pending", None)
         self._pending = None
         res_prev = self._finish(*prev) if prev is not None else None
+        # (the vocoder side starting beside the encoder instead: level, 248.9-249.3 vs
+        # 248.6-248.9 ms, profiles/r05_host_prefetch_ab.txt)
         vs.wait_stream(hi)
         ds.wait_stream(hi)
         wav = pcm16 = None
@@ -390,20 +392,64 @@ class JanusPipeline:
     def _finish(self, dec, pres, B, mode, override, timestamp) -> EncodeResult:
         """Host tail of an encode: transcripts, prosody tags (fallback Normal/Normal,
         engine.py:520-525), packets (engine.py:527-548)."""
+        host = getattr(dec, "host", None)
+        if host is not None:   # copies issued behind the decoder call (_host_prefetch)
+            ev, hdec, hpres = host
+            ev.synchronize()
         try:
             parts = pres if isinstance(pres, tuple) else (pres,)
-            tags = None if any(p is None for p in parts) else [t for p in parts for t in p.tags()]
+            if host is not None and hpres is not None:
+                tags = [t for (r, m, v) in hpres for t in ProsodyResult.tags_of(r.numpy(), m.numpy(), v.numpy())]
+            else:
+                tags = None if any(p is None for p in parts) else [t for p in parts for t in p.tags()]
         except Exception:
             tags = None
         if tags is None:
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
         settled = getattr(dec, "settled", None)
-        texts, gts = settled if settled is not None else _texts_and_gates(self.whisper, dec)
+        texts, gts = settled if settled is not None else _texts_and_gates(
+            self.whisper, hdec if host is not None else dec)
         ts = time.time() if timestamp is None else timestamp
         packets = [JanusPacket(t, mode, g, override, ts).serialize() if t.strip() else None
                    for t, g in zip(texts, tags)]
         stats = _prosody_stats(parts if pres is not None else None, B, dec.tokens.device)
         return EncodeResult(texts, tags, packets, dec.tokens, dec.n_tokens, stats, gts)
+
+    def _host_prefetch(self, part, pres, st, stream):
+        """Device-to-host copies of what _finish reads of a completing batch (its tokens,
+        counts, log-probs, no-speech probabilities and YIN statistics), issued on `stream`
+        right behind the decoder call that completed it, into pinned buffers. _finish then
+        waits for that call alone — not, through the caller's stream, for the vocoder side
+        that ends later — so the host tail (detokenising, gates, packets) overlaps the
+        vocoder's last milliseconds. One buffer set: the next call's copies are enqueued
+        after this host tail has read them. The copies run on a torch-owned stream behind
+        `stream` (the pinned blocks' lifetime events then never sit on a CU-masked stream
+        that is destroyed before them at exit)."""
+        from .whisper import DecodeOut
+        hb = st.setdefault("hbuf", {})
+        cs = getattr(self, "_d2h_stream", None)
+        if cs is None:
+            cs = self._d2h_stream = torch.cuda.Stream(part.tokens.device)
+        cs.wait_stream(stream)
+        stream = cs
+
+        def pin(name, t):
+            buf = hb.get(name)
+            if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+                buf = hb[name] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            buf.copy_(t, non_blocking=True)
+            return buf
+        with torch.cuda.stream(stream):
+            hdec = DecodeOut(pin("tok", part.tokens), pin("nt", part.n_tokens), pin("lp", part.sum_logprob),
+                             pin("ns", part.no_speech_prob), part.prompt_lens)
+            parts = pres if isinstance(pres, tuple) else (pres,)
+            hpres = None
+            if all(p is not None for p in parts):
+                hpres = [(pin(f"rms{i}", p.rms), pin(f"mf{i}", p.mean_f0), pin(f"nv{i}", p.n_voiced))
+                         for i, p in enumerate(parts)]
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ev, hdec, hpres
 
     # ------------------------------------------- staggered (continuous-batching) step
     def step_staggered(self, pcm, offsets, lengths, frames, dec_per_xcd: int = 16,
@@ -510,6 +556,7 @@ class JanusPipeline:
         offs = [o for o in set_offs for _ in range(B)]
         cont = st["sets"][jc] if jc is not None else None
         dec = None
+        host = None
         if pcm is not None or any(x is not None for x in st["sets"]):
             with torch.cuda.stream(ds):
                 # cross-attention at ONE key split (r05): with 2 x 64 rows the grid fills the
@@ -538,6 +585,13 @@ class JanusPipeline:
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
                                   xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "1")),
                                   cu_count=self._dec_s.n_cus, persistent=self.persistent)
+                if cont is not None and len(self.temperatures) == 1 and \
+                        int(os.environ.get("JANUS_HOST_PREFETCH", "1")):
+                    from .whisper import DecodeOut
+                    sl = slice(jc * B, (jc + 1) * B)
+                    hpart = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
+                                      dec.no_speech_prob[sl], dec.prompt_lens[sl])
+                    host = self._host_prefetch(hpart, cont["pres"], st, ds)
                 if beside:
                     ds.wait_stream(ys)
                     pres = (pd, pres)
@@ -572,6 +626,8 @@ class JanusPipeline:
             part = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
                              dec.no_speech_prob[sl], dec.prompt_lens[sl])
             part.settled = None
+            if host is not None:
+                part.host = host
             if len(self.temperatures) > 1:
                 # the fallback of the completing batch's failing windows, on the whole GPU
                 # after both sides (its encoder output stays in slot set jc until the next

@@ -52,9 +52,11 @@ class ProsodyResult:
         self.f0, self.rms, self.mean_f0, self.n_voiced, self.hop_off = f0, rms, mean_f0, n_voiced, hop_off
 
     def tags(self):
-        rms = self.rms.cpu().numpy()
-        mf = self.mean_f0.cpu().numpy()
-        nv = self.n_voiced.cpu().numpy()
+        return self.tags_of(self.rms.cpu().numpy(), self.mean_f0.cpu().numpy(), self.n_voiced.cpu().numpy())
+
+    @staticmethod
+    def tags_of(rms, mf, nv):
+        """The tags from host copies of (rms, mean_f0, n_voiced)."""
         return [{'energy': energy_tag(float(rms[b])), 'pitch': pitch_tag(float(mf[b]), int(nv[b]))}
                 for b in range(len(rms))]
 
