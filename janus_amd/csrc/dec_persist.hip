@@ -161,12 +161,21 @@ __device__ __forceinline__ uint32_t l2_touch(const _Float16* base, uint32_t byte
   return v;
 }
 
-// the slab of a LayerNorm GEMM phase: the block's column group, split over its MT m-tiles
+// two m-tiles per block for a LayerNorm GEMM phase of N columns when one per block would
+// leave a wave more than one 16-column tile (uniform over the grid)
+__device__ __forceinline__ bool dec_seg_mb2(int N, int MT) {
+  return MT % 2 == 0 && (N / 16) / ((int)gridDim.x / MT) > 8;
+}
+
+// the slab of a LayerNorm GEMM phase: the block's column group, split over the blocks of
+// its m-groups (lng_tiles<MB>)
+template <int MB = 1>
 __device__ __forceinline__ uint32_t touch_lng(const _Float16* wt, int N, int MT) {
   const int b = blockIdx.x, G = gridDim.x;
   const int j = b >> 3, xcd = b & 7;
-  const int npg = (N / 16) / (G / MT), g = xcd + 8 * (j / MT);
-  return l2_touch(wt + (int64_t)16 * g * npg * kD, (uint32_t)npg * 16 * kD * 2, j % MT, MT);
+  const int MG = MT / MB;
+  const int npg = (N / 16) / (G / MG), g = xcd + 8 * (j / MG);
+  return l2_touch(wt + (int64_t)16 * g * npg * kD, (uint32_t)npg * 16 * kD * 2, j % MG, MG);
 }
 
 // the slab of a split-K phase: the rows of the pair's column tile(s), split over the
@@ -282,12 +291,17 @@ struct LngW {
   half8 w[16];
 };
 
+// MB m-tiles per block (MB = 2: the block's 32 rows share each weight fragment, so a block
+// reads half the weight bytes of MB = 1 for the same columns): block -> (m-group of MB
+// tiles, column group), the blocks of one column group on one XCD (its L2 serves them)
+template <int MB = 1>
 __device__ __forceinline__ void lng_tiles(int N, int MT, int& m, int& nt0, int& npg) {
   const int b = blockIdx.x, G = gridDim.x;
   const int j = b >> 3, xcd = b & 7;
-  const int NG = G / MT;
-  m = j % MT;
-  const int g = xcd + 8 * (j / MT);
+  const int MG = MT / MB;
+  const int NG = G / MG;
+  m = (j % MG) * MB;  // first m-tile
+  const int g = xcd + 8 * (j / MG);
   npg = (N / 16) / NG;
   nt0 = g * npg;
 }
@@ -314,24 +328,25 @@ struct LngOut {
   _Float16* kc; _Float16* vc; int pos, n_ctx; const int32_t* roff;  // LE_QKV
 };
 
-template <int EPI, class Pre>
+template <int EPI, int MB = 1, class Pre>
 __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, int MT,
                                           int B, __amdgpu_buffer_rsrc_t rx, const float* g,
                                           const float* bt, const float* bias,
                                           const LngOut& o, _Float16* sA, float* patch_all, int lane,
                                           int wv, Pre&& pre, long long* st = nullptr, int si = 0) {
   int m, nt0, npg;
-  lng_tiles(N, MT, m, nt0, npg);
+  lng_tiles<MB>(N, MT, m, nt0, npg);
+  constexpr int RW = 2 * MB;  // LayerNorm rows per wave
   // ---- LayerNorm of rows 16m + 2wv, 16m + 2wv + 1 (sc1 loads: x was just handed off).
   // Issue order: both rows and gamma / beta first, THEN the phase's weight fragments, so
   // the LayerNorm waits only for its own loads (vector loads retire in issue order: with
   // the weights issued first it waited for all 16 of them) while the weights stream in
-  float4 v[2][2], gg[2], bb[2];
+  float4 v[RW][2], gg[2], bb[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < RW; ++j)
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-      v[j][k] = as_f4(ld_sc1(rx, (uint32_t)(((16 * m + 2 * wv + j) * kD + 4 * (lane + 64 * k)) * 4)));
+      v[j][k] = as_f4(ld_sc1(rx, (uint32_t)(((16 * m + RW * wv + j) * kD + 4 * (lane + 64 * k)) * 4)));
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     gg[k] = reinterpret_cast<const float4*>(g)[lane + 64 * k];
@@ -339,12 +354,17 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
   }
   __builtin_amdgcn_sched_barrier(0);
   // unconditional (a wave without a tile re-reads the group's first, unused): behind a
-  // branch the wait-count pass merged the paths and the LayerNorm waited for the weights
-  lng_load(W.w, wt, nt0 + (wv < npg ? wv : 0), lane);
+  // branch the wait-count pass merged the paths and the LayerNorm waited for the weights.
+  // MB = 2 (four rows in flight) issues the first 8 k-steps here and the rest after the
+  // LayerNorm: all 16 beside the rows would spill
+  const _Float16* wrow = wt + (int64_t)(16 * (nt0 + (wv < npg ? wv : 0)) + (lane & 15)) * kD + 8 * (lane >> 4);
+  constexpr int WH = MB == 1 ? 16 : 8;
+#pragma unroll
+  for (int k = 0; k < WH; ++k) W.w[k] = *reinterpret_cast<const half8*>(wrow + 32 * k);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int lrow = 2 * wv + j;
+  for (int j = 0; j < RW; ++j) {
+    const int lrow = RW * wv + j;
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 2; ++k) s += ln_sum4(v[j][k]);
@@ -359,6 +379,10 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
     for (int k = 0; k < 2; ++k)
       *reinterpret_cast<half4*>(sA + lrow * kAP + 4 * (lane + 64 * k)) = ln_norm4(v[j][k], mean, rstd, gg[k], bb[k]);
   }
+  if constexpr (WH < 16) {
+#pragma unroll
+    for (int k = WH; k < 16; ++k) W.w[k] = *reinterpret_cast<const half8*>(wrow + 32 * k);
+  }
   __syncthreads();
   SEG_STAMP(st, si);
   const int lr = lane & 15, kc8 = 8 * (lane >> 4);
@@ -372,13 +396,20 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
     // the tile's bias now: loaded in the epilogue it would queue behind the next tile's
     // weight loads issued there (vector loads retire in order)
     const float4 bias4 = *reinterpret_cast<const float4*>(bias + 16 * nt + 4 * (lane & 3));
-    f32x4 acc = zero_f32x4();
-    half8 a[2];
-    a[0] = *reinterpret_cast<const half8*>(sA + lr * kAP + kc8);
+    f32x4 acc[MB];
+#pragma unroll
+    for (int u = 0; u < MB; ++u) acc[u] = zero_f32x4();
+    half8 a[2][MB];
+#pragma unroll
+    for (int u = 0; u < MB; ++u) a[0][u] = *reinterpret_cast<const half8*>(sA + (16 * u + lr) * kAP + kc8);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s + 1 < 16) a[(s + 1) & 1] = *reinterpret_cast<const half8*>(sA + lr * kAP + 32 * (s + 1) + kc8);
-      acc = mfma16(a[s & 1], W.w[s], acc);
+      if (s + 1 < 16)
+#pragma unroll
+        for (int u = 0; u < MB; ++u)
+          a[(s + 1) & 1][u] = *reinterpret_cast<const half8*>(sA + (16 * u + lr) * kAP + 32 * (s + 1) + kc8);
+#pragma unroll
+      for (int u = 0; u < MB; ++u) acc[u] = mfma16(a[s & 1][u], W.w[s], acc[u]);
     }
     if (li == wv) SEG_STAMP(st, si + 1);
     // the next tile's weights (or the next phase's) in flight during this epilogue
@@ -389,11 +420,13 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
     else pre();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) patch[(4 * (lane >> 4) + r) * 17 + lr] = acc[r];
+    for (int u = 0; u < MB; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) patch[(4 * (lane >> 4) + r) * 17 + lr] = acc[u][r];
     // wave-private patch: own stores visible to own loads in order
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     const int row = lane >> 2, c4 = 4 * (lane & 3);
-    const int grow = 16 * m + row, col = 16 * nt + c4;
+    const int grow = 16 * (m + u) + row, col = 16 * nt + c4;
     float v[4];
     v[0] = patch[row * 17 + c4 + 0] + bias4.x;
     v[1] = patch[row * 17 + c4 + 1] + bias4.y;
@@ -423,12 +456,77 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
       }
     }
     if (li == wv) SEG_STAMP(st, si + 2);
+    }  // u: the patch is reused by the next m-tile (one wave's LDS operations run in order)
     // the patch is rewritten by the next tile: LDS operations of one wave run in order
   };
   for (int i = 0; i + 1 < ntile; ++i) tile(wv + 8 * i, false);
   if (ntile > 0) tile(wv + 8 * (ntile - 1), true);
   else pre();  // no tile for this wave
   (void)N;
+}
+
+// K = 4d (fc2) with both tiles of the pair in the same column tile (MT even): every wave
+// takes one eighth of K for BOTH tiles — its 8 weight fragments shared by the two m-tiles,
+// 2 x 8 activation fragments — so all of a wave's loads go out in one round trip (the
+// quarter split needed 16 weight + 2 x 8 activation fragments per wave and issued the
+// second activation half after the first half's MFMAs: two round trips); the 8 partials
+// per output are summed in a fixed order
+__device__ __forceinline__ void splitk8_pair(const _Float16* wt, int pair, int MT,
+                                             __amdgpu_buffer_rsrc_t ra, const float* bias,
+                                             __amdgpu_buffer_rsrc_t rx, float* red, int lane, int wv,
+                                             long long* st, int si) {
+  constexpr int K = 4 * kD, KS = K / 8 / 32;  // 8 k-steps per wave
+  const int t0 = 2 * pair;
+  const int m0 = t0 % MT, n = t0 / MT;
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const int k0 = wv * (K / 8) + kc8;
+  half8 w[KS], a0[KS], a1[KS];
+  const _Float16* wr = wt + (int64_t)(16 * n + lr) * K + k0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) w[s] = *reinterpret_cast<const half8*>(wr + 32 * s);
+  const uint32_t ab0 = (uint32_t)(((16 * m0 + lr) * K + k0) * 2);
+  const uint32_t ab1 = ab0 + (uint32_t)(16 * K * 2);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) a0[s] = as_h8(ld_sc1(ra, ab0 + 64 * s));
+#pragma unroll
+  for (int s = 0; s < KS; ++s) a1[s] = as_h8(ld_sc1(ra, ab1 + 64 * s));
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc0 = zero_f32x4(), acc1 = zero_f32x4();
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    acc0 = mfma16(a0[s], w[s], acc0);
+    acc1 = mfma16(a1[s], w[s], acc1);
+  }
+  // red[tile][wave][16][17]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[((0 * 8 + wv) * 16 + 4 * (lane >> 4) + r) * 17 + lr] = acc0[r];
+    red[((1 * 8 + wv) * 16 + 4 * (lane >> 4) + r) * 17 + lr] = acc1[r];
+  }
+  SEG_STAMP(st, si);
+  __syncthreads();
+  SEG_STAMP(st, si + 1);
+  const int tid = threadIdx.x;
+  if (tid < 128) {
+    const int es = tid >> 6, q = tid & 63;
+    const int em = m0 + es;
+    const int row = q >> 2, c4 = 4 * (q & 3);
+    const float* r0 = red + (es * 8) * 16 * 17 + row * 17 + c4;
+    const float4 b4 = *reinterpret_cast<const float4*>(bias + 16 * n + c4);
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float sum = r0[i];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) sum += r0[k * 16 * 17 + i];
+      v[i] = sum;
+    }
+    v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
+    const uint32_t eoff = (uint32_t)((16 * em + row) * kD + 16 * n + c4);
+    const float4 xv = as_f4(ld_sc1(rx, eoff * 4));
+    const float4 y = make_float4(xv.x + v[0], xv.y + v[1], xv.z + v[2], xv.w + v[3]);
+    st_sc1(__builtin_bit_cast(u32x4v, y), rx, eoff * 4);
+  }
 }
 
 // one pair per block: the grid always has at least 16 * MT blocks (dec_seg_grid)
@@ -447,9 +545,10 @@ __device__ __forceinline__ void splitk_phase(const SplitW<KSW>& W, const _Float1
 }  // namespace
 
 // LDS: split-K reduction [2][4][16][17] f32 | LN tile [16][kAP] f16 | wave patches [8][16][17]
-constexpr int kRedF = 2 * 4 * 16 * 17;
+constexpr int kRedF = 2 * 8 * 16 * 17;  // [2 tiles][8 k-parts][16][17] (the quarter split uses half)
 constexpr int kPatchF = 8 * 16 * 17;
-constexpr size_t kSegLds = (size_t)kRedF * 4 + (size_t)16 * kAP * 2 + (size_t)kPatchF * 4;
+constexpr int kSegRows = 32;            // LayerNorm rows per block (MB = 2)
+constexpr size_t kSegLds = (size_t)kRedF * 4 + (size_t)kSegRows * kAP * 2 + (size_t)kPatchF * 4;
 
 // 128 VGPRs (four waves per SIMD): two blocks fit a CU, so a CU already holding other
 // blocks (the YIN grid beside the decoder) still takes one and the grid stays co-resident.
@@ -478,12 +577,15 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
   long long* st = seg_stamps(a.prof, 0);
   float* red = seg_smem;
   _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
-  float* patch = reinterpret_cast<float*>(sA + 16 * kAP);
+  float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
   const int lane = threadIdx.x & 63, wv = wave_id();
   const int B = a.B, MT = a.MT;
   const auto rx = rsrc(a.x, (uint32_t)B * kD * 4);
   const bool first = (int)blockIdx.x < 16 * MT;
-  uint32_t touched = touch_lng(a.wqk, 8 * kD, MT), sink = 0;
+  // the qk projection (N = 8d) at two m-tiles per block where one would leave a wave two
+  // weight tiles in a row (dec_seg_mb2): one weight round trip instead of two
+  const bool mb2 = dec_seg_mb2(8 * kD, MT);
+  uint32_t touched = mb2 ? touch_lng<2>(a.wqk, 8 * kD, MT) : touch_lng<1>(a.wqk, 8 * kD, MT), sink = 0;
   // phase 1: x += o Wo^T + bo (o from the self-attention launch)
   {
     SplitW<4> w;
@@ -497,7 +599,10 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
   {
     LngW w;
     LngOut o{a.xqk, 8 * kD, nullptr, nullptr, 0, 0, nullptr};
-    lng_phase<LE_F16>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, st, 19);
+    if (mb2)
+      lng_phase<LE_F16, 2>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, st, 19);
+    else
+      lng_phase<LE_F16, 1>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, st, 19);
   }
   // the touched dwords feed a store no reader looks at (word 150 of the counter block is
   // unused), taken with probability 2^-32: the loads cannot be dropped
@@ -511,7 +616,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
   long long* st = seg_stamps(a.prof, 1);
   float* red = seg_smem;
   _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
-  float* patch = reinterpret_cast<float*>(sA + 16 * kAP);
+  float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
   const int lane = threadIdx.x & 63, wv = wave_id();
   const int B = a.B, MT = a.MT;
   const auto rx = rsrc(a.x, (uint32_t)B * kD * 4);
@@ -546,8 +651,12 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
   grid_barrier(a.bar, 3, a.err, st);
   sink ^= touched;
   touched = a.wqkv ? touch_lng(a.wqkv, 3 * kD, MT) : 0u;
-  // phase 4: x += f W2^T + b2 (K = 4d: 16 k-steps per quarter)
-  {
+  // phase 4: x += f W2^T + b2 (K = 4d: eighths of K shared by the pair's two tiles, or
+  // 16 k-steps per quarter when the pair spans two column tiles, MT = 1)
+  if (MT % 2 == 0) {
+    if (first)
+      splitk8_pair(a.w2, blockIdx.x, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, st, 25);
+  } else {
     SplitW<16> w;
     if (first) splitk_prefetch<16>(w, a.w2, 4 * kD, blockIdx.x, MT, lane, wv);
     splitk_phase<16, SE_RESID, false>(w, a.w2, 4 * kD, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), 4 * kD, a.b2,
