@@ -533,14 +533,16 @@ class JanusPipeline:
                 return None
         # the last kv packets of the batch render on the decoder's CUs after its call (a
         # second vocoder context), the rest here: a decoder side that finishes early takes
-        # vocoder work the way the vocoder side takes YIN (JANUS_VOC_DEC_UTTS)
+        # vocoder work the way the vocoder side takes YIN (JANUS_VOC_DEC_UTTS; with the r05
+        # decoder segments: 3 / 4 / 5 -> 252.2-252.7 / 251.2-251.3 / 251.9-252.3 ms per step,
+        # profiles/r05_voc_dec_sweep2.txt)
         kv = 0
         pk_dec = []
         wav_b = pcm_b = None
         with torch.cuda.stream(vs):
             if res_prev is not None:
                 pk = res_prev.packets
-                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "2"))))
+                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "4"))))
                 pk_dec = pk[len(pk) - kv:] if kv else []
                 wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
             if pcm is not None:
