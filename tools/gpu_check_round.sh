@@ -29,7 +29,7 @@ timeout -k 10 300 python3 -u bench.py --config 1 --steps 5 --warmup 1 > $out/con
 tail -1 $out/config1.log > $out/config1.json
 timeout -k 10 300 python3 -u tools/stream_bench.py --model base.en > $out/stream5.log 2>&1 || { tail -20 $out/stream5.log; exit 1; }
 tail -1 $out/stream5.log > $out/stream5.json
-python3 $root/tools/conv_avg.py $out/kernel_stats.csv $out/bench_under_rocprof.json > $out/conv_avg.txt || true
+python3 $root/tools/conv_avg.py "$(find $out/prof -name "*.db" | head -1)" $out/bench_under_rocprof.json > $out/conv_avg.txt || true
 cut -c1-900 $out/bench.json
 cat $out/conv_avg.txt
 head -12 $out/kernel_top.txt

@@ -11,5 +11,5 @@ f=$(find $out/prof -name "*.db" | head -1)
 python3 $root/tools/rocprof_stats.py "$f" 60 --csv $out/kernel_stats.csv > $out/kernel_top.txt
 grep '"metric"' $out/prof.log > $out/bench_under_rocprof.json
 cd $root
-python3 tools/conv_avg.py $out/kernel_stats.csv $out/bench_under_rocprof.json > $out/conv_avg.txt || true
+python3 tools/conv_avg.py "$f" $out/bench_under_rocprof.json > $out/conv_avg.txt || true
 head -40 $out/kernel_top.txt | cut -c1-150
