@@ -254,7 +254,12 @@ typedef struct {
                               (d_model 512, 8 heads, <= 128 rows, >= 16 CUs per 16 rows; the
                               other shapes keep the launch path): 29 launches per position
                               at base.en instead of 75. Same arithmetic per row except the
-                              GEMMs' k order (fp32-rounding level, not bit-identical to 0) */
+                              GEMMs' k order (fp32-rounding level, not bit-identical to 0).
+                              2: one launch per layer step — segment B of layer l, the
+                              self-attention of l + 1 (one wave per row and head, online
+                              softmax over 64-key chunks) and segment A of l + 1 as one
+                              grid: 19 launches per position; the step measures level with
+                              1 (the attention phase's longest rows set its length) */
 } janus_decode_options;
 
 /*

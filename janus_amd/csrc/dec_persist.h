@@ -29,6 +29,15 @@ struct DecSegArgs {
   long long* prof;           // phase stamps (JANUS_PHASE_PROF builds, tools/seg_prof.py); null
 };
 
+// The layer kernel's segment A runs the NEXT layer's weights over the same buffers: only
+// these change against segment B's DecSegArgs (its qkv / kc / vc / pos / roff / o feed the
+// self-attention phase between them, 64-wide heads, scale 1/8).
+struct DecSegNext {
+  const _Float16* wo; const float* bo;
+  const float* ln2g; const float* ln2b;
+  const _Float16* wqk; const float* bqk;
+};
+
 // 16-row tiles for B rows (0: unsupported, B > 128)
 int dec_seg_mtiles(int B);
 // blocks of the resident grid on a partition of `cus` CUs (0: unsupported)
@@ -36,6 +45,9 @@ int dec_seg_grid(int B, int cus);
 bool dec_seg_supported(int d, int H, int B, int cus);
 void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s);
 void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s);
+// segment B of layer l (b: its args, with layer l + 1's QKV weights and cache), the
+// self-attention of l + 1 and segment A of l + 1 (nx: its weights) in one launch
+void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s);
 // JANUS_PHASE_PROF builds: the stamp buffer for layer l when JANUS_SEG_PROF=l, else null
 long long* dec_seg_prof_target(int l);
 

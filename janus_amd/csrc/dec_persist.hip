@@ -83,12 +83,13 @@ __device__ __forceinline__ float4 as_f4(u32x4v v) { return __builtin_bit_cast(fl
 // bar: [0] top, [16 * (1 + g)] group g (g < 8), [16 * 9] exit — 64-byte lines.
 // Phase stamps (JANUS_PHASE_PROF builds): thread 0 of every block writes the real-time
 // clock (100 MHz) at kernel start [0], at each barrier's arrival [2e - 1] (every wave
-// drained) and release [2e], before the exit [11]; [12] HW_ID, [13] XCC_ID; inside phase
-// p (1-based) wave 0's progress at [16 + 3 (p - 1) + i] (split-K: MFMAs done, reduction
-// synced; LayerNorm GEMM: LayerNorm synced, first tile's MFMAs done, its stores issued).
+// drained) and release [2e] (e <= 7), before the exit [15]; [16] HW_ID, [17] XCC_ID; inside
+// phase p (1-based, segment kernels) wave 0's progress at [18 + 3 (p - 1) + i] (split-K:
+// MFMAs done, reduction synced; LayerNorm GEMM: LayerNorm synced, first tile's MFMAs done,
+// its stores issued). 48 slots per block.
 #ifdef JANUS_PHASE_PROF
 #define SEG_STAMP(ST, I) do { if ((ST) && threadIdx.x == 0) (ST)[I] = (long long)wall_clock64(); } while (0)
-#define SEG_END(ST) do { __syncthreads(); SEG_STAMP(ST, 11); } while (0)
+#define SEG_END(ST) do { __syncthreads(); SEG_STAMP(ST, 15); } while (0)
 #else
 #define SEG_STAMP(ST, I) do { (void)(ST); } while (0)
 #define SEG_END(ST) do { (void)(ST); } while (0)
@@ -440,19 +441,21 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
                  (uint32_t)((grow * o.ldo + col) * 2));
       } else {
         const half4 h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-        _Float16* dst;
         if constexpr (EPI == LE_QKV) {
+          // write-through: the layer kernel's self-attention phase reads q and the new K/V
+          // rows in the same launch (the 16-column tile is in one of q / K / V: uniform)
           if (col < kD) {
-            dst = o.out + (int64_t)grow * o.ldo + col;
+            st_sc1_8(__builtin_bit_cast(u32x2v, h), rsrc(o.out, (uint32_t)B * o.ldo * 2),
+                     (uint32_t)((grow * o.ldo + col) * 2));
           } else {
             _Float16* cache = col < 2 * kD ? o.kc : o.vc;
             const int cpos = o.pos + (o.roff ? o.roff[grow] : 0);
-            dst = cache + ((int64_t)grow * o.n_ctx + cpos) * kD + (col % kD);
+            st_sc1_8(__builtin_bit_cast(u32x2v, h), rsrc(cache, (uint32_t)B * o.n_ctx * kD * 2),
+                     (uint32_t)(((grow * o.n_ctx + cpos) * kD + (col % kD)) * 2));
           }
         } else {
-          dst = o.out + (int64_t)grow * o.ldo + col;
+          *reinterpret_cast<half4*>(o.out + (int64_t)grow * o.ldo + col) = h;
         }
-        *reinterpret_cast<half4*>(dst) = h;
       }
     }
     if (li == wv) SEG_STAMP(st, si + 2);
@@ -559,11 +562,11 @@ constexpr size_t kSegLds = (size_t)kRedF * 4 + (size_t)kSegRows * kAP * 2 + (siz
 __device__ __forceinline__ long long* seg_stamps(long long* prof, int k) {
 #ifdef JANUS_PHASE_PROF
   if (prof) {
-    long long* st = prof + ((int64_t)k * 256 + blockIdx.x) * 32;
+    long long* st = prof + ((int64_t)k * 256 + blockIdx.x) * 48;
     if (threadIdx.x == 0) {
       st[0] = (long long)wall_clock64();
-      st[12] = (long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
-      st[13] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+      st[16] = (long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+      st[17] = (long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
     }
     return st;
   }
@@ -572,9 +575,12 @@ __device__ __forceinline__ long long* seg_stamps(long long* prof, int k) {
   return nullptr;
 }
 
-__global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
-  long long* st = seg_stamps(a.prof, 0);
+// Segment A after barrier epoch e0: x += o Wo^T + bo | barrier e0 + 1 | xqk = LN2(x) Wqk^T +
+// bqk. touched: the previous phase's L2 touch (folded into sink here, after the barrier that
+// ended that phase); pst: in-phase stamps (stand-alone kernels only).
+__device__ __forceinline__ void seg_a_body(const DecSegArgs& a, float* seg_smem, long long* st,
+                                           long long* pst, unsigned e0, uint32_t& touched,
+                                           uint32_t& sink) {
   float* red = seg_smem;
   _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
   float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
@@ -585,35 +591,34 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
   // the qk projection (N = 8d) at two m-tiles per block where one would leave a wave two
   // weight tiles in a row (dec_seg_mb2): one weight round trip instead of two
   const bool mb2 = dec_seg_mb2(8 * kD, MT);
-  uint32_t touched = mb2 ? touch_lng<2>(a.wqk, 8 * kD, MT) : touch_lng<1>(a.wqk, 8 * kD, MT), sink = 0;
-  // phase 1: x += o Wo^T + bo (o from the self-attention launch)
+  sink ^= touched;
+  touched = mb2 ? touch_lng<2>(a.wqk, 8 * kD, MT) : touch_lng<1>(a.wqk, 8 * kD, MT);
+  // phase 1: x += o Wo^T + bo (o from the self-attention launch / phase)
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.wo, kD, blockIdx.x, MT, lane, wv);
     splitk_phase<4, SE_RESID, false>(w, a.wo, kD, MT, rsrc(a.o, (uint32_t)B * kD * 2), kD, a.bo, rx, rx,
-                                     red, lane, wv, [] {}, st, 16);
+                                     red, lane, wv, [] {}, pst, 18);
   }
-  grid_barrier(a.bar, 1, a.err, st);
+  grid_barrier(a.bar, e0 + 1, a.err, st);
   sink ^= touched;
+  touched = 0u;
   // phase 2: xqk = LN2(x) Wqk^T + bqk (read by the cross-attention launch)
   {
     LngW w;
     LngOut o{a.xqk, 8 * kD, nullptr, nullptr, 0, 0, nullptr};
     if (mb2)
-      lng_phase<LE_F16, 2>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, st, 19);
+      lng_phase<LE_F16, 2>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, pst, 21);
     else
-      lng_phase<LE_F16, 1>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, st, 19);
+      lng_phase<LE_F16, 1>(w, a.wqk, 8 * kD, MT, B, rx, a.ln2g, a.ln2b, a.bqk, o, sA, patch, lane, wv, [] {}, pst, 21);
   }
-  // the touched dwords feed a store no reader looks at (word 150 of the counter block is
-  // unused), taken with probability 2^-32: the loads cannot be dropped
-  if ((sink ^ touched) == 0x5eed5eedu) a.bar[150] = 1u;
-  SEG_END(st);
-  grid_exit(a.bar);
 }
 
-__global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
-  long long* st = seg_stamps(a.prof, 1);
+// Segment B after barrier epoch e0 (phases 1-4, barriers e0 + 1 .. e0 + 3, and with the next
+// layer's weights phase 5 behind barrier e0 + 4).
+__device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem, long long* st,
+                                           long long* pst, unsigned e0, uint32_t& touched,
+                                           uint32_t& sink) {
   float* red = seg_smem;
   _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
   float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
@@ -622,60 +627,215 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
   const auto rx = rsrc(a.x, (uint32_t)B * kD * 4);
   const auto rom = rsrc(a.omid, (uint32_t)B * kD * 2);
   const bool first = (int)blockIdx.x < 16 * MT;
-  uint32_t touched = touch_splitk(a.woc, kD, MT), sink = 0;
+  sink ^= touched;
+  touched = touch_splitk(a.woc, kD, MT);
   // phase 1: o' = c_h Wv_h^T + bv (c from the cross-attention launch), sc1 out
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.wv, kD, blockIdx.x, MT, lane, wv);
     splitk_phase<4, SE_F16_SC1, true>(w, a.wv, kD, MT, rsrc(a.xc, (uint32_t)B * 8 * kD * 2), 8 * kD, a.bv,
-                                      rx, rom, red, lane, wv, [] {}, st, 16);
+                                      rx, rom, red, lane, wv, [] {}, pst, 18);
   }
-  grid_barrier(a.bar, 1, a.err, st);
+  grid_barrier(a.bar, e0 + 1, a.err, st);
   sink ^= touched;
   touched = touch_lng(a.w1, 4 * kD, MT);
   // phase 2: x += o' Wo_c^T + bo_c
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.woc, kD, blockIdx.x, MT, lane, wv);
-    splitk_phase<4, SE_RESID, false>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {}, st, 19);
+    splitk_phase<4, SE_RESID, false>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {}, pst, 21);
   }
-  grid_barrier(a.bar, 2, a.err, st);
+  grid_barrier(a.bar, e0 + 2, a.err, st);
   sink ^= touched;
   touched = touch_splitk(a.w2, 4 * kD, MT);
   // phase 3: f = gelu(LN3(x) W1^T + b1), sc1 out
   {
     LngW w;
     LngOut o{a.f, 4 * kD, nullptr, nullptr, 0, 0, nullptr};
-    lng_phase<LE_GELU_SC1>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {}, st, 22);
+    lng_phase<LE_GELU_SC1>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {}, pst, 24);
   }
-  grid_barrier(a.bar, 3, a.err, st);
+  grid_barrier(a.bar, e0 + 3, a.err, st);
   sink ^= touched;
   touched = a.wqkv ? touch_lng(a.wqkv, 3 * kD, MT) : 0u;
   // phase 4: x += f W2^T + b2 (K = 4d: eighths of K shared by the pair's two tiles, or
   // 16 k-steps per quarter when the pair spans two column tiles, MT = 1)
   if (MT % 2 == 0) {
     if (first)
-      splitk8_pair(a.w2, blockIdx.x, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, st, 25);
+      splitk8_pair(a.w2, blockIdx.x, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
   } else {
     SplitW<16> w;
     if (first) splitk_prefetch<16>(w, a.w2, 4 * kD, blockIdx.x, MT, lane, wv);
     splitk_phase<16, SE_RESID, false>(w, a.w2, 4 * kD, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), 4 * kD, a.b2,
-                                      rx, rx, red, lane, wv, [] {}, st, 25);
+                                      rx, rx, red, lane, wv, [] {}, pst, 27);
   }
-  // phase 5 (all but the last layer): the next layer's q and K/V cache rows
+  // phase 5 (all but the last layer): the next layer's q and K/V cache rows (write-through)
   if (a.wqkv) {
-    grid_barrier(a.bar, 4, a.err, st);
+    grid_barrier(a.bar, e0 + 4, a.err, st);
     sink ^= touched;
     touched = 0u;
     LngW w;
     LngOut o{a.qkv, 3 * kD, a.kc, a.vc, a.pos, a.n_ctx, a.roff};
-    lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, st, 28);
+    lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, pst, 30);
   }
-  // the touched dwords feed a store no reader looks at (word 150 of the counter block is
-  // unused), taken with probability 2^-32: the loads cannot be dropped
-  if ((sink ^ touched) == 0x5eed5eedu) a.bar[150] = 1u;
+}
+
+// Self-attention of one (row, head) per wave (B * 8 units over the grid's 8 waves per
+// block): decode_head_kernel's lane layout (lane: key 8r + (lane >> 3) of a round, dims
+// 8 (lane & 7) ..) over 64-key chunks (8 rounds, all 16 K / V loads of a chunk in flight),
+// online softmax across chunks (exp2 domain, explicit fmaf), the 8 key groups summed by
+// shuffles. The cache rows below the row's position come from earlier launches (loaded
+// non-temporal, as the launch path does); the chunk holding the newest row — written by
+// phase 5 of this launch — is loaded sc1, as is q.
+__device__ __forceinline__ void attn_phase(const DecSegArgs& g, int lane, int wv) {
+  // block j takes 4 heads of row p = j mod B/2 and 4 of row p + B/2: the staggered call's
+  // two slot sets (positions S apart) share every block, so no CU streams only long rows
+  // (one row per block: the longest rows' blocks took 34 us against a median of 25)
+  const int j = blockIdx.x, B = g.B;
+  if (j >= B) return;  // wave-uniform
+  int b, h;
+  if ((B & 1) == 0) {
+    const int half = B >> 1, p = j % half;
+    b = wv < 4 ? p : p + half;
+    h = (j >= half ? 4 : 0) + (wv & 3);
+  } else {
+    b = j;
+    h = wv;
+  }
+  const int kg = lane >> 3, dg = lane & 7;
+  const int cpos = g.pos + (g.roff ? g.roff[b] : 0);  // newest key of the row
+  const uint32_t kvbytes = (uint32_t)g.B * g.n_ctx * kD * 2;
+  const auto rk = rsrc(g.kc, kvbytes), rv = rsrc(g.vc, kvbytes);
+  constexpr float kScaleLog2 = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64), exp2 domain
+  float qv[8];
+  {
+    const half8 qh = as_h8(ld_sc1(rsrc(g.qkv, (uint32_t)g.B * 3 * kD * 2),
+                                  (uint32_t)((b * 3 * kD + h * 64 + dg * 8) * 2)));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = (float)qh[j] * kScaleLog2;
+  }
+  const uint32_t rowoff = (uint32_t)(((b * g.n_ctx) * kD + h * 64 + dg * 8) * 2);
+  float m_run = -INFINITY, l_run = 0.f, acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int nch = (cpos + 64) / 64;
+  for (int c = 0; c < nch; ++c) {
+    u32x4v kr[8], vr[8];
+    const bool newest = c == nch - 1;  // wave-uniform
+    if (newest) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t off = rowoff + (uint32_t)min(64 * c + 8 * r + kg, cpos) * (kD * 2);
+        kr[r] = ld_sc1(rk, off);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t off = rowoff + (uint32_t)min(64 * c + 8 * r + kg, cpos) * (kD * 2);
+        vr[r] = ld_sc1(rv, off);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t off = rowoff + (uint32_t)(64 * c + 8 * r + kg) * (kD * 2);
+        kr[r] = __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 2);  // nt
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t off = rowoff + (uint32_t)(64 * c + 8 * r + kg) * (kD * 2);
+        vr[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 2);
+      }
+    }
+    float sc[8], cm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const half8 k8 = as_h8(kr[r]);
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot = fmaf((float)k8[j], qv[j], dot);
+      dot += __shfl_xor(dot, 1);
+      dot += __shfl_xor(dot, 2);
+      dot += __shfl_xor(dot, 4);
+      sc[r] = 64 * c + 8 * r + kg <= cpos ? dot : -INFINITY;
+      cm = fmaxf(cm, sc[r]);
+    }
+    cm = fmaxf(cm, __shfl_xor(cm, 8));
+    cm = fmaxf(cm, __shfl_xor(cm, 16));
+    cm = fmaxf(cm, __shfl_xor(cm, 32));
+    const float m_new = fmaxf(m_run, cm);  // finite: every chunk holds key 64c <= cpos
+    const float alpha = exp2f(m_run - m_new);
+    l_run *= alpha;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= alpha;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float p = exp2f(sc[r] - m_new);  // -inf -> 0
+      l_run += p;
+      const half8 v8 = as_h8(vr[r]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(p, (float)v8[j], acc[j]);
+    }
+    m_run = m_new;
+  }
+  // the 8 key groups (lanes sharing dg) share m_run: plain sums
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    l_run += __shfl_xor(l_run, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += __shfl_xor(acc[j], o);
+  }
+  if (kg == 0) {
+    const float il = 1.0f / l_run;
+    half8 o8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o8[j] = (_Float16)(acc[j] * il);
+    st_sc1(__builtin_bit_cast(u32x4v, o8), rsrc(g.o, (uint32_t)g.B * kD * 2),
+           (uint32_t)((b * kD + h * 64 + dg * 8) * 2));
+  }
+}
+
+// the touched dwords feed a store no reader looks at (word 150 of the counter block is
+// unused), taken with probability 2^-32: the loads cannot be dropped
+#define SEG_SINK(A, T, S) do { if (((S) ^ (T)) == 0x5eed5eedu) (A).bar[150] = 1u; } while (0)
+
+__global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  long long* st = seg_stamps(a.prof, 0);
+  uint32_t touched = 0u, sink = 0u;
+  seg_a_body(a, seg_smem, st, st, 0, touched, sink);
+  SEG_SINK(a, touched, sink);
   SEG_END(st);
   grid_exit(a.bar);
+}
+
+__global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  long long* st = seg_stamps(a.prof, 1);
+  uint32_t touched = 0u, sink = 0u;
+  seg_b_body(a, seg_smem, st, st, 0, touched, sink);
+  SEG_SINK(a, touched, sink);
+  SEG_END(st);
+  grid_exit(a.bar);
+}
+
+// One launch per layer step (r05): segment B of layer l (its phase 5 writes layer l + 1's q
+// and K/V rows write-through) | barrier 5 | the self-attention of layer l + 1 | barrier 6 |
+// segment A of layer l + 1 — the launches between two cross-attentions as one grid.
+__global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSegNext nx) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  long long* st = seg_stamps(bsg.prof, 2);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  uint32_t touched = 0u, sink = 0u;
+  seg_b_body(bsg, seg_smem, st, nullptr, 0, touched, sink);
+  grid_barrier(bsg.bar, 5, bsg.err, st);
+  sink ^= touched;
+  touched = touch_splitk(nx.wo, kD, bsg.MT);
+  attn_phase(bsg, lane, wv);
+  grid_barrier(bsg.bar, 6, bsg.err, st);
+  DecSegArgs asg = bsg;
+  asg.wo = nx.wo; asg.bo = nx.bo; asg.ln2g = nx.ln2g; asg.ln2b = nx.ln2b; asg.wqk = nx.wqk; asg.bqk = nx.bqk;
+  seg_a_body(asg, seg_smem, st, nullptr, 6, touched, sink);
+  SEG_SINK(bsg, touched, sink);
+  SEG_END(st);
+  grid_exit(bsg.bar);
 }
 
 int dec_seg_grid(int B, int cus) {
@@ -719,10 +879,19 @@ void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s) {
   JANUS_LAUNCH_CHECK();
 }
 
+void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_layer_kernel); attr = true; }
+  JANUS_CHECK(b.B * 8 <= grid * (kNT / 64) && b.wqkv != nullptr && b.qkv != nullptr,
+              "decoder layer kernel: one (row, head) per wave and a next layer");
+  dec_layer_kernel<<<grid, kNT, kSegLds, s>>>(b, nx);
+  JANUS_LAUNCH_CHECK();
+}
+
 #ifdef JANUS_PHASE_PROF
-// JANUS_SEG_PROF=l: every seg_a / seg_b launch of layer l stamps into one buffer (graph
-// replays included), so it holds the last such launch of the run
-__device__ long long g_seg_prof[2 * 256 * 32];  // a device global: no allocation under capture
+// JANUS_SEG_PROF=l: every seg_a / seg_b / layer launch of layer l stamps into one buffer
+// (graph replays included), so it holds the last such launch of the run
+__device__ long long g_seg_prof[3 * 256 * 48];  // a device global: no allocation under capture
 long long* dec_seg_prof_target(int l) {
   static const int want = std::getenv("JANUS_SEG_PROF") ? std::atoi(std::getenv("JANUS_SEG_PROF")) : -1;
   if (l != want) return nullptr;
@@ -732,8 +901,8 @@ long long* dec_seg_prof_target(int l) {
 }
 }  // namespace janus
 extern "C" int janus_debug_seg_read(long long* dst, int cap) {
-  const int n = std::min(cap, 2 * 256);
-  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(janus::g_seg_prof), sizeof(long long) * 32 * (size_t)n, 0,
+  const int n = std::min(cap, 3 * 256);
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(janus::g_seg_prof), sizeof(long long) * 48 * (size_t)n, 0,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;

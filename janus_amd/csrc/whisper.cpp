@@ -647,6 +647,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const int seg_grid = opt->persistent ? dec_seg_grid(B, cus) : 0;
   const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && xabs && !shared && !fused_ln &&
                        !ln_fuse && !rln && ngroups == 0 && npairs == 0;
+  // persistent = 2: segment B of layer l, the self-attention of l + 1 and its segment A as
+  // ONE launch per layer step (dec_layer_kernel): 29 -> 19 launches per position
+  const bool layerk = persist && opt->persistent >= 2 && B * 8 <= seg_grid * 8;
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
     if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed
@@ -712,14 +715,23 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
           kv_store_launch(qkv, d, pos, NC, kc, vc, B, s);
         }
       }
-      decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
-                                    part_o, part_ml, s, roff, max_roff);
+      // (layer kernel: layers > 0 got their self-attention and segment A in the previous
+      // layer's launch)
+      if (!(layerk && l > 0))
+        decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
+                                      part_o, part_ml, s, roff, max_roff);
       if (persist) {
         const DecSegArgs g = seg_args(l, pos);
-        dec_seg_a_launch(g, seg_grid, s);
+        if (!(layerk && l > 0)) dec_seg_a_launch(g, seg_grid, s);
         xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
                      s, true, nullptr, 0);
-        dec_seg_b_launch(g, seg_grid, s);
+        if (layerk && l + 1 < nl) {
+          DecLayer& N = w->dec[l + 1];
+          const DecSegNext nx{N.wo.as<_Float16>(), N.bo, N.ln2g, N.ln2b, N.wqk.as<_Float16>(), N.bqk.as<float>()};
+          dec_layer_launch(g, nx, seg_grid, s);
+        } else {
+          dec_seg_b_launch(g, seg_grid, s);
+        }
         continue;
       }
       if (rln2) resid_ln(o, L.wo, L.bo, L.ln2g, L.ln2b);
@@ -811,7 +823,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
       (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
       (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows, (int64_t)roff,
-      (int64_t)max_roff, (int64_t)persist, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
+      (int64_t)max_roff, (int64_t)persist + (int64_t)layerk, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
       (int64_t)Z.d_segerr.p};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {

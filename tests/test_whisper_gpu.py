@@ -506,18 +506,21 @@ def test_layernorm_placements_bit_identical(base_engine, gpu, monkeypatch, env):
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
 
 
-def test_persistent_segments_vs_oracle(base_engine, gpu):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_persistent_segments_vs_oracle(base_engine, gpu, mode):
     """The persistent decoder segments (janus_decode_options.persistent: per layer two
     resident-grid launches with in-launch barriers instead of ten launches) decode base.en
     free-running to 448 tokens like the oracle — identical, or first divergence at an
     oracle near-tie — and agree with the launch path on the gate inputs (sum of chosen
-    log-probs within 1e-3 where the sequences match, no-speech probability within 0.5 %)."""
+    log-probs within 1e-3 where the sequences match, no-speech probability within 0.5 %).
+    mode 2: the layer kernel (segment B, the next layer's self-attention and its segment A in
+    one launch per layer step)."""
     eng, W = base_engine
     secs = [30.0, 17.0, 8.0, 3.0, 1.0, 0.3, 24.0, 12.0]
     utts = [synth_speech(140 + k, s) for k, s in enumerate(secs)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    per = eng.decode_ex(enc, max_length=448, persistent=1)
+    per = eng.decode_ex(enc, max_length=448, persistent=mode)
     lau = eng.decode_ex(enc, max_length=448, persistent=0)
     torch.cuda.synchronize()
     tk = eng.tokenizer
@@ -526,7 +529,7 @@ def test_persistent_segments_vs_oracle(base_engine, gpu):
     assert (nt >= 128).all()
     ref = ow.greedy_cached(enc.float().cpu(), W, BASE, tk, 448, no_speech=50361)
     seq, pk = _check_free_running(per.tokens.cpu().numpy(), ref, tk, plen, nt)
-    print(f"persistent segments, base.en free-running: sequences identical {seq:.3f}, packets {pk:.3f}")
+    print(f"persistent mode {mode}, base.en free-running: sequences identical {seq:.3f}, packets {pk:.3f}")
     assert seq >= 0.75 and pk >= 0.75
     pt, lt = per.tokens.cpu(), lau.tokens.cpu()
     for b in range(len(utts)):
@@ -537,8 +540,8 @@ def test_persistent_segments_vs_oracle(base_engine, gpu):
         assert abs(a - c) <= 5e-3 * c + 1e-12, (b, a, c)
 
 
-@pytest.mark.parametrize("rows", [40, 64])
-def test_persistent_staggered_bit_identical(base_engine, gpu, rows):
+@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2)])
+def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode):
     """Continuous batching through the persistent segments: two slot sets of `rows` rows
     (2 x 64 = the bench's decoder call), each batch started fresh in one call and continued
     in the next, equal a full persistent decode of that batch alone bit for bit — a row's
@@ -552,7 +555,7 @@ def test_persistent_staggered_bit_identical(base_engine, gpu, rows):
         batches.append(eng.encode(eng.logmel(pcm, offs, rows, 3)))
     # the same launch geometry on both sides (cu_count sets the vocabulary projection's
     # block count, whose partial merge order reaches the log-prob sums' last bits)
-    ref = [eng.decode_ex(e, max_length=L, persistent=1, cu_count=128) for e in batches]
+    ref = [eng.decode_ex(e, max_length=L, persistent=mode, cu_count=128) for e in batches]
     sets = [None, None]
     got = {}
     for call in range(4):
@@ -569,7 +572,7 @@ def test_persistent_staggered_bit_identical(base_engine, gpu, rows):
                 offs += [0 if st == fresh else S] * rows
         if call == 0:
             offs = [0] * (2 * rows)
-        out = eng.decode_ex(torch.cat(rows_enc), max_length=L, pos_offset=offs, steps=S, persistent=1,
+        out = eng.decode_ex(torch.cat(rows_enc), max_length=L, pos_offset=offs, steps=S, persistent=mode,
                             cu_count=128)
         if call > 0 and sets[cont] is not None:
             bi = sets[cont]

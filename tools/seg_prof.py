@@ -19,18 +19,19 @@ sys.path.insert(0, ROOT)
 
 
 def summarize(p, nbar):
-    """p: [blocks][32] stamps of one launch (10 ns ticks)."""
+    """p: [blocks][48] stamps of one launch (10 ns ticks): [0] start, [2e-1] / [2e] barrier e
+    arrival / release, [15] end, marks of phase p at [18 + 3 (p - 1) + i]."""
     p = p[p[:, 0] > 0]
     if len(p) == 0:
         return None
     us = lambda v: round(float(v) / 100.0, 2)  # noqa: E731
     t0 = p[:, 0].min()
-    out = {"blocks": int(len(p)), "span_us": us(p[:, 11].max() - t0),
+    out = {"blocks": int(len(p)), "span_us": us(p[:, 15].max() - t0),
            "start_skew_us": us(p[:, 0].max() - t0), "phases": []}
     prev = p[:, 0]
     for e in range(1, nbar + 2):
-        arr = p[:, 11] if e == nbar + 1 else p[:, 2 * e - 1]
-        inner = [p[:, 16 + 3 * (e - 1) + i] for i in range(3)]
+        arr = p[:, 15] if e == nbar + 1 else p[:, 2 * e - 1]
+        inner = [p[:, 18 + 3 * (e - 1) + i] for i in range(3)] if e <= 5 else [p[:, 0] * 0] * 3
         ph = {"compute_med_us": us(np.median(arr - prev)), "compute_max_us": us((arr - prev).max()),
               # wave 0's marks inside the phase, from the phase start (medians)
               "marks_med_us": [us(np.median(m - prev)) if (m > 0).all() else None for m in inner],
@@ -54,11 +55,12 @@ def main():
     bench.main()
     fn = _native.lib().janus_debug_seg_read
     fn.argtypes = [ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
-    buf = np.zeros((512, 32), dtype=np.int64)
-    n = fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), 512)
-    assert n == 512, n
+    buf = np.zeros((768, 48), dtype=np.int64)
+    n = fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), 768)
+    assert n == 768, n
     res = {"layer": int(os.environ["JANUS_SEG_PROF"]),
-           "seg_a": summarize(buf[:256], 1), "seg_b": summarize(buf[256:], 4)}
+           "seg_a": summarize(buf[:256], 1), "seg_b": summarize(buf[256:512], 4),
+           "layer_kernel": summarize(buf[512:], 7)}
     print(json.dumps(res))
 
 
