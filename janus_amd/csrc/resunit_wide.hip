@@ -596,8 +596,10 @@ struct LdsGeo {
 
 // EPF: load the residual / accumulator rows at c2's start (in flight during its MFMAs)
 // instead of after its last k-block (costs 2*NE*4 VGPRs across the c2 loop).
-template <int C, bool EPF, int V>
-__global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel(ResUnitArgs a,
+// KC / DC: the unit's (k, d) at compile time (0: run-time a.k / a.d) — Firefly's nine
+// ResBlock1 geometries get constant tap offsets, k-block counts and staged-row counts
+template <int C, bool EPF, int V, int KC = 0, int DC = 0>
+__global__ __launch_bounds__((LdsGeo<C, V>::NT), 3) void resunit_wide_lds_kernel(ResUnitArgs a,
                                                                          int tiles_per_utt) {
   using G = LdsGeo<C, V>;
   constexpr int BM = G::BM, WM = G::WM, KB = G::KB, NT = G::NT, LI = G::LI, LW = G::LW;
@@ -609,7 +611,7 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
   float* sE = reinterpret_cast<float*>(smem);  // [BM][ES] epilogue (over sS and sW)
   _Float16* sW = smem + G::ACT_H;              // [2][C][LW]
 
-  const int k = a.k, d = a.d, T = a.T;
+  const int k = KC ? KC : a.k, d = DC ? DC : a.d, T = a.T;
   const int p1 = d * (k - 1) / 2, p2 = (k - 1) / 2;
   const int R1 = BM + 2 * p2;                  // c1 rows c2 reads
   const int R0 = MT1 * 16 + (k - 1) * d;       // x rows c1 reads
@@ -833,12 +835,11 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 2) void resunit_wide_lds_kernel
 #undef WIDE_WSTORE
 #undef WIDE_KLOOP
 
-template <int C, bool EPF, int V>
-static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
+template <int C, bool EPF, int V, int KC, int DC>
+static void lds_go(const ResUnitArgs& a, hipStream_t s) {
   using G = LdsGeo<C, V>;
-  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
   static_assert(G::LDS <= 160 * 1024, "LDS");
-  auto kern = resunit_wide_lds_kernel<C, EPF, V>;
+  auto kern = resunit_wide_lds_kernel<C, EPF, V, KC, DC>;
   static bool attr = false;
   if (!attr) {
     JANUS_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -848,6 +849,26 @@ static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
   const int tiles_per_utt = (a.T + G::BM - 1) / G::BM;
   kern<<<(unsigned)(tiles_per_utt * a.B), G::NT, G::LDS, s>>>(a, tiles_per_utt);
   JANUS_LAUNCH_CHECK();
+}
+
+template <int C, bool EPF, int V>
+static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
+  JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
+  // Firefly-GAN's ResBlock1 geometry (k in {3, 7, 11} x d in {1, 3, 5}) compiled per (k, d)
+  // for C = 64 (r05; JANUS_WIDE_LDS_RT=1: the run-time form, A/B); any other (k, d) and C
+  // run the run-time form
+  static const bool rt = std::getenv("JANUS_WIDE_LDS_RT") != nullptr;
+  if constexpr (C == 64 && V == 0) {
+    if (!rt) {
+#define JANUS_LDS_KD(K_, D_) \
+      if (a.k == K_ && a.d == D_) return lds_go<C, EPF, V, K_, D_>(a, s);
+      JANUS_LDS_KD(3, 1) JANUS_LDS_KD(3, 3) JANUS_LDS_KD(3, 5)
+      JANUS_LDS_KD(7, 1) JANUS_LDS_KD(7, 3) JANUS_LDS_KD(7, 5)
+      JANUS_LDS_KD(11, 1) JANUS_LDS_KD(11, 3) JANUS_LDS_KD(11, 5)
+#undef JANUS_LDS_KD
+    }
+  }
+  lds_go<C, EPF, V, 0, 0>(a, s);
 }
 
 bool resunit_wide_supported(int C, int k, int d) {
