@@ -855,8 +855,9 @@ template <int C, bool EPF, int V>
 static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_CHECK((a.k - 1) * a.d <= 50 && a.k <= 11, "resunit (wide): (k-1)*d must be <= 50, k <= 11");
   // Firefly-GAN's ResBlock1 geometry (k in {3, 7, 11} x d in {1, 3, 5}) compiled per (k, d)
-  // for C = 64 (r05; JANUS_WIDE_LDS_RT=1: the run-time form, A/B); any other (k, d) and C
-  // run the run-time form
+  // for C = 64 (r05; JANUS_WIDE_LDS_RT=1: the run-time form, A/B): standalone 64 x 30 s
+  // forward, C = 64 units 29.7-29.8 vs 30.7 ms; step 250.3-251.2 vs 251.5-251.9 ms
+  // (profiles/r05_c64_kd_ab.txt); any other (k, d) and C run the run-time form
   static const bool rt = std::getenv("JANUS_WIDE_LDS_RT") != nullptr;
   if constexpr (C == 64 && V == 0) {
     if (!rt) {
