@@ -870,7 +870,11 @@ def main():
         traffic = None
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("bytes_per_launch")
+            # measured on a standalone forward of tj["batch"] utterances; the line's launches
+            # are the main vocoder context's, which renders B minus the utterances the
+            # staggered step hands to the decoder's CUs: bytes scale with the utterances
+            main_b = B - int(getattr(pipe, "voc_dec_utts", 0) or 0)
+            traffic = tj.get("bytes_per_launch") * main_b / float(tj.get("batch", 64))
         except Exception:
             traffic = None
         out = {

@@ -543,6 +543,7 @@ class JanusPipeline:
             if res_prev is not None:
                 pk = res_prev.packets
                 kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "4"))))
+                self.voc_dec_utts = kv   # the main vocoder context renders the other len(pk) - kv
                 pk_dec = pk[len(pk) - kv:] if kv else []
                 wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
             if pcm is not None:
