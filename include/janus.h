@@ -258,8 +258,9 @@ typedef struct {
                               2: one launch per layer step — segment B of layer l, the
                               self-attention of l + 1 (one wave per row and head, online
                               softmax over 64-key chunks) and segment A of l + 1 as one
-                              grid: 19 launches per position; the step measures level with
-                              1 (the attention phase's longest rows set its length) */
+                              grid: 19 launches per position (every row's keys in two
+                              parts cut by its own length, merged in order: rows stay
+                              independent of their neighbours) */
 } janus_decode_options;
 
 /*

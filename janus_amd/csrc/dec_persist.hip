@@ -679,70 +679,54 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   }
 }
 
-// Self-attention of one (row, head) per wave (B * 8 units over the grid's 8 waves per
-// block): decode_head_kernel's lane layout (lane: key 8r + (lane >> 3) of a round, dims
-// 8 (lane & 7) ..) over 64-key chunks (8 rounds, all 16 K / V loads of a chunk in flight),
-// online softmax across chunks (exp2 domain, explicit fmaf), the 8 key groups summed by
-// shuffles. The cache rows below the row's position come from earlier launches (loaded
-// non-temporal, as the launch path does); the chunk holding the newest row — written by
-// phase 5 of this launch — is loaded sc1, as is q.
-__device__ __forceinline__ void attn_phase(const DecSegArgs& g, int lane, int wv) {
-  // block j takes 4 heads of row p = j mod B/2 and 4 of row p + B/2: the staggered call's
-  // two slot sets (positions S apart) share every block, so no CU streams only long rows
-  // (one row per block: the longest rows' blocks took 34 us against a median of 25)
-  const int j = blockIdx.x, B = g.B;
-  if (j >= B) return;  // wave-uniform
-  int b, h;
-  if ((B & 1) == 0) {
-    const int half = B >> 1, p = j % half;
-    b = wv < 4 ? p : p + half;
-    h = (j >= half ? 4 : 0) + (wv & 3);
-  } else {
-    b = j;
-    h = wv;
-  }
+// Self-attention phase of the layer kernel: decode_head_kernel's lane layout (lane: key
+// 8r + (lane >> 3) of a round, dims 8 (lane & 7) ..) over 64-key chunks, all 16 K / V loads
+// of a chunk in flight, online softmax across chunks (exp2 domain, explicit fmaf), the 8
+// key groups summed by shuffles. Cache rows below a row's position come from earlier
+// launches (loaded non-temporal, as the launch path does); the chunk holding the newest
+// row — written by phase 5 of this launch — is loaded sc1, as is q.
+struct AttnState {
+  float m, l, acc[8];
+};
+
+__device__ __forceinline__ void attn_init(AttnState& t) {
+  t.m = -INFINITY;
+  t.l = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t.acc[j] = 0.f;
+}
+
+__device__ __forceinline__ void attn_q(const DecSegArgs& g, int b, int h, int dg, float (&qv)[8]) {
+  constexpr float kScaleLog2 = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64), exp2 domain
+  const half8 qh = as_h8(ld_sc1(rsrc(g.qkv, (uint32_t)g.B * 3 * kD * 2),
+                                (uint32_t)((b * 3 * kD + h * 64 + dg * 8) * 2)));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) qv[j] = (float)qh[j] * kScaleLog2;
+}
+
+// keys [k0, k1) (k0 a multiple of 64, k1 <= cpos + 1) of row b, head h into the state
+__device__ __forceinline__ void attn_keys(const DecSegArgs& g, int b, int h, int k0, int k1, int cpos,
+                                          const float (&qv)[8], AttnState& t, int lane) {
   const int kg = lane >> 3, dg = lane & 7;
-  const int cpos = g.pos + (g.roff ? g.roff[b] : 0);  // newest key of the row
   const uint32_t kvbytes = (uint32_t)g.B * g.n_ctx * kD * 2;
   const auto rk = rsrc(g.kc, kvbytes), rv = rsrc(g.vc, kvbytes);
-  constexpr float kScaleLog2 = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64), exp2 domain
-  float qv[8];
-  {
-    const half8 qh = as_h8(ld_sc1(rsrc(g.qkv, (uint32_t)g.B * 3 * kD * 2),
-                                  (uint32_t)((b * 3 * kD + h * 64 + dg * 8) * 2)));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qv[j] = (float)qh[j] * kScaleLog2;
-  }
   const uint32_t rowoff = (uint32_t)(((b * g.n_ctx) * kD + h * 64 + dg * 8) * 2);
-  float m_run = -INFINITY, l_run = 0.f, acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  const int nch = (cpos + 64) / 64;
-  for (int c = 0; c < nch; ++c) {
+  for (int c0 = k0; c0 < k1; c0 += 64) {
     u32x4v kr[8], vr[8];
-    const bool newest = c == nch - 1;  // wave-uniform
-    if (newest) {
+    if (c0 + 64 > cpos) {  // wave-uniform: the chunk holding the newest row
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t off = rowoff + (uint32_t)min(64 * c + 8 * r + kg, cpos) * (kD * 2);
-        kr[r] = ld_sc1(rk, off);
-      }
+      for (int r = 0; r < 8; ++r)
+        kr[r] = ld_sc1(rk, rowoff + (uint32_t)min(c0 + 8 * r + kg, cpos) * (kD * 2));
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t off = rowoff + (uint32_t)min(64 * c + 8 * r + kg, cpos) * (kD * 2);
-        vr[r] = ld_sc1(rv, off);
-      }
+      for (int r = 0; r < 8; ++r)
+        vr[r] = ld_sc1(rv, rowoff + (uint32_t)min(c0 + 8 * r + kg, cpos) * (kD * 2));
     } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t off = rowoff + (uint32_t)(64 * c + 8 * r + kg) * (kD * 2);
-        kr[r] = __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 2);  // nt
-      }
+      for (int r = 0; r < 8; ++r)
+        kr[r] = __builtin_amdgcn_raw_buffer_load_b128(rk, rowoff + (uint32_t)(c0 + 8 * r + kg) * (kD * 2), 0, 2);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t off = rowoff + (uint32_t)(64 * c + 8 * r + kg) * (kD * 2);
-        vr[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 2);
-      }
+      for (int r = 0; r < 8; ++r)
+        vr[r] = __builtin_amdgcn_raw_buffer_load_b128(rv, rowoff + (uint32_t)(c0 + 8 * r + kg) * (kD * 2), 0, 2);
     }
     float sc[8], cm = -INFINITY;
 #pragma unroll
@@ -754,41 +738,109 @@ __device__ __forceinline__ void attn_phase(const DecSegArgs& g, int lane, int wv
       dot += __shfl_xor(dot, 1);
       dot += __shfl_xor(dot, 2);
       dot += __shfl_xor(dot, 4);
-      sc[r] = 64 * c + 8 * r + kg <= cpos ? dot : -INFINITY;
+      sc[r] = c0 + 8 * r + kg < k1 ? dot : -INFINITY;
       cm = fmaxf(cm, sc[r]);
     }
     cm = fmaxf(cm, __shfl_xor(cm, 8));
     cm = fmaxf(cm, __shfl_xor(cm, 16));
     cm = fmaxf(cm, __shfl_xor(cm, 32));
-    const float m_new = fmaxf(m_run, cm);  // finite: every chunk holds key 64c <= cpos
-    const float alpha = exp2f(m_run - m_new);
-    l_run *= alpha;
+    const float m_new = fmaxf(t.m, cm);  // finite: every chunk holds key c0 < k1
+    const float alpha = exp2f(t.m - m_new);
+    t.l *= alpha;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] *= alpha;
+    for (int j = 0; j < 8; ++j) t.acc[j] *= alpha;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float p = exp2f(sc[r] - m_new);  // -inf -> 0
-      l_run += p;
+      t.l += p;
       const half8 v8 = as_h8(vr[r]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = fmaf(p, (float)v8[j], acc[j]);
+      for (int j = 0; j < 8; ++j) t.acc[j] = fmaf(p, (float)v8[j], t.acc[j]);
     }
-    m_run = m_new;
+    t.m = m_new;
   }
-  // the 8 key groups (lanes sharing dg) share m_run: plain sums
+  // the 8 key groups (lanes sharing dg) share m: plain sums
 #pragma unroll
   for (int o = 8; o < 64; o <<= 1) {
-    l_run += __shfl_xor(l_run, o);
+    t.l += __shfl_xor(t.l, o);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += __shfl_xor(acc[j], o);
+    for (int j = 0; j < 8; ++j) t.acc[j] += __shfl_xor(t.acc[j], o);
   }
-  if (kg == 0) {
-    const float il = 1.0f / l_run;
+}
+
+__device__ __forceinline__ void attn_store(const DecSegArgs& g, int b, int h, const AttnState& t, int lane) {
+  if ((lane >> 3) == 0) {
+    const float il = 1.0f / t.l;
     half8 o8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o8[j] = (_Float16)(acc[j] * il);
+    for (int j = 0; j < 8; ++j) o8[j] = (_Float16)(t.acc[j] * il);
     st_sc1(__builtin_bit_cast(u32x4v, o8), rsrc(g.o, (uint32_t)g.B * kD * 2),
-           (uint32_t)((b * kD + h * 64 + dg * 8) * 2));
+           (uint32_t)((b * kD + h * 64 + (lane & 7) * 8) * 2));
+  }
+}
+
+// Work split. Every row's keys are cut in two parts by its own length only (the first
+// s(n) = 64 ceil(n / 128) keys and the rest), so a row's arithmetic — part one, part two,
+// merged in that order — does not depend on the rows beside it (staggered bit-identity).
+// Block j takes head group 4 (j >= H2) .. + 3 of rows a = j mod H2 and b = a + H2 (H2 =
+// ceil(B / 2): in the staggered call one row of each slot set, S positions apart); waves w
+// and w + 4 share head h: wave w runs a's first part and b's second, wave w + 4 b's first
+// and a's second — about the same keys on every wave whatever the two rows' lengths (one
+// (row, head) per wave left the longest rows' waves with three times the shortest's keys)
+// — and each finishes its first-part row with the partner's second part through LDS.
+__device__ __forceinline__ int attn_split(int n) { return min(n, 64 * ((n + 127) / 128)); }
+
+__device__ __forceinline__ void attn_phase(const DecSegArgs& g, float* lds, int lane, int wv) {
+  const int B = g.B, H2 = (B + 1) >> 1;
+  const int j = blockIdx.x;
+  if (j >= 2 * H2) return;  // block-uniform
+  const int p = j % H2;
+  const int h = (j >= H2 ? 4 : 0) + (wv & 3);
+  const bool hasb = p + H2 < B;
+  // this wave's first-part row r1 and second-part row r2
+  const int r1 = wv < 4 ? p : p + H2, r2 = wv < 4 ? p + H2 : p;
+  const bool has1 = wv < 4 || hasb, has2 = wv < 4 ? hasb : true;
+  float qv[8];
+  // second part first, straight to the partner's LDS slot (one state live at a time)
+  float* mine = lds + ((wv & 3) * 2 + (wv >> 2)) * 80;       // [8 lanes][8 acc] + [m, l]
+  const float* other = lds + ((wv & 3) * 2 + 1 - (wv >> 2)) * 80;
+  {
+    AttnState t2;
+    attn_init(t2);
+    if (has2) {
+      const int c2 = g.pos + (g.roff ? g.roff[r2] : 0);
+      const int s2 = attn_split(c2 + 1);
+      if (s2 < c2 + 1) {
+        attn_q(g, r2, h, lane & 7, qv);
+        attn_keys(g, r2, h, s2, c2 + 1, c2, qv, t2, lane);
+      }
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mine[lane * 8 + q] = t2.acc[q];
+      if (lane == 0) { mine[64] = t2.m; mine[65] = t2.l; }
+    }
+  }
+  AttnState t1;
+  attn_init(t1);
+  if (has1) {
+    const int c1 = g.pos + (g.roff ? g.roff[r1] : 0);
+    attn_q(g, r1, h, lane & 7, qv);
+    attn_keys(g, r1, h, 0, attn_split(c1 + 1), c1, qv, t1, lane);
+  }
+  __syncthreads();
+  if (has1) {
+    const float m2 = other[64], l2 = other[65];
+    if (m2 != -INFINITY) {  // the row has a second part (block-uniform per pair)
+      const float M = fmaxf(t1.m, m2);
+      const float f1 = exp2f(t1.m - M), f2 = exp2f(m2 - M);
+      t1.l = t1.l * f1 + l2 * f2;
+      if (lane < 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t1.acc[q] = t1.acc[q] * f1 + other[lane * 8 + q] * f2;
+      }
+    }
+    attn_store(g, r1, h, t1, lane);
   }
 }
 
@@ -828,7 +880,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
   grid_barrier(bsg.bar, 5, bsg.err, st);
   sink ^= touched;
   touched = touch_splitk(nx.wo, kD, bsg.MT);
-  attn_phase(bsg, lane, wv);
+  attn_phase(bsg, seg_smem, lane, wv);
   grid_barrier(bsg.bar, 6, bsg.err, st);
   DecSegArgs asg = bsg;
   asg.wo = nx.wo; asg.bo = nx.bo; asg.ln2g = nx.ln2g; asg.ln2b = nx.ln2b; asg.wqk = nx.wqk; asg.bqk = nx.bqk;
@@ -882,8 +934,8 @@ void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s) {
 void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) { seg_attr((const void*)dec_layer_kernel); attr = true; }
-  JANUS_CHECK(b.B * 8 <= grid * (kNT / 64) && b.wqkv != nullptr && b.qkv != nullptr,
-              "decoder layer kernel: one (row, head) per wave and a next layer");
+  JANUS_CHECK(2 * ((b.B + 1) / 2) <= grid && b.wqkv != nullptr && b.qkv != nullptr,
+              "decoder layer kernel: a block per row pair and head group, and a next layer");
   dec_layer_kernel<<<grid, kNT, kSegLds, s>>>(b, nx);
   JANUS_LAUNCH_CHECK();
 }

@@ -649,7 +649,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                        !ln_fuse && !rln && ngroups == 0 && npairs == 0;
   // persistent = 2: segment B of layer l, the self-attention of l + 1 and its segment A as
   // ONE launch per layer step (dec_layer_kernel): 29 -> 19 launches per position
-  const bool layerk = persist && opt->persistent >= 2 && B * 8 <= seg_grid * 8;
+  const bool layerk = persist && opt->persistent >= 2 && 2 * ((B + 1) / 2) <= seg_grid;
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
     if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed

@@ -135,8 +135,10 @@ class JanusPipeline:
         # ~98 MB alive between calls at base.en, batch 64)
         self.keep_encoder_output = False
         self.last_encoder_output = None
-        # the staggered step's decoder: persistent segments (janus_decode_options.persistent)
-        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "1"))
+        # the staggered step's decoder: persistent segments (janus_decode_options.persistent;
+        # 2 = one launch per layer step, 19 launches per position: 246.5-248.5 vs
+        # 248.9-250.1 ms per step in three same-box rounds, profiles/r05_layer_kernel_ab.txt)
+        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "2"))
 
     # ------------------------------------------------------------------ encode
     def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
