@@ -704,8 +704,11 @@ def main():
     pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(dev)
     frames = int(np.ceil(args.seconds * 44100 / 512))
     from janus_amd.services.transcriber import TEMPERATURES
+    from janus_amd.pipeline import ServingTuning
+    # the measured serving geometry; JANUS_<FIELD> overrides one field for an A/B
+    tuning = ServingTuning.from_env()
     pipe = JanusPipeline(args.model, max_length=args.max_length,
-                         temperatures=TEMPERATURES if args.fallback else (0.0,))
+                         temperatures=TEMPERATURES if args.fallback else (0.0,), tuning=tuning)
     torch.cuda.synchronize()
 
     last = {}
@@ -732,12 +735,12 @@ def main():
 
     # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
     # pass), then the W warm-up steps, each a full encode + decode like the timed ones
-    # decoder slot sets (staggered: JANUS_STAGGER_SETS batches per decoder call) and the
+    # decoder slot sets (staggered: tuning.stagger_sets batches per decoder call) and the
     # pipeline depth (calls before the first batch comes out)
     # (the three-lane step is greedy-only: with --fallback --stagger 2 the staggered step runs)
     if args.fallback and args.stagger == 2:
         args.stagger = 1
-    sets = (max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2"))) if args.stagger == 1
+    sets = (max(2, tuning.stagger_sets) if args.stagger == 1
             else 2 if args.stagger == 2 else 1)
     depth = (sets if args.stagger == 1 else 3 if args.stagger == 2 else 1) if args.overlap > 0 else 0
     prime = depth

@@ -261,7 +261,31 @@ typedef struct {
                               grid: 19 launches per position (every row's keys in two
                               parts cut by its own length, merged in order: rows stay
                               independent of their neighbours) */
+  uint32_t path_flags;     /* alternative decoder paths (JANUS_DEC_PATH_* bits), for the
+                              parity tests that hold every path bit-identical and for A/B
+                              measurements; 0 = the measured default */
+  int lanes;               /* concurrent decoder lanes of janus_whisper_decode_greedy: the
+                              batch split over streams and host threads (0 = 1; slower at
+                              B = 64) */
 } janus_decode_options;
+
+/* janus_decode_options.path_flags */
+#define JANUS_DEC_PATH_NO_GRAPH     0x0001u /* launch every position, no captured graph */
+#define JANUS_DEC_PATH_NO_XABSORB   0x0002u /* per-layer cross K/V instead of the absorbed
+                                               cross-attention over the encoder output */
+#define JANUS_DEC_PATH_NO_XPAIR     0x0004u /* rows sharing an encoder row: no PAIR blocks */
+#define JANUS_DEC_PATH_XGROUP       0x0008u /* ... GROUP blocks of up to 6 rows */
+#define JANUS_DEC_PATH_FUSED_LN     0x0010u /* LayerNorm statistics on the projections */
+#define JANUS_DEC_PATH_LN_FUSE      0x0020u /* LayerNorm in the producing kernels */
+#define JANUS_DEC_PATH_RESID_LN     0x0040u /* whole-row residual projection + LayerNorm */
+#define JANUS_DEC_PATH_NO_CVP       0x0080u /* split merge and value projection apart */
+#define JANUS_DEC_PATH_CVP          0x0100u /* ... fused, above 64 rows too */
+#define JANUS_DEC_PATH_NO_SEL_EMBED 0x0200u /* token selection and embedding apart */
+#define JANUS_DEC_PATH_NO_EMBED_LN  0x0400u /* first LayerNorm not in the embedding kernel */
+#define JANUS_DEC_PATH_LN_PROLOGUE  0x0800u /* LayerNorm-into-prologue mask m (bits 12-15:
+                                               1 LN1, 2 LN2, 4 LN3, 8 final) instead of the
+                                               default 9 up to 64 rows, 0 above */
+#define JANUS_DEC_PATH_LN_MASK(m)   (JANUS_DEC_PATH_LN_PROLOGUE | (((uint32_t)(m) & 15u) << 12))
 
 /*
  * Batched greedy decoding (temperature 0) with the Whisper logit rules

@@ -357,13 +357,13 @@ void attention_launch(const _Float16* qkv, _Float16* out, int B, int T, int H, f
                       hipStream_t s) {
   if (B <= 0 || T <= 0) return;
   // JANUS_ATTN_V1: the first form (P through LDS, one query row per 4 lanes' registers)
-  static const bool v1 = std::getenv("JANUS_ATTN_V1") != nullptr;
+  static const bool v1 = ab_env("JANUS_ATTN_V1") != nullptr;
   if (v1) {
     dim3 grid((T + kQT - 1) / kQT, H, B);
     attention_kernel<<<grid, 256, 0, s>>>(qkv, out, T, H, scale * 1.4426950408889634f);
   } else {
     // JANUS_ATTN_NO_REMAP: dispatch order (blocks of one head spread over all XCDs)
-    static const int remap = std::getenv("JANUS_ATTN_NO_REMAP") ? 0 : 1;
+    static const int remap = ab_env("JANUS_ATTN_NO_REMAP") ? 0 : 1;
     const int nqb = (T + kSQB - 1) / kSQB;
     const int64_t nblk = (int64_t)nqb * H * B;
     JANUS_CHECK(nblk < (1ll << 31), "attention: grid too large");
@@ -748,11 +748,11 @@ void decode_attention_split_launch(const _Float16* q, int64_t q_bs, const _Float
                                    const int32_t* roff, int max_roff) {
   JANUS_CHECK(H <= kMaxHeads, "split decode attention: at most 8 heads (d <= 512)");
   if (B <= 0 || Tkv <= 0) return;
-  static const bool force_split = std::getenv("JANUS_DEC_SPLIT") != nullptr;
+  static const bool force_split = ab_env("JANUS_DEC_SPLIT") != nullptr;
   const int tmax = Tkv + (roff ? max_roff : 0);
   JANUS_CHECK(!roff || tmax <= kHeadKeys, "decode attention: staggered rows need <= 512 keys");
   if (tmax <= kHeadKeys && (!force_split || part_o == nullptr || roff)) {
-    static const bool all_rounds = std::getenv("JANUS_HEAD_ALL_ROUNDS") != nullptr;
+    static const bool all_rounds = ab_env("JANUS_HEAD_ALL_ROUNDS") != nullptr;
     const int nr = all_rounds ? kHeadRounds : (tmax + 8 * kHeadWaves - 1) / (8 * kHeadWaves);
     const float sl = scale * 1.4426950408889634f;
     const dim3 grid(H, B), blk(64 * kHeadWaves);

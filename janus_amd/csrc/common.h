@@ -9,12 +9,25 @@
 #include <hip/hip_fp16.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <stdexcept>
 
 namespace janus {
 
 void set_error(const std::string& msg);
+
+// Kernel-geometry A/B switches (JANUS_* environment variables) are read only by builds made
+// with -DJANUS_AB_KNOBS (the A/B libraries the tools build beside the product); the product
+// library takes no tuning from the environment and always runs the measured defaults.
+inline const char* ab_env(const char* name) {
+#ifdef JANUS_AB_KNOBS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // CUs a stream may dispatch to: the popcount of its CU mask (hipExtStreamGetCUMask; all
 // CUs for an unmasked stream). Cached per stream handle. Persistent / per-CU grids size

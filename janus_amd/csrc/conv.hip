@@ -367,7 +367,7 @@ void conv_launch(const ConvArgs& args, hipStream_t s) {
   // 1.84x for runs of row blocks per phase (1): the u phases of an upsampler read the same
   // input rows; in the overlapped step 3 costs ~0.9 ms of conv time against 1 (19.9 vs
   // 19.0 ms), at equal step time. JANUS_CONV_REMAP overrides
-  static const int remap_env = std::getenv("JANUS_CONV_REMAP") ? std::atoi(std::getenv("JANUS_CONV_REMAP")) : 3;
+  static const int remap_env = ab_env("JANUS_CONV_REMAP") ? std::atoi(ab_env("JANUS_CONV_REMAP")) : 3;
   ConvArgs a = args;
   if (a.remap < 0) a.remap = remap_env;
   JANUS_CHECK(a.Cin % 16 == 0, "conv: Cin must be a multiple of 16");

@@ -639,7 +639,7 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   const int nw = lg_waves(K);
   const size_t lds = (size_t)64 * (K + 16) * 2 + (size_t)nw * 64 * 17 * 4 + 64 * sizeof(RowRules);
   // weight tiles in flight per wave (JANUS_LG_DEPTH=2: two)
-  static const int depth = std::getenv("JANUS_LG_DEPTH") ? std::atoi(std::getenv("JANUS_LG_DEPTH")) : 1;
+  static const int depth = ab_env("JANUS_LG_DEPTH") ? std::atoi(ab_env("JANUS_LG_DEPTH")) : 1;
   auto kern = sample ? (K == 384 ? logits_partial_kernel<12, 1, true> : K == 512 ? logits_partial_kernel<16, 1, true>
                                                                           : logits_partial_kernel<24, 1, true>)
               : depth > 1 ? (K == 384 ? logits_partial_kernel<12, 2, false> : K == 512 ? logits_partial_kernel<16, 2, false>
@@ -660,7 +660,7 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   // rule-filter epilogue, several times a plain tile's VALU work; rotated so they land in
   // the first round of the waves with one tile fewer. Order-dependent only in the last
   // bits of the softmax sums (the argmax ties break by index either way).
-  static const bool no_rot = std::getenv("JANUS_LG_NO_ROT") != nullptr;
+  static const bool no_rot = ab_env("JANUS_LG_NO_ROT") != nullptr;
   int rot = 0;
   {
     const int stride = grid * nw, rem = ntiles % stride;

@@ -534,7 +534,7 @@ template <int AM, int EPI, int MTB>
 static void skinny_go(const SkinnyArgs& p, dim3 grid, hipStream_t s) {
   auto kern = gemm_skinny_kernel<EPI, AM, MTB>;
   if constexpr (AM == AM_F16 && MTB == 4) {
-    if (p.K <= kSkWaves * 32 && std::getenv("JANUS_SKINNY_NO_K1") == nullptr)
+    if (p.K <= kSkWaves * 32 && ab_env("JANUS_SKINNY_NO_K1") == nullptr)
       kern = gemm_skinny_kernel<EPI, AM, MTB, true>;
   }
   size_t lds = 0;
@@ -572,7 +572,7 @@ template <int AM>
 static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
   // plain fp16 outputs wider than 2048 columns (more 16-column tiles than a 128-CU
   // partition holds in one round) at K <= 512: 32 columns per block
-  static const bool nct2 = std::getenv("JANUS_SKINNY_NO_NCT2") == nullptr;
+  static const bool nct2 = ab_env("JANUS_SKINNY_NO_NCT2") == nullptr;
   if constexpr (AM == AM_F16 || AM == AM_LNX) {
     if (nct2 && epi == EPI_F16 && p.N > 2048 && p.K <= kSkWaves * 32 && p.a_group_cols == 0 && p.M <= 64) {
       if constexpr (AM == AM_LNX) {
@@ -594,7 +594,7 @@ static void launch_skinny_t(int epi, const SkinnyArgs& p, hipStream_t s) {
   // narrow outputs (N <= JANUS_SKINNY_MSPLIT_N, default 2048: <= 128 column tiles) split the
   // rows over 16-row blocks as well, so 4x as many CUs share the latency-bound product
   static const int msplit_n = [] {
-    const char* e = std::getenv("JANUS_SKINNY_MSPLIT_N");
+    const char* e = ab_env("JANUS_SKINNY_MSPLIT_N");
     return e ? std::atoi(e) : 2048;
   }();
   if (p.N <= (p.msplit_n > 0 ? p.msplit_n : msplit_n)) { launch_skinny_m<AM, 1>(epi, p, s); return; }

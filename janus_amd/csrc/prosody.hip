@@ -555,7 +555,7 @@ void prosody_launch(const float* pcm, const int64_t* sample_off, const int64_t* 
     // standalone, 302.0-302.2 vs 304.7-305.1 ms per step; with the scalar loop one-wave
     // blocks had been 1.6 ms per step faster); a capped grid beside the greedy decoder
     // keeps the 256-thread blocks (back-to-back step: 422 vs 449 ms per step with 128)
-    static const int nt_env = std::getenv("JANUS_YIN_THREADS") ? std::atoi(std::getenv("JANUS_YIN_THREADS")) : 0;
+    static const int nt_env = ab_env("JANUS_YIN_THREADS") ? std::atoi(ab_env("JANUS_YIN_THREADS")) : 0;
     const int nt = nt_env > 0 ? nt_env : (max_blocks > 0 ? 256 : 128);
     if (nt == 256)
       yin_hops_kernel<256><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(

@@ -353,7 +353,7 @@ static void narrow_cfg(const ResUnitArgs& a, hipStream_t s) {
   // HBM contention with the decoder) better than fewer, longer stripes. Sweep (vocoder
   // side per step): 128 -> +3 ms, 256 -> 315.6, 512 -> 313.5, 1024 -> 312.2, 2048 -> 313,
   // one block per tile -> 327.7 ms. JANUS_NARROW_GRID_CUS overrides the 1024.
-  static const int gcu = std::getenv("JANUS_NARROW_GRID_CUS") ? std::atoi(std::getenv("JANUS_NARROW_GRID_CUS")) : 1024;
+  static const int gcu = ab_env("JANUS_NARROW_GRID_CUS") ? std::atoi(ab_env("JANUS_NARROW_GRID_CUS")) : 1024;
   const int grid = std::min(n_tiles, std::max(1, gcu) * per_cu);
   kern<<<grid, G::NT, G::LDS, s>>>(a, tiles_per_utt, n_tiles);
   JANUS_LAUNCH_CHECK();
@@ -380,7 +380,7 @@ static void narrow_dw(const ResUnitArgs& a, hipStream_t s) {
 // (3 blocks per CU already) is level-to-slower at 8 (29.9 -> 30.4 ms).
 template <int C, int K>
 static void narrow_d(const ResUnitArgs& a, hipStream_t s) {
-  static const int nw = std::getenv("JANUS_NARROW_WAVES") ? std::atoi(std::getenv("JANUS_NARROW_WAVES"))
+  static const int nw = ab_env("JANUS_NARROW_WAVES") ? std::atoi(ab_env("JANUS_NARROW_WAVES"))
                                                           : (C == 32 ? 8 : 4);
   if constexpr (C == 16 && JANUS_NARROW16_BM != 240) narrow_dw<C, K, 4>(a, s);  // BM A/B builds
   else if (nw == 8) narrow_dw<C, K, 8>(a, s);

@@ -528,7 +528,7 @@ static void wide_cfg(const ResUnitArgs& a, hipStream_t s) {
   JANUS_CHECK((a.k * C / 32) % G::NPB == 0, "resunit (wide): k-step count vs ring depth");
   // Firefly-GAN's ResBlock1 geometry (k in {3, 7, 11} x d in {1, 3, 5}) at compile time with
   // the residual kept resident; JANUS_WIDE_RES=0 (A/B) or any other (k, d): run-time form
-  static const bool res = [] { const char* e = std::getenv("JANUS_WIDE_RES"); return e ? std::atoi(e) != 0 : true; }();
+  static const bool res = [] { const char* e = ab_env("JANUS_WIDE_RES"); return e ? std::atoi(e) != 0 : true; }();
   constexpr bool fits = G::NT % G::CPR == 0 && (G::BM * G::CPR) % G::NT == 0 &&
                         G::BM * G::CPR / G::NT == G::NE;
   if constexpr (fits) {
@@ -858,7 +858,7 @@ static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
   // for C = 64 (r05; JANUS_WIDE_LDS_RT=1: the run-time form, A/B): standalone 64 x 30 s
   // forward, C = 64 units 29.7-29.8 vs 30.7 ms; step 250.3-251.2 vs 251.5-251.9 ms
   // (profiles/r05_c64_kd_ab.txt); any other (k, d) and C run the run-time form
-  static const bool rt = std::getenv("JANUS_WIDE_LDS_RT") != nullptr;
+  static const bool rt = ab_env("JANUS_WIDE_LDS_RT") != nullptr;
   if constexpr (C == 64 && V == 0) {
     if (!rt) {
 #define JANUS_LDS_KD(K_, D_) \
@@ -873,7 +873,7 @@ static void lds_cfg(const ResUnitArgs& a, hipStream_t s) {
 }
 
 bool resunit_wide_supported(int C, int k, int d) {
-  static const bool off = std::getenv("JANUS_NO_WIDE_UNITS") != nullptr;
+  static const bool off = ab_env("JANUS_NO_WIDE_UNITS") != nullptr;
   return !off && (C == 64 || C == 128 || C == 256) && k >= 1 && k <= 11 && (k & 1) &&
          (k - 1) * d <= 50;
 }
@@ -885,11 +885,11 @@ void resunit_wide_pack(const float* w, _Float16* out, int C, int k, hipStream_t 
 }
 
 void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
-  static const int epf = [] { const char* e = std::getenv("JANUS_WIDE_EPF"); return e ? std::atoi(e) : 1; }();
-  static const int w64 = std::getenv("JANUS_WIDE64_WAVES") ? std::atoi(std::getenv("JANUS_WIDE64_WAVES")) : 4;
-  static const int w256 = std::getenv("JANUS_WIDE256_WAVES") ? std::atoi(std::getenv("JANUS_WIDE256_WAVES")) : 8;
+  static const int epf = [] { const char* e = ab_env("JANUS_WIDE_EPF"); return e ? std::atoi(e) : 1; }();
+  static const int w64 = ab_env("JANUS_WIDE64_WAVES") ? std::atoi(ab_env("JANUS_WIDE64_WAVES")) : 4;
+  static const int w256 = ab_env("JANUS_WIDE256_WAVES") ? std::atoi(ab_env("JANUS_WIDE256_WAVES")) : 8;
   if (a.C == 64) {
-    static const std::string c64 = std::getenv("JANUS_WIDE64_CFG") ? std::getenv("JANUS_WIDE64_CFG") : "lds";
+    static const std::string c64 = ab_env("JANUS_WIDE64_CFG") ? ab_env("JANUS_WIDE64_CFG") : "lds";
     if (c64 == "ring") wide_cfg<64, 5>(a, s);
     else if (w64 == 8) epf ? lds_cfg<64, true, 1>(a, s) : lds_cfg<64, false, 1>(a, s);
     else epf ? lds_cfg<64, true, 0>(a, s) : lds_cfg<64, false, 0>(a, s);
@@ -898,7 +898,7 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
     // JANUS_WIDE128_CFG: 2 (default) = 4 waves, weight ring 2 deep (166 VGPRs, three blocks
     // per CU); 0 = ring 4 deep (178 VGPRs, two blocks); 1 = 8 waves. Standalone 64 x 30 s,
     // C = 128 units: 45.4 / 49.0 / 59.6 ms (46.5 before the issue order was pinned)
-    static const int c128 = std::getenv("JANUS_WIDE128_CFG") ? std::atoi(std::getenv("JANUS_WIDE128_CFG")) : 2;
+    static const int c128 = ab_env("JANUS_WIDE128_CFG") ? std::atoi(ab_env("JANUS_WIDE128_CFG")) : 2;
     if (c128 == 1) wide_cfg<128, 1>(a, s);
     else if (c128 == 0) wide_cfg<128, 0>(a, s);
     else wide_cfg<128, 2>(a, s);
@@ -908,7 +908,7 @@ void resunit_wide_launch(const ResUnitArgs& a, hipStream_t s) {
     // deep, 8 waves x 32 columns; standalone 64 x 30 s, C = 256 units 27.0 -> 22.3 ms;
     // overlapped step, vocoder side 289 -> 282 ms), ring (2 deep: 22.8 ms), lds (weights
     // staged through LDS, the r01 form)
-    static const std::string c256 = std::getenv("JANUS_WIDE256_CFG") ? std::getenv("JANUS_WIDE256_CFG") : "ring4";
+    static const std::string c256 = ab_env("JANUS_WIDE256_CFG") ? ab_env("JANUS_WIDE256_CFG") : "ring4";
     if (c256 == "ring") wide_cfg<256, 3>(a, s);
     else if (c256 == "ring4") wide_cfg<256, 4>(a, s);
     else if (w256 == 16) epf ? lds_cfg<256, true, 1>(a, s) : lds_cfg<256, false, 1>(a, s);

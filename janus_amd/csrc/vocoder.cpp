@@ -284,7 +284,7 @@ extern "C" int janus_vocoder_create(const janus_vocoder_config* cfg, janus_vocod
                 "vocoder: bad config");
     auto* v = new janus_vocoder();
     v->cfg = *cfg;
-    v->fuse = std::getenv("JANUS_NO_FUSE") == nullptr;
+    v->fuse = ab_env("JANUS_NO_FUSE") == nullptr;
     *out = v;
   });
 }

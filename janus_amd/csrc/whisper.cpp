@@ -308,6 +308,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
+  // alternative paths (janus_decode_options.path_flags, 0 = the measured default)
+  const uint32_t pf = opt->path_flags;
+  auto path = [pf](uint32_t f) { return (pf & f) != 0; };
   // shared encoder rows (janus_decode_rows::enc_index): row b attends to enc_in row
   // enc_index[b] of n_enc; the absorbed cross-attention then reads each shared row once per
   // pair of decoder rows (xattn PAIR blocks), other paths get a per-row gathered copy
@@ -320,7 +323,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       JANUS_CHECK(rows->enc_index[b] >= 0 && rows->enc_index[b] < n_enc, "decode: enc_index out of range");
   }
   const bool pair_ok = shared && xattn_supported(d, H) && H <= 8 && d <= 512 && B <= kSkinnyMaxRows &&
-                       std::getenv("JANUS_NO_XABSORB") == nullptr && std::getenv("JANUS_NO_XPAIR") == nullptr;
+                       !path(JANUS_DEC_PATH_NO_XABSORB) && !path(JANUS_DEC_PATH_NO_XPAIR);
   // rows sharing an encoder row (best_of = 5 hypotheses of a window): PAIR blocks
   // (xattn_kernel<PAIR>, two blocks per CU, the window's output read once per two rows).
   // GROUP blocks of up to 6 rows (xattn_group_kernel: one read for all hypotheses) are
@@ -334,7 +337,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     for (int b = 0; b < B; ++b) grp[rows->enc_index[b]].push_back(b);
     size_t maxg = 0;
     for (auto& g : grp) maxg = std::max(maxg, g.size());
-    if (maxg > 2 && std::getenv("JANUS_XGROUP") != nullptr) {
+    if (maxg > 2 && path(JANUS_DEC_PATH_XGROUP)) {
       grp_rows = (int)std::min<size_t>(6, maxg);
       for (int e = 0; e < n_enc; ++e)
         for (size_t i = 0; i < grp[e].size(); i += grp_rows) {
@@ -512,10 +515,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     rules_init_launch(Z.d_rules.as<RowRules>() + f0, f1 - f0, s);
   }
 
-  // cross-attention: absorbed (stream enc itself, JANUS_NO_XABSORB restores per-layer K/V)
-  const bool xabs = xattn_supported(d, H) && B <= kSkinnyMaxRows && std::getenv("JANUS_NO_XABSORB") == nullptr;
-  const int xsplit = xattn_split_count(
-      Te, std::getenv("JANUS_XSPLIT") ? std::atoi(std::getenv("JANUS_XSPLIT")) : opt->xattn_splits);
+  // cross-attention: absorbed (stream enc itself, JANUS_DEC_PATH_NO_XABSORB restores per-layer K/V)
+  const bool xabs = xattn_supported(d, H) && B <= kSkinnyMaxRows && !path(JANUS_DEC_PATH_NO_XABSORB);
+  const int xsplit = xattn_split_count(Te, opt->xattn_splits);
   if (xabs) {
     Z.d_xqk.ensure(sizeof(_Float16) * B * H * d);
     Z.d_xc.ensure(sizeof(_Float16) * B * H * d);
@@ -550,11 +552,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // index of the first sampled token (earliest row); staggered continuing rows sample from
   // the first step on
   const int sample_begin = (stagger && f1 - f0 < B) ? 0 : min_plen;
-  // JANUS_FUSED_LN (B <= 64): LayerNorm rides on the projections (row-statistic pieces
+  // JANUS_DEC_PATH_FUSED_LN (B <= 64): LayerNorm rides on the projections (row-statistic pieces
   // written by the producer of each residual row, normalised on load by the consumer).
   // Opt-in: with the 16-wave skinny GEMM the separate LayerNorm launch measured faster
   // (637.7 vs 660.8 ms per bench step) — the consumer ingests A as fp32.
-  const bool fused_ln = B <= 64 && std::getenv("JANUS_FUSED_LN") != nullptr;
+  const bool fused_ln = B <= 64 && path(JANUS_DEC_PATH_FUSED_LN);
   Z.d_lnp.ensure(sizeof(float2) * B * (d / 16));
   float2* lnp = Z.d_lnp.as<float2>();
   auto lnargs = [&](const float* g, const float* bta, const _Float16* W, const float* bias,
@@ -565,16 +567,16 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     p.kc = kcp; p.vc = vcp; p.pos = pos; p.n_ctx = NC; p.qkv_d = d;
     return p;
   };
-  // JANUS_LN_FUSE (opt-in, B <= 64): LayerNorm handed off inside the producing kernel —
+  // JANUS_DEC_PATH_LN_FUSE (opt-in, B <= 64): LayerNorm handed off inside the producing kernel —
   // the residual GEMM's last block normalises the new rows (GemmArgs::ln_out, sc1 stores
   // + arrival counter), the embedding kernel normalises its row; no LayerNorm launches.
   // Measured slower than the separate launches (616.8 vs 536.5 ms per bench step): the
   // write-through stores and the serial tail cost more than the launch they save.
-  const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && std::getenv("JANUS_LN_FUSE") != nullptr;
+  const bool ln_fuse = B <= 64 && !fused_ln && d <= 512 && path(JANUS_DEC_PATH_LN_FUSE);
   // LayerNorm in the consuming projection's prologue (GemmArgs::lnin_x: each block
   // normalises its rows of x into an fp16 LDS tile; the vocabulary projection the final
   // LayerNorm) instead of a LayerNorm launch.
-  // Per LayerNorm (bit mask, JANUS_LN_PROLOGUE overrides): 1 = LN1 into the QKV
+  // Per LayerNorm (bit mask, JANUS_DEC_PATH_LN_MASK(m) overrides): 1 = LN1 into the QKV
   // projection, 2 = LN2 into the absorbed query projection, 4 = LN3 into fc1, 8 = the final
   // LayerNorm into the vocabulary projection. Measured per kernel, decoder alone on 16 CUs
   // per XCD: QKV 9.2 us vs 5.6 + 5.1 (LayerNorm launch), fc1 8.6 vs 5.2 + 5.1, logits 49.4
@@ -586,34 +588,34 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // mask 0 against 235-241 (9), 245-249 (13), 265-269 (15) on one box
   // (profiles/r04_decoder_knobs.json): each prologue normalises its block's rows again.
   const int ln_pro_mask = (B <= kSkinnyMaxRows && d <= 512 && !fused_ln && !ln_fuse)
-                              ? (std::getenv("JANUS_LN_PROLOGUE") ? std::atoi(std::getenv("JANUS_LN_PROLOGUE"))
+                              ? (path(JANUS_DEC_PATH_LN_PROLOGUE) ? (int)((pf >> 12) & 15u)
                                                                   : (B <= 64 ? 9 : 0))
                               : 0;
   // the embedding kernel owns whole rows (one block per utterance): it also writes the
   // first layer's LayerNorm of its row, one launch fewer per position
   // (JANUS_NO_EMBED_LN restores the separate launch)
-  const bool embed_ln = !fused_ln && !ln_fuse && d <= 512 && std::getenv("JANUS_NO_EMBED_LN") == nullptr;
+  const bool embed_ln = !fused_ln && !ln_fuse && d <= 512 && !path(JANUS_DEC_PATH_NO_EMBED_LN);
   auto with_ln = [&](GemmArgs g, const float* lg, const float* lb, bool on) {
     if (on) { g.lnin_x = x; g.lnin_ldx = d; g.lnin_g = lg; g.lnin_b = lb; g.lnin_eps = 1e-5f; }
     return g;
   };
   const bool lnp2 = ln_pro_mask & 2, lnp3 = ln_pro_mask & 4, lnp_fin = ln_pro_mask & 8;
-  // Opt-in (JANUS_RESID_LN): the attention output projections and the LayerNorm after
+  // Opt-in (JANUS_DEC_PATH_RESID_LN): the attention output projections and the LayerNorm after
   // them (LN2 / LN3) in one launch (resid_ln_kernel: 16 rows per block over all d columns,
   // bit-identical to the residual GEMM + LayerNorm pair). Measured 72 ms per step SLOWER
   // on the decoder side (361 vs 289 ms): at B = 64 only 4 blocks stream the 0.5 MB weight
   // each, at ~25 GB/s per CU (≈ 24 µs per launch against 5.6 + 5.0 µs for the pair).
   const bool rln = B <= 64 && !fused_ln && !ln_fuse && resid_ln_supported(d, d) &&
-                   std::getenv("JANUS_RESID_LN") != nullptr;
+                   path(JANUS_DEC_PATH_RESID_LN);
   const bool rln2 = rln && !lnp2, rln3 = rln && !lnp3;
   // the split merge fused into the per-head value projection (one launch) up to 64 rows;
   // above (the staggered 2 x 64 rows) the merge in the cross-attention's last split block
   // and a block-diagonal skinny projection measured faster (decoder side -1.5 / -2.9 ms
   // per step on two boxes, profiles/r04_decoder_knobs.json); bit-identical either way
-  // (xattn_combine_vproj_kernel; JANUS_NO_CVP / JANUS_CVP force either form)
-  const bool cvp = xattn_cvp_supported(d, H) && xsplit <= 16 && std::getenv("JANUS_NO_CVP") == nullptr &&
-                   (B <= 64 || ngroups > 0 || std::getenv("JANUS_CVP") != nullptr);
-  Z.d_lncnt.ensure(sizeof(int) * 64);  // one arrival counter per 16-row block (JANUS_LN_FUSE)
+  // (xattn_combine_vproj_kernel; JANUS_DEC_PATH_NO_CVP / _CVP force either form)
+  const bool cvp = xattn_cvp_supported(d, H) && xsplit <= 16 && !path(JANUS_DEC_PATH_NO_CVP) &&
+                   (B <= 64 || ngroups > 0 || path(JANUS_DEC_PATH_CVP));
+  Z.d_lncnt.ensure(sizeof(int) * 64);  // one arrival counter per 16-row block (JANUS_DEC_PATH_LN_FUSE)
   JANUS_HIP(hipMemsetAsync(Z.d_lncnt.p, 0, sizeof(int) * 64, s));
   const float* fin_g = w->params.get("decoder.layer_norm.weight", d);
   const float* fin_b = w->params.get("decoder.layer_norm.bias", d);
@@ -633,9 +635,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     resid_ln_launch(p, s);
   };
   // the selection at pos and the embedding at pos + 1 in one launch (select_embed_kernel,
-  // bit-identical; JANUS_NO_SEL_EMBED restores the two launches): a step from the first
+  // bit-identical; JANUS_DEC_PATH_NO_SEL_EMBED restores the two launches): a step from the first
   // sampled position on finds its row already embedded by the previous step's selection
-  const bool fuse_se = std::getenv("JANUS_NO_SEL_EMBED") == nullptr;
+  const bool fuse_se = !path(JANUS_DEC_PATH_NO_SEL_EMBED);
   JANUS_CHECK(!stagger || (!fused_ln && !ln_fuse && !rln && xabs),
               "decode: staggered rows run the default decoder kernels only");
   // persistent segments (dec_persist.hip, janus_decode_options.persistent): per layer the
@@ -750,7 +752,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         }
         // o_h = c_h Wv_h^T + bv_h (block-diagonal over heads), then x += o Wo^T + bo; the
         // split merge and the value projection in one launch (cvp) where supported
-        JANUS_CHECK(!xgroups || cvp, "decode: shared-encoder groups need the fused merge (JANUS_NO_CVP unset)");
+        JANUS_CHECK(!xgroups || cvp, "decode: shared-encoder groups need the fused merge (no JANUS_DEC_PATH_NO_CVP)");
         if (xgroups)
           xattn_group_launch(xqk, enc, Te, d, H, xsplit, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), s,
                              xgroups, ngroups, grp_rows);
@@ -810,7 +812,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                              maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
                              Z.d_nsp.as<float>(), roff);
   };
-  const bool use_graph = std::getenv("JANUS_NO_GRAPH") == nullptr;
+  const bool use_graph = !path(JANUS_DEC_PATH_NO_GRAPH);
   const int chunk = opt->check_every > 0 ? opt->check_every : 16;
   // every device pointer a captured kernel touches, plus the shape: the graph cache key
   const std::vector<int64_t> base_key = {
@@ -1052,12 +1054,11 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     hipStream_t s = (hipStream_t)stream;
     prepare(w, s);
     const _Float16* e = reinterpret_cast<const _Float16*>(enc);
-    // lanes: JANUS_DEC_LANES (default 1). Two half-batch lanes measured slower at B = 64
+    // lanes: janus_decode_options.lanes (default 1). Two half-batch lanes measured slower at B = 64
     // (428.7 vs 419.6 ms per bench step): the skinny projections are weight-stream
     // launches, so each lane re-streams every weight matrix, and the cross-attention
     // already saturates HBM.
-    int nlanes = 1;
-    if (const char* v = std::getenv("JANUS_DEC_LANES")) nlanes = std::atoi(v);
+    int nlanes = opt->lanes > 0 ? opt->lanes : 1;
     nlanes = std::max(1, std::min(nlanes, std::min(batch, 8)));
     // shared encoder rows / staggered rows: one lane holds them all (and its slots' state)
     if (rows && (rows->enc_index || rows->pos_offset)) nlanes = 1;

@@ -776,7 +776,7 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
   JANUS_CHECK(!pairs || (H <= 8 && npairs >= 1 && D <= 512), "xattn: row pairs need H <= 8, D <= 512");
   // 64-key chunks (8 waves) unless JANUS_XATTN_CH32
-  static const bool ch32 = std::getenv("JANUS_XATTN_CH32") != nullptr;
+  static const bool ch32 = ab_env("JANUS_XATTN_CH32") != nullptr;
   // one key split with the merge requested: the kernel writes c itself (DIRECT), no merge
   if (combine && nsplit == 1 && !pairs && !ch32 && D <= 512) {
     if (D == 384) xattn_cfg<384, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out);

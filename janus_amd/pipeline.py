@@ -12,9 +12,11 @@ build the "(emotion) text" prompt (synthesizer.py:149-177), then the GPU front e
 Firefly-GAN vocoder produce f32 audio and int16 PCM for all packets in one batch.
 Morse packets stay on the host (synthesizer.py:257-326).
 """
+import dataclasses
 import os
 import sys
 import time
+from typing import Optional
 
 import numpy as np
 import torch
@@ -28,6 +30,45 @@ from .vocoder import DEFAULT_REFERENCE_ID, FireflyConfig, VocoderEngine, emotion
 from .whisper import CONFIGS, WhisperEngine
 
 CAPTURE_RATE = 48000
+
+
+@dataclasses.dataclass
+class ServingTuning:
+    """Launch geometry of the serving steps; the defaults are the measured ones (DESIGN.md
+    §5f-§5g, profiles/r04_* and r05_* A/Bs). The pipeline reads no environment: bench.py and
+    the A/B tools build one with ``from_env`` (JANUS_<FIELD> in upper case) and pass it in."""
+    persistent: int = 2             # staggered decoder: janus_decode_options.persistent
+    stagger_sets: int = 2           # decoder slot sets per staggered call (>= 2)
+    voc_dec_utts: int = 4           # staggered: packets rendered on the decoder's CUs
+    yin_dec_utts: Optional[int] = None  # YIN utterances on the decoder side (None: the
+                                    # staggered step's controller; 0 in the other steps)
+    yin_beside: int = 128           # staggered: YIN grid cap beside the decoder (0 = after it)
+    yin_side: str = "voc"           # overlapped step: "voc" (after the vocoder) or "beside"
+    yin_blocks: int = 0             # overlapped step: YIN grid cap on the vocoder side (0 = none)
+    yin_beside_blocks: int = 128    # overlapped step, yin_side "beside": its grid cap
+    xattn_splits: Optional[int] = None  # cross-attention key splits (None: 1 staggered, 4 else)
+    fallback_full: bool = True      # overlapped step: fallback re-decodes on the whole GPU
+    fallback_xattn_splits: int = 4
+    host_prefetch: bool = True      # staggered: D2H of the finished part behind the decoder
+    side_timing: bool = False       # overlapped step: record per-side HIP events
+
+    @classmethod
+    def from_env(cls, env=None):
+        """A tuning with every field JANUS_<NAME> sets in ``env`` (os.environ) overridden
+        (tools and bench.py A/Bs only)."""
+        env = os.environ if env is None else env
+        kw = {}
+        for f in dataclasses.fields(cls):
+            v = env.get("JANUS_" + f.name.upper())
+            if v is None:
+                continue
+            if f.name == "yin_side":
+                kw[f.name] = v
+            elif f.name in ("fallback_full", "host_prefetch", "side_timing"):
+                kw[f.name] = v not in ("", "0")
+            else:
+                kw[f.name] = int(v)
+        return cls(**kw)
 
 
 class EncodeResult:
@@ -120,7 +161,7 @@ def stagger_plan(sets, pos, started, k, S, fresh):
 class JanusPipeline:
     def __init__(self, model: str = "base.en", whisper_seed: int = 0, vocoder_seed: int = 0,
                  max_length: int = 448, vocoder_cfg: FireflyConfig = FireflyConfig(),
-                 temperatures=TEMPERATURES):
+                 temperatures=TEMPERATURES, tuning: Optional[ServingTuning] = None):
         """temperatures: faster-whisper's fallback schedule (the default, as the
         reference's transcribe_buffer runs it); (0.0,) decodes each window once at T = 0
         and only reports the gates (bench.py's headline setting on synthetic weights,
@@ -135,10 +176,11 @@ class JanusPipeline:
         # ~98 MB alive between calls at base.en, batch 64)
         self.keep_encoder_output = False
         self.last_encoder_output = None
-        # the staggered step's decoder: persistent segments (janus_decode_options.persistent;
-        # 2 = one launch per layer step, 19 launches per position: 246.5-248.5 vs
-        # 248.9-250.1 ms per step in three same-box rounds, profiles/r05_layer_kernel_ab.txt)
-        self.persistent = int(os.environ.get("JANUS_DEC_PERSIST", "2"))
+        # serving-step geometry. The staggered step's decoder runs persistent segments
+        # (janus_decode_options.persistent; 2 = one launch per layer step, 19 launches per
+        # position: 246.5-248.5 vs 248.9-250.1 ms per step in three same-box rounds,
+        # profiles/r05_layer_kernel_ab.txt)
+        self.tuning = tuning if tuning is not None else ServingTuning()
 
     # ------------------------------------------------------------------ encode
     def encode(self, pcm: torch.Tensor, offsets: torch.Tensor, lengths, mode=JanusMode.SEMANTIC_VOICE,
@@ -179,6 +221,10 @@ class JanusPipeline:
                    for t, g in zip(texts, tags)]
         stats = _prosody_stats(parts if pres is not None else None, B, pcm.device)
         return EncodeResult(texts, tags, packets, dec.tokens, dec.n_tokens, stats, gts)
+
+    def _xsplits(self, default):
+        x = self.tuning.xattn_splits
+        return default if x is None else x
 
     def _hi_stream(self, device):
         if getattr(self, "_hi", None) is None:
@@ -279,14 +325,14 @@ class JanusPipeline:
         main = torch.cuda.current_stream(pcm.device)
         hi = self._hi_stream(pcm.device)
         ds, vs = self._split_streams(pcm.device, dec_per_xcd)
-        timing = os.environ.get("JANUS_OVERLAP_TIMING") is not None
+        timing = self.tuning.side_timing
         # side_events (a list, set by the caller): each step appends its (vocoder side,
         # decoder side) HIP event pairs, recorded on the side streams without a host sync
         record = timing or getattr(self, "side_events", None) is not None
-        yin_side = os.environ.get("JANUS_YIN_SIDE", "voc")
+        yin_side = self.tuning.yin_side
         # YIN follows the vocoder on its own CUs: an uncapped grid lets the hardware balance
         # the uneven per-hop cost (early exit, silent hops) over them
-        yin_blocks = int(os.environ.get("JANUS_YIN_BLOCKS", "0"))
+        yin_blocks = self.tuning.yin_blocks
 
         def yin(u0=0, u1=B):
             try:
@@ -294,7 +340,7 @@ class JanusPipeline:
                                       max_blocks=yin_blocks)
             except Exception:  # engine.py:520-525
                 return None
-        # the YIN of the first JANUS_YIN_DEC_UTTS utterances can run on the decoder side,
+        # the YIN of the first tuning.yin_dec_utts utterances can run on the decoder side,
         # after the decoder, to even out the two sides (64 utterances, r02 v38: 2 / 6 / 8 /
         # 10 -> 316.7-317.1 / 314.5-315.2 / 313.6-314.3 / 315.2-315.7 ms per step; v40 with
         # the faster decoder: 8 / 12 / 16 -> 302.9-303.4 / 301.5-301.8 / 303.0-304.0; v42
@@ -304,7 +350,7 @@ class JanusPipeline:
         # 298.4-298.9 / 297.4-298.9 ms on one box; 8; v49 with the faster encoder phase and
         # packed-pair YIN (1.14x): 8 / 4 / 0 -> 299.7-300.3 / 298.6-300.1 / 296.7-297.3 ms,
         # sides 284.7 / 282.0 ms at 0: all of YIN after the vocoder)
-        n_dec = (min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "0")))
+        n_dec = (min(B - 1, self.tuning.yin_dec_utts or 0)
                  if yin_side == "voc" else 0)
         ys = self._yin_s.stream if yin_side == "beside" else None
         pres = None
@@ -341,7 +387,7 @@ class JanusPipeline:
                 ev[1].record(vs)  # before the decoder call, which blocks the host
         if ys is not None:  # YIN concurrently with the decoder, on its CUs, capped grid
             ys.wait_stream(hi)
-            yin_cap = int(os.environ.get("JANUS_YIN_BESIDE_BLOCKS", "128"))
+            yin_cap = self.tuning.yin_beside_blocks
             with torch.cuda.stream(ys):
                 try:
                     pres = prosody_launch(pcm, offsets, lengths, CAPTURE_RATE, 512, max_blocks=yin_cap)
@@ -354,20 +400,20 @@ class JanusPipeline:
             # ms); cu_count: the vocabulary projection at one block per CU of the partition
             # (128 vs 256 blocks: decoder side 308.6 -> 304.6 ms) and row-split skinny
             # projections from N <= 1024 (vs 2048: 310.5 -> 306.3 ms)
-            dec_kw = dict(xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+            dec_kw = dict(xattn_splits=self._xsplits(4),
                           cu_count=self._dec_s.n_cus)
             dec = w.decode_ex(enc, max_length=self.max_length, **dec_kw)
             # the fallback's sampled re-decodes (host-driven: reads the T = 0 gates); the
             # settled texts go to _finish. They run on the WHOLE GPU (the high-priority
             # stream, after the vocoder side and the T = 0 decode): the vocoder side ends
             # with the T = 0 decode anyway, and the 320-row cross-attention streams scale
-            # with the CUs (JANUS_FB_FULL=0: on the decoder's CUs, as the T = 0 decode)
+            # with the CUs (tuning.fallback_full False: on the decoder's CUs, as the T = 0 decode)
             dec.settled = None
             if len(self.temperatures) > 1:
-                if os.environ.get("JANUS_FB_FULL", "1") != "0":
+                if self.tuning.fallback_full:
                     hi.wait_stream(ds)
                     hi.wait_stream(vs)
-                    fb_kw = dict(xattn_splits=int(os.environ.get("JANUS_FB_XSPLITS", "4")),
+                    fb_kw = dict(xattn_splits=self.tuning.fallback_xattn_splits,
                                  cu_count=torch.cuda.get_device_properties(pcm.device).multi_processor_count)
                     with torch.cuda.stream(hi):
                         dec.settled = _texts_and_gates(w, dec, self.temperatures, enc, **fb_kw)
@@ -458,7 +504,7 @@ class JanusPipeline:
                        mode=JanusMode.SEMANTIC_VOICE, override="auto", timestamp=None):
         """The overlapped serving step with the greedy decoder as a continuous batch of N
         batches at different positions (janus_decode_rows.pos_offset; N =
-        JANUS_STAGGER_SETS, default 2): each call of the decoder advances N·B rows by
+        tuning.stagger_sets, default 2): each call of the decoder advances N·B rows by
         S = max_length // N positions — batch i's rows fresh (positions 0 .. S-1) and
         batch i-m's, m = 1 .. N-1, continuing in their slot set (positions mS .. (m+1)S-1),
         so every step still completes exactly one batch's decode, but the decoder's
@@ -491,7 +537,7 @@ class JanusPipeline:
                                  "in flight; call flush_staggered() first (or pad the batch)")
             st = None
         if st is None:
-            n = max(2, int(os.environ.get("JANUS_STAGGER_SETS", "2")))
+            n = max(2, self.tuning.stagger_sets)
             d = w.cfg.d_model
             st = self._stag = {"B": B, "n": n, "k": 0, "sets": [None] * n, "done": None,
                                "enc": torch.zeros(n * B, w.cfg.n_audio_ctx, d, dtype=torch.float16,
@@ -501,7 +547,7 @@ class JanusPipeline:
         # chunk may overrun by a position (a no-op past the row's end) but not past L
         S = -(-(L - 1) // n)
         if n * S > L:
-            raise ValueError(f"JANUS_STAGGER_SETS={n} does not tile max_length {L}")
+            raise ValueError(f"stagger_sets={n} does not tile max_length {L}")
         f = k % n   # this call's fresh slot set (its last batch completed in the previous call)
         hi.wait_stream(main)
         with torch.cuda.stream(hi):
@@ -535,7 +581,7 @@ class JanusPipeline:
                 return None
         # the last kv packets of the batch render on the decoder's CUs after its call (a
         # second vocoder context), the rest here: a decoder side that finishes early takes
-        # vocoder work the way the vocoder side takes YIN (JANUS_VOC_DEC_UTTS; with the r05
+        # vocoder work the way the vocoder side takes YIN (tuning.voc_dec_utts; with the r05
         # decoder segments: 3 / 4 / 5 -> 252.2-252.7 / 251.2-251.3 / 251.9-252.3 ms per step,
         # profiles/r05_voc_dec_sweep2.txt)
         kv = 0
@@ -544,7 +590,7 @@ class JanusPipeline:
         with torch.cuda.stream(vs):
             if res_prev is not None:
                 pk = res_prev.packets
-                kv = min(len(pk), max(0, int(os.environ.get("JANUS_VOC_DEC_UTTS", "4"))))
+                kv = min(len(pk), max(0, self.tuning.voc_dec_utts))
                 self.voc_dec_utts = kv   # the main vocoder context renders the other len(pk) - kv
                 pk_dec = pk[len(pk) - kv:] if kv else []
                 wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
@@ -571,12 +617,12 @@ class JanusPipeline:
                 # profiles/r05_xattn_split1_ab.txt; r04: 4 splits 252.6-255.3, 2 246.7-248.6,
                 # 8 264.7-266.7 ms)
                 # the decoder side's YIN runs concurrently with the decode call, on a second
-                # stream over the decoder's CUs with its grid capped at JANUS_YIN_BESIDE
+                # stream over the decoder's CUs with its grid capped at tuning.yin_beside
                 # blocks (default 128; 0: after the call): the latency-bound decoder leaves
                 # issue slots free. Same box, two rounds of 5 steps: 259.4 / 258.4 ms at 128
                 # against 261.7 / 262.3 after the call and 263.0 / 262.3 at 256
                 # (profiles/r04_yin_beside_ab.json)
-                yb = int(os.environ.get("JANUS_YIN_BESIDE", "128"))
+                yb = self.tuning.yin_beside
                 beside = yb > 0 and n_dec > 0
                 if beside:
                     ys = self._yin_s.stream
@@ -588,10 +634,9 @@ class JanusPipeline:
                         except Exception:  # engine.py:520-525
                             pd = None
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
-                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "1")),
-                                  cu_count=self._dec_s.n_cus, persistent=self.persistent)
-                if cont is not None and len(self.temperatures) == 1 and \
-                        int(os.environ.get("JANUS_HOST_PREFETCH", "1")):
+                                  xattn_splits=self._xsplits(1),
+                                  cu_count=self._dec_s.n_cus, persistent=self.tuning.persistent)
+                if cont is not None and len(self.temperatures) == 1 and self.tuning.host_prefetch:
                     from .whisper import DecodeOut
                     sl = slice(jc * B, (jc + 1) * B)
                     hpart = DecodeOut(dec.tokens[sl], dec.n_tokens[sl], dec.sum_logprob[sl],
@@ -638,7 +683,7 @@ class JanusPipeline:
                 # after both sides (its encoder output stays in slot set jc until the next
                 # call's encoder, later on the same stream, overwrites it)
                 hi.wait_stream(main)
-                fb_kw = dict(xattn_splits=int(os.environ.get("JANUS_FB_XSPLITS", "4")),
+                fb_kw = dict(xattn_splits=self.tuning.fallback_xattn_splits,
                              cu_count=torch.cuda.get_device_properties(dev).multi_processor_count,
                              state_slot=1)
                 with torch.cuda.stream(hi):
@@ -654,15 +699,14 @@ class JanusPipeline:
 
     def _yin_split(self, st, B):
         """Utterances whose YIN runs on the decoder side in the staggered step. Fixed by
-        JANUS_YIN_DEC_UTTS; otherwise self-balancing: starts at 7B/8 (where it settled on
+        tuning.yin_dec_utts; otherwise self-balancing: starts at 7B/8 (where it settled on
         the r04 boxes: 52-59 of 64) and moves by the previous full step's side-time gap
         (vocoder side minus decoder side, HIP events on the two CU-masked streams) over
         twice the per-utterance YIN time, at most 16 per step,
         so the two partitions finish together whatever the box's vocoder / decoder speed
         ratio (measured from box to box: vocoder side 253-265 ms at the same split)."""
-        env = os.environ.get("JANUS_YIN_DEC_UTTS")
-        if env is not None:
-            return max(0, min(B - 1, int(env)))
+        if self.tuning.yin_dec_utts is not None:
+            return max(0, min(B - 1, self.tuning.yin_dec_utts))
         n = st.get("n_dec", 7 * B // 8)
         prev = st.get("prev_ev")
         if prev is not None and prev[1].query() and prev[3].query():
@@ -773,7 +817,7 @@ class JanusPipeline:
             if staged is not None:
                 st["enc"][f * B:(f + 1) * B].copy_(st["stage"])
             copied.record(ds)
-        n_dec = min(B - 1, int(os.environ.get("JANUS_YIN_DEC_UTTS", "0"))) if pcm is not None else 0
+        n_dec = min(B - 1, self.tuning.yin_dec_utts or 0) if pcm is not None else 0
 
         def yin(u0, u1):
             try:
@@ -817,7 +861,7 @@ class JanusPipeline:
                     offs[k] = min(offs[k], st["pos"][k // B])
             with torch.cuda.stream(ds):
                 dec = w.decode_ex(st["enc"], max_length=L, pos_offset=offs, steps=S,
-                                  xattn_splits=int(os.environ.get("JANUS_XATTN_SPLITS", "4")),
+                                  xattn_splits=self._xsplits(4),
                                   cu_count=self._dec_s.n_cus)
             stand = w.decode_stand(2 * B)
             st["pos"] = [stand[0], stand[B]]

@@ -58,7 +58,29 @@ class janus_decode_options(ctypes.Structure):
                 ("max_initial_timestamp_index", ctypes.c_int), ("check_every", ctypes.c_int),
                 ("xattn_splits", ctypes.c_int), ("cu_count", ctypes.c_int),
                 ("state_slot", ctypes.c_int), ("logits_blocks", ctypes.c_int),
-                ("msplit_rows_n", ctypes.c_int), ("persistent", ctypes.c_int)]
+                ("msplit_rows_n", ctypes.c_int), ("persistent", ctypes.c_int),
+                ("path_flags", ctypes.c_uint32), ("lanes", ctypes.c_int)]
+
+
+# janus_decode_options.path_flags (include/janus.h JANUS_DEC_PATH_*): alternative decoder
+# paths the parity tests hold bit-identical to the default; 0 = the measured default
+DEC_PATH_NO_GRAPH = 0x0001
+DEC_PATH_NO_XABSORB = 0x0002
+DEC_PATH_NO_XPAIR = 0x0004
+DEC_PATH_XGROUP = 0x0008
+DEC_PATH_FUSED_LN = 0x0010
+DEC_PATH_LN_FUSE = 0x0020
+DEC_PATH_RESID_LN = 0x0040
+DEC_PATH_NO_CVP = 0x0080
+DEC_PATH_CVP = 0x0100
+DEC_PATH_NO_SEL_EMBED = 0x0200
+DEC_PATH_NO_EMBED_LN = 0x0400
+DEC_PATH_LN_PROLOGUE = 0x0800
+
+
+def dec_path_ln_mask(m: int) -> int:
+    """JANUS_DEC_PATH_LN_MASK(m): LayerNorm-into-prologue mask m instead of the default."""
+    return DEC_PATH_LN_PROLOGUE | ((m & 15) << 12)
 
 
 class janus_decode_rows(ctypes.Structure):
@@ -280,7 +302,7 @@ class WhisperEngine:
     def decode_options(self, max_length: int = 448, check_every: int = 16,
                        timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0,
                        state_slot: int = 0, logits_blocks: int = 0, msplit_rows_n: int = 0,
-                       persistent: int = 0):
+                       persistent: int = 0, path_flags: int = 0, lanes: int = 0):
         t = self.tokenizer
         prompt = np.array(t.sot_sequence, np.int32)
         supp = np.array(t.suppress_tokens(), np.int32)
@@ -303,13 +325,16 @@ class WhisperEngine:
         opt.logits_blocks = logits_blocks
         opt.msplit_rows_n = msplit_rows_n
         opt.persistent = persistent
+        opt.path_flags = path_flags
+        opt.lanes = lanes
         return opt, (prompt, supp)
 
     def decode(self, enc: torch.Tensor, max_length: int = 448, check_every: int = 16,
-               timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0):
+               timestamps: bool = True, xattn_splits: int = 0, cu_count: int = 0,
+               path_flags: int = 0, lanes: int = 0):
         B = enc.shape[0]
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits,
-                                        cu_count)
+                                        cu_count, path_flags=path_flags, lanes=lanes)
         tokens = torch.empty(B, max_length, dtype=torch.int32, device=self.device)
         ntok = torch.empty(B, dtype=torch.int32, device=self.device)
         slp = torch.empty(B, dtype=torch.float32, device=self.device)
@@ -322,7 +347,7 @@ class WhisperEngine:
                   check_every: int = 16, timestamps: bool = True, xattn_splits: int = 0,
                   cu_count: int = 0, temperature: float = 0.0, seeds=None, enc_index=None,
                   pos_offset=None, steps: int = 0, state_slot: int = 0, logits_blocks: int = 0,
-                  msplit_rows_n: int = 0, persistent: int = 0):
+                  msplit_rows_n: int = 0, persistent: int = 0, path_flags: int = 0):
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
@@ -336,7 +361,8 @@ class WhisperEngine:
         the call runs in (a sampled re-decode between two staggered calls takes another
         slot); ``logits_blocks`` / ``msplit_rows_n``: launch geometry (0 = measured
         defaults, janus_decode_options); ``persistent``: the persistent decoder segments
-        (dec_persist.hip) where the shape allows."""
+        (dec_persist.hip) where the shape allows; ``path_flags``: an alternative decoder path
+        (DEC_PATH_*, parity tests)."""
         B = enc.shape[0] if enc_index is None else len(enc_index)
         if steps < 0:
             raise ValueError("steps must be >= 0")
@@ -347,7 +373,8 @@ class WhisperEngine:
                 raise ValueError("sampling needs one uint32 seed per row")
             sd = np.ascontiguousarray(np.asarray(seeds, np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
         opt, keep = self.decode_options(max_length, check_every, timestamps, xattn_splits, cu_count,
-                                        state_slot, logits_blocks, msplit_rows_n, persistent)
+                                        state_slot, logits_blocks, msplit_rows_n, persistent,
+                                        path_flags)
         rows = janus_decode_rows()
         rows.no_speech_token = tok.NO_SPEECH
         po = None

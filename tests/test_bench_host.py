@@ -65,3 +65,17 @@ def test_conv_avg_tool(tmp_path):
     r = json.loads(out)
     assert r["rocprof_launches"] == 4 and abs(r["rocprof_avg_launch_ms"] - 3.0) < 1e-9
     assert r["ratio_line_over_rocprof"] == 1.0
+
+
+def test_serving_tuning_from_env():
+    """ServingTuning.from_env: JANUS_<FIELD> overrides one field (bench.py / tools A/Bs);
+    the pipeline itself reads no environment."""
+    from janus_amd.pipeline import ServingTuning
+    t = ServingTuning.from_env({})
+    assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 4
+    t = ServingTuning.from_env({"JANUS_STAGGER_SETS": "3", "JANUS_YIN_DEC_UTTS": "5",
+                                "JANUS_HOST_PREFETCH": "0", "JANUS_YIN_SIDE": "beside",
+                                "JANUS_OTHER": "1"})
+    assert (t.stagger_sets, t.yin_dec_utts, t.host_prefetch, t.yin_side) == (3, 5, False, "beside")
+    src = open(os.path.join(os.path.dirname(__file__), "..", "janus_amd", "pipeline.py")).read()
+    assert "os.environ.get(" not in src

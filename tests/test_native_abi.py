@@ -69,3 +69,50 @@ def test_group_cu_masks_three_lanes():
                 assert sum(1 for i in bits if i % 8 == x) == k
     for dec in (4, 16, 28):
         assert _native.group_cu_masks(256, [dec, 32 - dec]) == list(_native.split_cu_masks(256, dec))
+
+
+def _c_offsets(struct, fields):
+    """offsetof() of each field of a header struct, from a C program gcc builds here."""
+    import shutil
+    import subprocess
+    import tempfile
+    import pytest
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    body = "".join(f'  printf("%zu\\n", offsetof({struct}, {f}));\n' for f in fields)
+    src = ("#include <stddef.h>\n#include <stdio.h>\n#include \"janus.h\"\n"
+           f"int main(void) {{\n{body}  printf(\"%zu\\n\", sizeof({struct}));\n  return 0;\n}}\n")
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "o.c"), os.path.join(d, "o")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", HEADER_DIR, c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    return [int(v) for v in out]
+
+
+def test_decode_structs_match_header():
+    """The ctypes mirrors of janus_decode_options / janus_decode_rows lay out exactly as the
+    C header (field offsets and size), so every option reaches the library."""
+    from janus_amd.whisper import janus_decode_options, janus_decode_rows
+    for cls in (janus_decode_options, janus_decode_rows):
+        names = [n for n, _ in cls._fields_]
+        want = _c_offsets(cls.__name__, names)
+        got = [getattr(cls, n).offset for n in names] + [ctypes.sizeof(cls)]
+        assert got == want, (cls.__name__, got, want)
+
+
+def test_decode_path_flags_match_header():
+    from janus_amd import whisper as w
+    src = open(os.path.join(HEADER_DIR, "janus.h")).read()
+    flags = dict(re.findall(r"#define JANUS_DEC_PATH_([A-Z_]+)\s+(0x[0-9a-fA-F]+)u", src))
+    assert len(flags) == 12
+    for name, v in flags.items():
+        assert getattr(w, "DEC_PATH_" + name) == int(v, 16), name
+    assert w.dec_path_ln_mask(9) == 0x0800 | (9 << 12)
+
+
+def test_product_library_reads_no_tuning_environment():
+    """Kernel-geometry A/B switches exist only in -DJANUS_AB_KNOBS builds (common.h ab_env):
+    the product library carries no JANUS_* environment name."""
+    data = open(_native.LIB_PATH, "rb").read()
+    assert not re.findall(rb"JANUS_[A-Z0-9_]+\x00", data)

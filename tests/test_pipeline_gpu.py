@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from janus_amd.pipeline import JanusPipeline
+from janus_amd.pipeline import JanusPipeline, ServingTuning
 from janus_amd.workload import synth_speech
 from oracle import packet as opk
 from oracle.prosody import OracleProsody
@@ -66,15 +66,14 @@ def test_transcriber_wav(gpu, tmp_path):
         assert tr.model.stats[k] - before[k] == gold["counters"][ko], k
 
 
-@pytest.mark.parametrize("yin_dec", ["0", "1"])
-def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
+@pytest.mark.parametrize("yin_dec", [0, 1])
+def test_overlapped_step_matches_sequential(gpu, yin_dec):
     """The serving pipeline (encode batch i on the whole GPU, then the greedy decoder of
     batch i and the vocoder of batch i-1 + YIN on disjoint CU-masked streams) produces the
     same packets and the same waveforms as the back-to-back step — with all of YIN on the
     vocoder side (the default) and with the first utterance's YIN on the decoder side
-    (JANUS_YIN_DEC_UTTS=1: the prosody result comes back in two parts)."""
-    monkeypatch.setenv("JANUS_YIN_DEC_UTTS", yin_dec)
-    pipe = JanusPipeline("tiny.en", max_length=12)
+    (yin_dec_utts=1: the prosody result comes back in two parts)."""
+    pipe = JanusPipeline("tiny.en", max_length=12, tuning=ServingTuning(yin_dec_utts=yin_dec))
     batches = []
     for i in range(2):
         utts = [synth_speech(300 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]
@@ -102,17 +101,16 @@ def test_overlapped_step_matches_sequential(gpu, monkeypatch, yin_dec):
         assert torch.equal(pcm16, seq[i][2])
 
 
-@pytest.mark.parametrize("sets,voc_dec", [("2", "0"), ("3", "0"), ("4", "0"), ("2", "1"), ("2", "3")])
-def test_staggered_step_matches_sequential(gpu, monkeypatch, sets, voc_dec):
+@pytest.mark.parametrize("sets,voc_dec", [(2, 0), (3, 0), (4, 0), (2, 1), (2, 3)])
+def test_staggered_step_matches_sequential(gpu, sets, voc_dec):
     """The continuous-batching serving step (step_staggered: the decoder advances batch i's
     rows from position 0 and batch i-m's from position mS, m < N, in one call, N·B rows;
-    N = JANUS_STAGGER_SETS) produces, per batch and N steps later, the same packets and
+    N = tuning.stagger_sets) produces, per batch and N steps later, the same packets and
     waveforms as the back-to-back step of that batch alone; flush_staggered drains. With
-    JANUS_VOC_DEC_UTTS = k the batch's last k packets render on the decoder's CUs through a
+    tuning.voc_dec_utts = k the batch's last k packets render on the decoder's CUs through a
     second vocoder context: the waveforms are still bit-identical, in packet order."""
-    monkeypatch.setenv("JANUS_STAGGER_SETS", sets)
-    monkeypatch.setenv("JANUS_VOC_DEC_UTTS", voc_dec)
-    pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,))
+    pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,),
+                         tuning=ServingTuning(stagger_sets=sets, voc_dec_utts=voc_dec))
     batches = []
     for i in range(3):
         utts = [synth_speech(700 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]

@@ -17,7 +17,9 @@ import numpy as np
 import pytest
 import torch
 
-from janus_amd.whisper import engine_weights, CONFIGS, WhisperEngine, mel_filters, synthetic_weights
+from janus_amd.whisper import (CONFIGS, DEC_PATH_NO_CVP, DEC_PATH_NO_SEL_EMBED, DEC_PATH_RESID_LN,
+                               DEC_PATH_XGROUP, WhisperEngine, dec_path_ln_mask, engine_weights,
+                               mel_filters, synthetic_weights)
 from janus_amd.workload import synth_speech
 from oracle import packet as opk
 from oracle import whisper as ow
@@ -191,18 +193,14 @@ def test_weight_reupload_after_decode(gpu):
 @pytest.mark.parametrize("T", [0.0, 0.6])
 @pytest.mark.parametrize("idx", [[0, 0, 0, 0, 0, 1, 1, 2, 2, 2, 2, 2, 1, 0], [0, 0, 1, 2, 2, 1, 0]],
                          ids=["five", "two"])
-@pytest.mark.parametrize("xgroup", ["", "1"], ids=["pairs", "groups"])
-def test_shared_encoder_rows_match_replicated(engine, gpu, monkeypatch, T, idx, xgroup):
+@pytest.mark.parametrize("xgroup", [0, DEC_PATH_XGROUP], ids=["pairs", "groups"])
+def test_shared_encoder_rows_match_replicated(engine, gpu, T, idx, xgroup):
     """Decoder rows sharing an encoder output (enc_index: faster-whisper's best_of
     hypotheses of one window) decode exactly as with a private copy per row: the
-    cross-attention reads it once per PAIR of rows (default), or with JANUS_XGROUP=1 and
+    cross-attention reads it once per PAIR of rows (default), or with DEC_PATH_XGROUP and
     more than two rows per window once per GROUP of up to 6 (xattn_group_kernel);
     including a batch above 64 rows (the skinny GEMMs split the rows over blocks). Tokens,
     summed log-probabilities and no-speech probabilities bit-identical."""
-    if xgroup:
-        monkeypatch.setenv("JANUS_XGROUP", xgroup)
-    else:
-        monkeypatch.delenv("JANUS_XGROUP", raising=False)
     eng, _ = engine
     utts = [synth_speech(70 + k, 2.0 + k) for k in range(3)]
     pcm, offs = pack(utts, gpu)
@@ -212,7 +210,8 @@ def test_shared_encoder_rows_match_replicated(engine, gpu, monkeypatch, T, idx, 
         seeds = [1000 + i for i in range(len(ei))] if T > 0 else None
         rep = enc.index_select(0, torch.tensor(ei, device=gpu)).contiguous()
         a = eng.decode_ex(rep, max_length=40, temperature=T, seeds=seeds)
-        b = eng.decode_ex(enc, max_length=40, temperature=T, seeds=seeds, enc_index=ei)
+        b = eng.decode_ex(enc, max_length=40, temperature=T, seeds=seeds, enc_index=ei,
+                          path_flags=xgroup)
         torch.cuda.synchronize()
         assert torch.equal(a.tokens.cpu(), b.tokens.cpu())
         assert torch.equal(a.n_tokens.cpu(), b.n_tokens.cpu())
@@ -325,19 +324,17 @@ def test_staggered_offset_past_stand_is_rejected(engine, gpu):
         eng.decode_ex(enc[:1].repeat(3, 1, 1), max_length=L, pos_offset=[0, 5, 5], steps=5)
 
 
-def test_decode_lanes_match_single_lane(engine, gpu, monkeypatch):
-    """Opt-in decoder lanes (JANUS_DEC_LANES: the batch split over concurrent streams and
+def test_decode_lanes_match_single_lane(engine, gpu):
+    """Opt-in decoder lanes (janus_decode_options.lanes: the batch split over concurrent streams and
     host threads) decode every utterance exactly as the single-lane decoder does: rows
     are independent through every decoder kernel."""
     eng, _ = engine
     utts = [synth_speech(60 + k, 3.0 + k) for k in range(5)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    monkeypatch.setenv("JANUS_DEC_LANES", "1")
-    t1, n1, _ = eng.decode(enc, 24)
+    t1, n1, _ = eng.decode(enc, 24, lanes=1)
     t1, n1 = t1.cpu(), n1.cpu()
-    monkeypatch.setenv("JANUS_DEC_LANES", "2")
-    t2, n2, _ = eng.decode(enc, 24)
+    t2, n2, _ = eng.decode(enc, 24, lanes=2)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
 
@@ -452,47 +449,44 @@ def test_sampling_leaves_greedy_unchanged(engine, gpu):
 
 
 @pytest.mark.parametrize("which", ["tiny", "base"])
-def test_fused_xattn_merge_vproj_bit_identical(engine, base_engine, gpu, monkeypatch, which):
+def test_fused_xattn_merge_vproj_bit_identical(engine, base_engine, gpu, which):
     """The cross-attention split merge fused with the per-head value projection
     (xattn_combine_vproj_kernel, default) decodes bit-identically to the two launches it
-    replaces (JANUS_NO_CVP): same tokens, same summed log-probabilities."""
+    replaces (DEC_PATH_NO_CVP): same tokens, same summed log-probabilities."""
     eng, _ = engine if which == "tiny" else base_engine
     utts = [synth_speech(80 + k, 4.0 + 2 * k) for k in range(6)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    monkeypatch.setenv("JANUS_NO_CVP", "1")
-    t1, n1, s1 = eng.decode(enc, 48)
+    t1, n1, s1 = eng.decode(enc, 48, path_flags=DEC_PATH_NO_CVP)
     t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
-    monkeypatch.delenv("JANUS_NO_CVP")
     t2, n2, s2 = eng.decode(enc, 48)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu())
     assert torch.equal(s1, s2.cpu())
 
 
-def test_fused_select_embed_bit_identical(base_engine, gpu, monkeypatch):
+def test_fused_select_embed_bit_identical(base_engine, gpu):
     """The token selection at position p fused with the embedding of the chosen token at
     p + 1 (select_embed_kernel, default) decodes bit-identically to the two launches
-    (JANUS_NO_SEL_EMBED), including rows that finish early and the last position."""
+    (DEC_PATH_NO_SEL_EMBED), including rows that finish early and the last position."""
     eng, _ = base_engine
     utts = [synth_speech(90 + k, 3.0 + 3 * k) for k in range(5)]
     pcm, offs = pack(utts, gpu)
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
-    monkeypatch.setenv("JANUS_NO_SEL_EMBED", "1")
-    t1, n1, s1 = eng.decode(enc, 37, check_every=8)
+    t1, n1, s1 = eng.decode(enc, 37, check_every=8, path_flags=DEC_PATH_NO_SEL_EMBED)
     t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
-    monkeypatch.delenv("JANUS_NO_SEL_EMBED")
     t2, n2, s2 = eng.decode(enc, 37, check_every=8)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
 
 
-@pytest.mark.parametrize("env", [("JANUS_RESID_LN", "1"), ("JANUS_LN_PROLOGUE", "15"), ("JANUS_LN_PROLOGUE", "0")])
-def test_layernorm_placements_bit_identical(base_engine, gpu, monkeypatch, env):
+@pytest.mark.parametrize("flags", [DEC_PATH_RESID_LN, dec_path_ln_mask(15), dec_path_ln_mask(0)],
+                         ids=["resid_ln", "mask15", "mask0"])
+def test_layernorm_placements_bit_identical(base_engine, gpu, flags):
     """Every LayerNorm placement rounds alike (mfma.h ln_sum4 / ln_sq4 / ln_norm4): the
     separate launch (mask 0), the GEMM prologues (mask 15: LN1 -> QKV, LN2 -> absorbed query
     projection, LN3 -> fc1, final -> vocabulary projection), the whole-row residual
-    projection + LayerNorm kernel (JANUS_RESID_LN) and the default (mask 9) decode the same
+    projection + LayerNorm kernel (DEC_PATH_RESID_LN) and the default (mask 9) decode the same
     tokens with the same summed log-probabilities."""
     eng, _ = base_engine
     utts = [synth_speech(120 + k, 3.0 + 2 * k) for k in range(4)]
@@ -500,8 +494,7 @@ def test_layernorm_placements_bit_identical(base_engine, gpu, monkeypatch, env):
     enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
     t1, n1, s1 = eng.decode(enc, 40)
     t1, n1, s1 = t1.cpu(), n1.cpu(), s1.cpu()
-    monkeypatch.setenv(*env)
-    t2, n2, s2 = eng.decode(enc, 40)
+    t2, n2, s2 = eng.decode(enc, 40, path_flags=flags)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
 

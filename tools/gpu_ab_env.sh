@@ -1,7 +1,8 @@
 #!/bin/bash
 # bench A/B over env settings / builds, timed steps only (--no-idle-latency):
 #   tools/gpu_ab_env.sh tag default env:A=1,B=2 lib:libx.so ...
-# (env: comma-separated NAME=VALUE pairs; lib: an alternative in-tree build, JANUS_LIB)
+# (env: comma-separated NAME=VALUE pairs: ServingTuning fields, or kernel switches with a
+# -DJANUS_AB_KNOBS lib; lib: an alternative in-tree build, JANUS_LIB)
 # AB_REPS rounds (default 2), AB_STEPS timed steps (default 5). One line per run:
 # variant, ms/step, mean vocoder / decoder side, conv avg launch ms.
 set -o pipefail

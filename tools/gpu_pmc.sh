@@ -1,17 +1,32 @@
 #!/bin/bash
-# PMC passes (one counter group per pass, kernel-trace only) over kbench shapes.
-# usage (via gpurun): bash tools/gpu_pmc.sh <tag> <kbench args...>
+# PMC summaries (run via gpurun): the greedy decoder at the headline shape (128 rows,
+# 16 CUs per XCD, alone, 64 positions) with the persistent segments on and off, and the
+# vocoder families (standalone 64 x 30 s forward), counters normalised by tools/pmc_reduce.py
 set -o pipefail
-tag=$1; shift
 root=$(pwd)
-mkdir -p $root/gpurun_out/$tag
+out=$root/gpurun_out/${1:-pmc}
+mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 60 rocprofv3 -L > $root/gpurun_out/$tag/counters.txt 2>&1 || true
-i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" \
-  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
-  "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_MISC"; do
-  i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d $root/gpurun_out/$tag/p$i -o run --output-format csv -- python3 $root/${SCRIPT:-tools/kbench.py} "$@" > $root/gpurun_out/$tag/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $root/gpurun_out/$tag/p$i.log; exit 1; }
+DEC="python3 $root/tools/decoder_probe.py --per-xcd 16 --beside 0 --reps 1 --max-length 64 --rows 128 --xsplits 1"
+for P in 1 0; do
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE -d $out/dec$P/p1 -o run --output-format csv -- $DEC --persistent $P > $out/dec$P.p1.log 2>&1 || { tail -5 $out/dec$P.p1.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/dec$P/p2 -o run --output-format csv -- $DEC --persistent $P > $out/dec$P.p2.log 2>&1 || { tail -5 $out/dec$P.p2.log; exit 1; }
+  python3 $root/tools/pmc_reduce.py $out/dec$P/p1 $out/dec$P/p2 --by-kernel --cus 128 > $out/decoder_persistent$P.json
 done
-echo done
+timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $out/voc/p1 -o run --output-format csv -- python3 $root/tools/vocoder_traffic.py > $out/voc.p1.log 2>&1 || { tail -5 $out/voc.p1.log; exit 1; }
+timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES -d $out/voc/p2 -o run --output-format csv -- python3 $root/tools/vocoder_traffic.py > $out/voc.p2.log 2>&1 || { tail -5 $out/voc.p2.log; exit 1; }
+python3 $root/tools/pmc_reduce.py $out/voc/p1 $out/voc/p2 --cus 256 > $out/vocoder_families.json
+grep -h '"decoder_ms"' $out/dec1.p1.log $out/dec0.p1.log || true
+python3 - <<PY
+import json
+for P in (1, 0):
+    d = json.load(open("$out/decoder_persistent%d.json" % P))
+    print("persistent", P)
+    for k, v in sorted(d.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:10]:
+        print("  %-60s n=%5d wait=%.2f issue=%.2f active=%.2f fetchKB=%s" % (k[:60], v["dispatches"],
+              v.get("sq_wait_any_frac", 0), v.get("sq_wait_inst_any_frac", 0), v.get("sq_active_inst_any_frac", 0),
+              v.get("fetch_kb_per_dispatch")))
+v = json.load(open("$out/vocoder_families.json"))
+for k, g in v.items():
+    print(k, {x: g.get(x) for x in ("mfma_busy_frac", "cycles_per_mfma", "sq_wait_any_frac", "sq_wait_inst_lds_frac", "lds_conflict_frac", "fetch_kb_per_dispatch")})
+PY

@@ -1,11 +1,15 @@
 #!/bin/bash
-# Kernel-trace profile of a short bench run (run via gpurun). $1 = tag
+# kernel-trace profile of the timed staggered steps only (--no-idle-latency) -> gpurun_out/<tag>/
 set -o pipefail
 tag=${1:-prof}
-mkdir -p gpurun_out
 root=$(pwd)
+out=$root/gpurun_out/$tag
+mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $root/gpurun_out/$tag -o run -- python3 $root/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $root/gpurun_out/$tag.log 2>&1 || { tail -20 $root/gpurun_out/$tag.log; exit 1; }
-grep '"metric"' $root/gpurun_out/$tag.log | cut -c1-400
-f=$(find $root/gpurun_out/$tag -name "*.db" | head -1)
-python3 $root/tools/rocprof_stats.py "$f" 40 --csv $root/gpurun_out/$tag/kernel_stats.csv
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 $root/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-idle-latency > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
+f=$(find $out/prof -name "*.db" | head -1)
+python3 $root/tools/rocprof_stats.py "$f" 60 --csv $out/kernel_stats.csv > $out/kernel_top.txt
+grep '"metric"' $out/prof.log > $out/bench_under_rocprof.json
+cd $root
+python3 tools/conv_avg.py "$f" $out/bench_under_rocprof.json > $out/conv_avg.txt || true
+head -40 $out/kernel_top.txt | cut -c1-150
