@@ -58,6 +58,11 @@ int janus_gemm_ln_f16(int epi, const float* x, int64_t ldx, const float* gamma, 
 int janus_layernorm_f16(const float* x, const float* gamma, const float* beta, uint16_t* out,
                         int rows, int d, float eps, void* stream);
 
+/* The cross-lane moves every wave reduction of the library uses (DPP / v_permlane swaps in
+ * place of ds_bpermute): in [device] f32 [n_waves][64] -> out [device] f32 [n_waves][6][64],
+ * out[w][k][l] = in[w][l ^ (1 << k)] when they are right. Test entry. */
+int janus_wave_xor_f32(const float* in, float* out, int n_waves, void* stream);
+
 /* x[M][N] += A[M][K] W[N][K]^T + bias (fp32 residual, in place), then out[M][N] =
  * LayerNorm(x) fp16 (gamma/beta f32 [N], eps) in ONE launch: 16 rows per workgroup over
  * all N columns. N = K in {384, 512} (tiny.en / base.en d_model). Bit-identical to

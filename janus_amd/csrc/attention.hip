@@ -685,16 +685,16 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
     float dot = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dot = fmaf((float)h8[j], qv[j], dot);
-    dot += __shfl_xor(dot, 1);
-    dot += __shfl_xor(dot, 2);
-    dot += __shfl_xor(dot, 4);
+    dot += xshfl<1>(dot);
+    dot += xshfl<2>(dot);
+    dot += xshfl<4>(dot);
     const bool ok = 8 * (i * kHeadWaves + w) + kg < Tkv;
     sc[i] = ok ? dot : -INFINITY;
     m = fmaxf(m, sc[i]);
   }
-  m = fmaxf(m, __shfl_xor(m, 8));
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  m = fmaxf(m, xshfl<8>(m));
+  m = fmaxf(m, xshfl<16>(m));
+  m = fmaxf(m, xshfl<32>(m));
   float l = 0.f, a[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) a[j] = 0.f;
@@ -709,12 +709,14 @@ __global__ __launch_bounds__(512) void decode_head_kernel(
     }
   }
   // sum over the 8 key groups (lanes sharing dg); l is replicated over dg
+  auto merge = [&](auto sh) __attribute__((always_inline)) {
+    l += sh(l);
 #pragma unroll
-  for (int o = 8; o < 64; o <<= 1) {
-    l += __shfl_xor(l, o);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] += __shfl_xor(a[j], o);
-  }
+    for (int j = 0; j < 8; ++j) a[j] += sh(a[j]);
+  };
+  merge([](float x) { return xshfl<8>(x); });
+  merge([](float x) { return xshfl<16>(x); });
+  merge([](float x) { return xshfl<32>(x); });
   if (kg == 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) wo[w][dg * 8 + j] = a[j];

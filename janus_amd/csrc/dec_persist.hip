@@ -369,12 +369,12 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 2; ++k) s += ln_sum4(v[j][k]);
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    s = wave_sum_f32(s);
     const float mean = s / kD;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < 2; ++k) q += ln_sq4(v[j][k], mean);
-    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+    q = wave_sum_f32(q);
     const float rstd = rsqrtf(q / kD + 1e-5f);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -735,15 +735,15 @@ __device__ __forceinline__ void attn_keys(const DecSegArgs& g, int b, int h, int
       float dot = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot = fmaf((float)k8[j], qv[j], dot);
-      dot += __shfl_xor(dot, 1);
-      dot += __shfl_xor(dot, 2);
-      dot += __shfl_xor(dot, 4);
+      dot += xshfl<1>(dot);
+      dot += xshfl<2>(dot);
+      dot += xshfl<4>(dot);
       sc[r] = c0 + 8 * r + kg < k1 ? dot : -INFINITY;
       cm = fmaxf(cm, sc[r]);
     }
-    cm = fmaxf(cm, __shfl_xor(cm, 8));
-    cm = fmaxf(cm, __shfl_xor(cm, 16));
-    cm = fmaxf(cm, __shfl_xor(cm, 32));
+    cm = fmaxf(cm, xshfl<8>(cm));
+    cm = fmaxf(cm, xshfl<16>(cm));
+    cm = fmaxf(cm, xshfl<32>(cm));
     const float m_new = fmaxf(t.m, cm);  // finite: every chunk holds key c0 < k1
     const float alpha = exp2f(t.m - m_new);
     t.l *= alpha;
@@ -760,12 +760,14 @@ __device__ __forceinline__ void attn_keys(const DecSegArgs& g, int b, int h, int
     t.m = m_new;
   }
   // the 8 key groups (lanes sharing dg) share m: plain sums
+  auto merge = [&](auto sh) __attribute__((always_inline)) {
+    t.l += sh(t.l);
 #pragma unroll
-  for (int o = 8; o < 64; o <<= 1) {
-    t.l += __shfl_xor(t.l, o);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t.acc[j] += __shfl_xor(t.acc[j], o);
-  }
+    for (int j = 0; j < 8; ++j) t.acc[j] += sh(t.acc[j]);
+  };
+  merge([](float x) { return xshfl<8>(x); });
+  merge([](float x) { return xshfl<16>(x); });
+  merge([](float x) { return xshfl<32>(x); });
 }
 
 __device__ __forceinline__ void attn_store(const DecSegArgs& g, int b, int h, const AttnState& t, int lane) {

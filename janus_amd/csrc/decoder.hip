@@ -47,14 +47,14 @@ void cast_f32_f16_launch(const float* in, _Float16* out, int64_t n, hipStream_t 
 // lane over 8 aligned lanes; every lane of the group returns it.
 __device__ __forceinline__ float2 ln_piece8x2(float v0, float v1) {
   float s = v0 + v1;
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  s += __shfl_xor(s, 4);
+  s += xshfl<1>(s);
+  s += xshfl<2>(s);
+  s += xshfl<4>(s);
   const float m = s * (1.0f / 16.0f);
   float q = (v0 - m) * (v0 - m) + (v1 - m) * (v1 - m);
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
-  q += __shfl_xor(q, 4);
+  q += xshfl<1>(q);
+  q += xshfl<2>(q);
+  q += xshfl<4>(q);
   return make_float2(s, q);
 }
 
@@ -91,12 +91,12 @@ __device__ __forceinline__ void embed_row(const _Float16* __restrict__ tok_emb,
     const int col = 2 * threadIdx.x, wv = threadIdx.x >> 6;
     const bool ok = col < d;
     float s = v0 + v1;
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum_f32(s);
     if ((threadIdx.x & 63) == 0) red[0][wv] = s;
     __syncthreads();
     const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / d;
     float q = ok ? (v0 - mean) * (v0 - mean) + (v1 - mean) * (v1 - mean) : 0.f;
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum_f32(q);
     if ((threadIdx.x & 63) == 0) red[1][wv] = q;
     __syncthreads();
     const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / d + 1e-5f);
@@ -212,7 +212,8 @@ __device__ __forceinline__ bool allowed_unmasked(int t, const DecodeRules& R, co
 
 template <class Op>
 __device__ __forceinline__ float block_reduce(float v, float* red, Op op) {
-  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
+  v = op(v, xshfl<32>(v)); v = op(v, xshfl<16>(v)); v = op(v, xshfl<8>(v));
+  v = op(v, xshfl<4>(v)); v = op(v, xshfl<2>(v)); v = op(v, xshfl<1>(v));
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -722,23 +723,30 @@ __device__ __forceinline__ int select_row(
     if (better(p.b_all_v, p.b_all_i, ba_v, ba_i)) { ba_v = p.b_all_v; ba_i = p.b_all_i; ba_r = p.b_all_r; }
     if (better(p.b_ts_v, p.b_ts_i, bt_v, bt_i)) { bt_v = p.b_ts_v; bt_i = p.b_ts_i; bt_r = p.b_ts_r; }
   }
-  for (int o = 32; o > 0; o >>= 1) {
+  // butterfly over the wave (xshfl: the partner lane's values as __shfl_xor, no LDS trip)
+  auto level = [&](auto shf, auto shi) __attribute__((always_inline)) {
     float mo;
-    const float om = __shfl_xor(m_all, o), os = __shfl_xor(s_all, o);
+    const float om = shf(m_all), os = shf(s_all);
     s_all = lse_merge(m_all, s_all, om, os, &mo); m_all = mo;
-    const float tm = __shfl_xor(m_ts, o), ts = __shfl_xor(s_ts, o);
+    const float tm = shf(m_ts), ts = shf(s_ts);
     s_ts = lse_merge(m_ts, s_ts, tm, ts, &mo); m_ts = mo;
-    const float rm = __shfl_xor(m_raw, o), rs = __shfl_xor(s_raw, o);
+    const float rm = shf(m_raw), rs = shf(s_raw);
     s_raw = lse_merge(m_raw, s_raw, rm, rs, &mo); m_raw = mo;
-    m_text = fmaxf(m_text, __shfl_xor(m_text, o));
-    t_v = fmaxf(t_v, __shfl_xor(t_v, o));
-    const float av = __shfl_xor(ba_v, o); const int ai = __shfl_xor(ba_i, o);
-    const float ar = __shfl_xor(ba_r, o);
+    m_text = fmaxf(m_text, shf(m_text));
+    t_v = fmaxf(t_v, shf(t_v));
+    const float av = shf(ba_v); const int ai = shi(ba_i);
+    const float ar = shf(ba_r);
     if (better(av, ai, ba_v, ba_i)) { ba_v = av; ba_i = ai; ba_r = ar; }
-    const float tv = __shfl_xor(bt_v, o); const int ti = __shfl_xor(bt_i, o);
-    const float tr = __shfl_xor(bt_r, o);
+    const float tv = shf(bt_v); const int ti = shi(bt_i);
+    const float tr = shf(bt_r);
     if (better(tv, ti, bt_v, bt_i)) { bt_v = tv; bt_i = ti; bt_r = tr; }
-  }
+  };
+  level([](float x) { return xshfl<32>(x); }, [](int x) { return xshfl_i<32>(x); });
+  level([](float x) { return xshfl<16>(x); }, [](int x) { return xshfl_i<16>(x); });
+  level([](float x) { return xshfl<8>(x); }, [](int x) { return xshfl_i<8>(x); });
+  level([](float x) { return xshfl<4>(x); }, [](int x) { return xshfl_i<4>(x); });
+  level([](float x) { return xshfl<2>(x); }, [](int x) { return xshfl_i<2>(x); });
+  level([](float x) { return xshfl<1>(x); }, [](int x) { return xshfl_i<1>(x); });
   if (lane == 0) {
     LogitPart p;
     p.m_all = m_all; p.s_all = s_all; p.m_text = m_text; p.m_ts = m_ts; p.s_ts = s_ts;

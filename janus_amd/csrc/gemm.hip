@@ -803,7 +803,7 @@ __global__ __launch_bounds__(NW * 64) void resid_ln_kernel(ResidLnArgs p) {
       xv[k] = i < NV ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       s += ln_sum4(xv[k]);
     }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum_f32(s);
     const float mean = s / (float)N;
     float q = 0.f;
 #pragma unroll
@@ -811,7 +811,7 @@ __global__ __launch_bounds__(NW * 64) void resid_ln_kernel(ResidLnArgs p) {
       const int i = lane + k * 64;
       if (i < NV) q += ln_sq4(xv[k], mean);
     }
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum_f32(q);
     const float rstd = rsqrtf(q / (float)N + p.eps);
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {

@@ -111,6 +111,13 @@ extern "C" int janus_layernorm_f16(const float* x, const float* gamma, const flo
   });
 }
 
+extern "C" int janus_wave_xor_f32(const float* in, float* out, int n_waves, void* stream) {
+  return guarded([&] {
+    JANUS_CHECK(in && out, "null argument");
+    wave_xor_launch(in, out, n_waves, (hipStream_t)stream);
+  });
+}
+
 extern "C" int janus_attention_f16(const uint16_t* qkv, uint16_t* out, int batch, int T, int H,
                                    float scale, void* stream) {
   return guarded([&] {

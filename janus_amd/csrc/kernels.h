@@ -88,6 +88,8 @@ void gemm_skinny_ln_launch(int epi, const SkinnyLnArgs& p, hipStream_t s);
 
 // ------------------------------------------------------------- LayerNorm
 // out[r][:] = fp16( (x[r]-mean)/sqrt(var+eps) * g + b ), x fp32 [rows][d]
+// out[w][k][lane] = mfma.h xshfl<2^k>(in[w][lane]) (kernel test entry)
+void wave_xor_launch(const float* in, float* out, int n_waves, hipStream_t s);
 void layernorm_launch(const float* x, const float* g, const float* b, _Float16* out, int rows,
                       int d, float eps, hipStream_t s);
 // fp32 out variant (final encoder LN keeps fp32 for the cross-attention K/V GEMMs' input)

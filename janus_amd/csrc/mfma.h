@@ -37,6 +37,52 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 
+// __shfl_xor(v, O) over a full wave without the LDS crossbar: the partner lane's value,
+// bit for bit, so every butterfly reduction keeps its association. O = 1, 2: quad_perm;
+// 8: row_ror:8; 4: row_shl:4 / row_shr:4 and a select; 16, 32: v_permlane16_swap /
+// v_permlane32_swap (gfx950) and a select. Each is a few VALU cycles where a ds_bpermute
+// is an LDS round trip, and reductions chain six of them (a softmax's max and sum, a
+// LayerNorm's two moments). All 64 lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int O>
+__device__ __forceinline__ float xshfl(float v) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor offset");
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if constexpr (O == 1) return dpp_f32<0xB1>(v);        // quad_perm [1, 0, 3, 2]
+  else if constexpr (O == 2) return dpp_f32<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  else if constexpr (O == 8) return dpp_f32<0x128>(v);  // row_ror:8
+  else if constexpr (O == 4) {
+    const float up = dpp_f32<0x104>(v), dn = dpp_f32<0x114>(v);  // row_shl:4 / row_shr:4
+    return (lane & 4) ? dn : up;
+  } else if constexpr (O == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v),
+                                                    __builtin_bit_cast(unsigned, v), false, false);
+    return __builtin_bit_cast(float, (unsigned)((lane & 16) ? r[0] : r[1]));
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v),
+                                                    __builtin_bit_cast(unsigned, v), false, false);
+    return __builtin_bit_cast(float, (unsigned)((lane & 32) ? r[0] : r[1]));
+  }
+}
+template <int O>
+__device__ __forceinline__ int xshfl_i(int v) {
+  return __builtin_bit_cast(int, xshfl<O>(__builtin_bit_cast(float, v)));  // moves only: bits kept
+}
+// butterfly sum / max over the whole wave (the __shfl_xor 32, 16, ..., 1 order)
+__device__ __forceinline__ float wave_sum_f32(float v) {
+  v += xshfl<32>(v); v += xshfl<16>(v); v += xshfl<8>(v);
+  v += xshfl<4>(v); v += xshfl<2>(v); v += xshfl<1>(v);
+  return v;
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+  v = fmaxf(v, xshfl<32>(v)); v = fmaxf(v, xshfl<16>(v)); v = fmaxf(v, xshfl<8>(v));
+  v = fmaxf(v, xshfl<4>(v)); v = fmaxf(v, xshfl<2>(v)); v = fmaxf(v, xshfl<1>(v));
+  return v;
+}
+
 // x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the
 // ~10-instruction IEEE division: SiLU runs on every staged vocoder activation.
 __device__ __forceinline__ float silu(float x) {
@@ -280,13 +326,13 @@ __device__ __forceinline__ void ln_rows_wave(const float* x, int64_t ldx, int ro
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) s += ln_sum4(v[j][k]);
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum_f32(s);
     const float mean = s / d;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
       if (lane + 64 * k < nv) q += ln_sq4(v[j][k], mean);
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum_f32(q);
     const float rstd = rsqrtf(q / d + eps);
     const bool rok = row0 + j * rstep < nrows;
     _Float16* orow = out + (int64_t)(lrow0 + j * rstep) * ldo;
@@ -319,7 +365,7 @@ __device__ __forceinline__ void ln_row_wave(const float* xr, const float* __rest
       v[i] = t;
       s += t;
     }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum_f32(s);
     const float mean = s / d;
     float q = 0.f;
 #pragma unroll
@@ -327,7 +373,7 @@ __device__ __forceinline__ void ln_row_wave(const float* xr, const float* __rest
       const int c = lane + 64 * i;
       if (c < d) q += (v[i] - mean) * (v[i] - mean);
     }
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum_f32(q);
     const float rstd = rsqrtf(q / d + eps);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     v[k] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     s += ln_sum4(v[k]);
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave_sum_f32(s);
   const float mean = s / d;
   float q = 0.f;
 #pragma unroll
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     const int i = lane + k * 64;
     if (i < nv) q += ln_sq4(v[k], mean);
   }
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  q = wave_sum_f32(q);
   const float rstd = rsqrtf(q / d + eps);
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
@@ -84,6 +84,27 @@ void layernorm_launch(const float* x, const float* g, const float* b, _Float16* 
 void layernorm_f32_launch(const float* x, const float* g, const float* b, float* out, int rows,
                           int d, float eps, hipStream_t s) {
   ln_dispatch<true>(x, g, b, out, rows, d, eps, s);
+}
+
+// The wave shuffles of mfma.h (xshfl<O>, 64 lanes) against the lane permutation they stand
+// for: out[w][k][lane] = xshfl<2^k>(in[w][lane]), k = 0..5 (janus_wave_xor_f32, a kernel
+// test entry).
+__global__ __launch_bounds__(64) void wave_xor_kernel(const float* __restrict__ in, float* __restrict__ out) {
+  const int lane = threadIdx.x;
+  const float v = in[blockIdx.x * 64 + lane];
+  float* o = out + (int64_t)blockIdx.x * 6 * 64 + lane;
+  o[0] = xshfl<1>(v);
+  o[64] = xshfl<2>(v);
+  o[128] = xshfl<4>(v);
+  o[192] = xshfl<8>(v);
+  o[256] = xshfl<16>(v);
+  o[320] = xshfl<32>(v);
+}
+
+void wave_xor_launch(const float* in, float* out, int n_waves, hipStream_t s) {
+  if (n_waves <= 0) return;
+  wave_xor_kernel<<<n_waves, 64, 0, s>>>(in, out);
+  JANUS_LAUNCH_CHECK();
 }
 
 }  // namespace janus

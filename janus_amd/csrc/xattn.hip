@@ -104,8 +104,13 @@ struct XGeo {
 // DIRECT (one key split, r05): the block holds the whole softmax of its row, so it writes
 // c[b][h*D + j] = C / l in fp16 itself (the merge's arithmetic at one split: weight
 // exp2(m - m) = 1, L = l, c = C * (1 / L)) and no merge launch follows.
-template <int D, int CH, bool PAIR = false, bool DIRECT = false>
-__global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xattn_kernel(
+// PF2 (DIRECT, r05): two chunks in flight per wave — chunk c + 2's E fragments load while
+// chunk c + 1's are already in flight, so each block streams at twice the bytes per round
+// trip (one block per CU on the staggered decoder's partition streams at the per-CU
+// latency rate: ≈ 24 GB/s with one 64 KB chunk in flight). Same chunk order and
+// arithmetic: bit-identical to the one-deep form. 32 more VGPRs: one block per CU.
+template <int D, int CH, bool PAIR = false, bool DIRECT = false, bool PF2 = false>
+__global__ __launch_bounds__(CH * 8, PF2 ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2)) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
     _Float16* __restrict__ out = nullptr) {
@@ -147,20 +152,24 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
                         : zero_half8();
   for (int i = tid; i < 16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
 
-  half8 ef[KS];
-  auto load_e = [&](int t) {
-    const int key = t + 16 * nt + lr;
-    const bool ok = key < t1;
+  half8 ef[KS], eg[KS];  // eg: the second chunk in flight (PF2)
+  auto load_to = [&](half8 (&dst)[KS], int t) __attribute__((always_inline)) {
+    // PF2: keys past the split's end load its last key instead (no branch around the loads,
+    // so the wait before a chunk's first MFMA counts only the other chunk's loads as still
+    // in flight); their scores are masked (-inf) and their P entries are 0, so those finite
+    // rows add exact zeros to C, as the zero rows of the one-deep form do
+    const int key = PF2 ? min(t + 16 * nt + lr, t1 - 1) : t + 16 * nt + lr;
+    const bool ok = PF2 || key < t1;
     const _Float16* src = eb + (int64_t)key * D + kh * KH + 8 * lg;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #ifdef JANUS_XATTN_NT
     {
       const uint4 u = ok ? ld_nt(src + 32 * ks) : make_uint4(0, 0, 0, 0);
-      ef[ks] = *reinterpret_cast<const half8*>(&u);
+      dst[ks] = *reinterpret_cast<const half8*>(&u);
     }
 #else
-      ef[ks] = ok ? *reinterpret_cast<const half8*>(src + 32 * ks) : zero_half8();
+      dst[ks] = ok ? *reinterpret_cast<const half8*>(src + 32 * ks) : zero_half8();
 #endif
   };
 
@@ -171,20 +180,24 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
 #pragma unroll
   for (int i = 0; i < HPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 
-  if (t0 < t1) load_e(t0);
+  if (PF2 || t0 < t1) load_to(ef, t0);
+  if (PF2) load_to(eg, t0 + CH);
   __syncthreads();
-  for (int t = t0; t < t1; t += CH) {
+  // one chunk of CH keys whose E fragments are in `cur`; `cur` is refilled with the chunk
+  // `ahead` chunks on (1, or 2 with PF2) once its rows are in LDS
+  auto chunk = [&](int t, half8 (&cur)[KS]) __attribute__((always_inline)) {
     // ---- S partial: rows = heads, cols = keys 16nt.., k = dims of half kh
     f32x4 accs = zero_f32x4();
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) accs = mfma16(qa[ks], ef[ks], accs);
+    for (int ks = 0; ks < KS; ++ks) accs = mfma16(qa[ks], cur[ks], accs);
     // E rows -> LDS (row-major) for the P.E product
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
-      *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = ef[ks];
+      *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = cur[ks];
 #pragma unroll
     for (int r = 0; r < 4; ++r) sS[(kh * 16 + 4 * lg + r) * CH + 16 * nt + lr] = accs[r];
-    if (t + CH < t1) load_e(t + CH);  // next chunk in flight during softmax + P.E
+    if constexpr (PF2) load_to(cur, t + 2 * CH);        // in flight during the next chunk
+    else if (t + CH < t1) load_to(cur, t + CH);          // in flight during softmax + P.E
     __syncthreads();
 
     // ---- online softmax: wave w owns heads w, w + NW, ...; lane = key (lanes < CH)
@@ -199,13 +212,11 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
       }
       const bool valid = lane < nk;
       const float sc = valid ? sS[h * CH + lane] + sS[(16 + h) * CH + lane] : -INFINITY;
-      float mc = sc;
-      for (int o = 32; o > 0; o >>= 1) mc = fmaxf(mc, __shfl_xor(mc, o));
+      const float mc = wave_max_f32(sc);
       const float m_new = fmaxf(m_run[i], mc);
       const float alpha = exp2f(m_run[i] - m_new);  // 0 on the first chunk
       const float p = valid ? exp2f(sc - m_new) : 0.f;
-      float ps = p;
-      for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
+      const float ps = wave_sum_f32(p);
       l_run[i] = l_run[i] * alpha + ps;
       m_run[i] = m_new;
       if (lane < CH) sP[h * PP + (lane & ~31) + xkappa_inv(lane & 31)] = (_Float16)p;
@@ -242,6 +253,19 @@ __global__ __launch_bounds__(CH * 8, CH == 32 ? (D > 512 ? 2 : 3) : 2) void xatt
       }
     }
     __syncthreads();  // sE / sS / sP are rewritten by the next chunk
+  };
+  if constexpr (PF2) {
+    // both chunks of a pair run unconditionally inside the loop, so on every path into the
+    // loop head ef's loads are the older ones (the wait before its first MFMA leaves eg's
+    // eight in flight); an odd last chunk runs after it
+    int t = t0;
+    for (; t + CH < t1; t += 2 * CH) {
+      chunk(t, ef);
+      chunk(t + CH, eg);
+    }
+    if (t < t1) chunk(t, ef);
+  } else {
+    for (int t = t0; t < t1; t += CH) chunk(t, ef);
   }
 
   if constexpr (DIRECT) {
@@ -414,13 +438,11 @@ __global__ __launch_bounds__(CH * 8, 1) void xattn_group_kernel(
       if (!row_ok(h)) continue;  // wave-uniform
       const bool valid = lane < nk;
       const float sc = valid ? sS[h * CH + lane] + sS[(R16 + h) * CH + lane] : -INFINITY;
-      float mc = sc;
-      for (int o = 32; o > 0; o >>= 1) mc = fmaxf(mc, __shfl_xor(mc, o));
+      const float mc = wave_max_f32(sc);  // the same reductions as xattn_kernel
       const float m_new = fmaxf(m_run[i], mc);
       const float alpha = exp2f(m_run[i] - m_new);
       const float p = valid ? exp2f(sc - m_new) : 0.f;
-      float ps = p;
-      for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
+      const float ps = wave_sum_f32(p);
       l_run[i] = l_run[i] * alpha + ps;
       m_run[i] = m_new;
       if (lane < CH) sP[h * PP + (lane & ~31) + xkappa_inv(lane & 31)] = (_Float16)p;
@@ -743,6 +765,11 @@ int xattn_split_count(int Te, int requested) {
   return std::max(n, 1);
 }
 
+#ifndef JANUS_XATTN_PF1
+constexpr bool kXattnPF2 = true;
+#else
+constexpr bool kXattnPF2 = false;  // A/B build: one chunk in flight
+#endif
 template <int D, int CH>
 static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
                       float* part_c, float* part_ml, hipStream_t s, const int4* pairs, int npairs,
@@ -750,7 +777,7 @@ static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, in
   const int chunks = (Te + CH - 1) / CH;
   const int kps = (chunks + nsplit - 1) / nsplit * CH;
   const bool direct = out != nullptr;
-  auto kern = direct ? xattn_kernel<D, CH, false, true>
+  auto kern = direct ? xattn_kernel<D, CH, false, true, kXattnPF2>
               : pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
   const int ai = direct ? 2 : pairs != nullptr;
   static bool attr[3] = {false, false, false};

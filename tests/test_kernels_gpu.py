@@ -392,3 +392,18 @@ def test_gemm_layernorm_prologue_bit_identical(gpu, M, N):
              None, N, M, N, K, stream())
     torch.cuda.synchronize()
     assert torch.equal(out1, out2)
+
+
+def test_wave_xor_shuffles(gpu):
+    """mfma.h xshfl<O> (DPP quad_perm / row_ror / row_shl+shr, v_permlane16/32_swap): every
+    lane receives exactly lane ^ O's value, so the butterfly reductions built on it
+    (softmax, LayerNorm) keep __shfl_xor's association bit for bit."""
+    n = 4
+    x = torch.randn(n, 64, generator=torch.Generator().manual_seed(7))
+    dx = x.to(gpu)
+    out = torch.empty(n, 6, 64, device=gpu)
+    nat.call("janus_wave_xor_f32", dx.data_ptr(), out.data_ptr(), n, stream())
+    torch.cuda.synchronize()
+    lanes = torch.arange(64)
+    for k in range(6):
+        assert torch.equal(out[:, k].cpu(), x[:, lanes ^ (1 << k)]), k
