@@ -89,6 +89,23 @@ __device__ __forceinline__ float silu(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
 
+// SiLU of 8 staged fp16 activations. Default: each through fp32 (silu above) and rounded
+// once. JANUS_SILU_F16: fp16 arithmetic (v_exp_f16 / v_rcp_f16, packed multiplies), no
+// conversions — a few fp16 ulps instead of half of one.
+__device__ __forceinline__ half8 silu_h8(half8 v) {
+#ifdef JANUS_SILU_F16
+  const half8 t = v * (_Float16)(-1.4426950408889634f);
+  half8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = __builtin_amdgcn_rcph((_Float16)1.0f + __builtin_elementwise_exp2(t[j]));
+  return v * r;
+#else
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+  return v;
+#endif
+}
+
 // Streaming activation traffic of the vocoder (tiles read once per unit, outputs written
 // once): with JANUS_ACT_NT the accesses carry the non-temporal hint, so the multi-GB
 // vocoder stream does not displace what the concurrently running decoder re-reads

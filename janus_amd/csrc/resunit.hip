@@ -177,8 +177,7 @@ __global__ __launch_bounds__(64 * NW) void resunit_kernel(ResUnitArgs a, int til
           const int rr = r - P2 - P1;
           if (rr >= 0 && rr < BM) *reinterpret_cast<half8*>(sR + rr * LI + cc * 8) = v;
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)silu((float)v[j]);
+        v = silu_h8(v);
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
       }
     }

@@ -324,8 +324,12 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       const int rl = (ILO + i) * RPI + rr0;
       if (rl >= -P && rl < R0C - P) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#ifdef JANUS_ABL_NOSILU
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
+#else
+        v = silu_h8(v);
+#endif
         *reinterpret_cast<half8*>(sX + (rl + P) * LI + cc * 8) = v;
       }
     }
@@ -354,8 +358,12 @@ __global__ __launch_bounds__((WideGeo<C, V>::NT), (WideGeo<C, V>::MINB)) void re
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#ifdef JANUS_ABL_NOSILU
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
+#else
+        v = silu_h8(v);
+#endif
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
       }
     }
@@ -676,8 +684,12 @@ __global__ __launch_bounds__((LdsGeo<C, V>::NT), 3) void resunit_wide_lds_kernel
       const int r = idx / CPR, cc = idx % CPR;
       if (r < R0) {
         half8 v = *reinterpret_cast<const half8*>(&pf[i]);
+#ifdef JANUS_ABL_NOSILU
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)WSILU((float)v[j]);
+#else
+        v = silu_h8(v);
+#endif
         *reinterpret_cast<half8*>(sX + r * LI + cc * 8) = v;
       }
     }
