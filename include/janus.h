@@ -258,7 +258,9 @@ typedef struct {
                               2: one launch per layer step — segment B of layer l, the
                               self-attention of l + 1 (one wave per row and head, online
                               softmax over 64-key chunks) and segment A of l + 1 as one
-                              grid: 19 launches per position (every row's keys in two
+                              grid (layer 0's QKV, self-attention and segment A one head
+                              grid, the final LayerNorm the last segment's phase): 16
+                              launches per position (every row's keys in two
                               parts cut by its own length, merged in order: rows stay
                               independent of their neighbours) */
   uint32_t path_flags;     /* alternative decoder paths (JANUS_DEC_PATH_* bits), for the

@@ -27,6 +27,10 @@ struct DecSegArgs {
   unsigned* bar;             // 160 zeroed words (barrier counters, self-cleaning)
   unsigned* err;             // timeout flag (host-checked)
   long long* prof;           // phase stamps (JANUS_PHASE_PROF builds, tools/seg_prof.py); null
+  // [wqkv == null, fin_out != null] the last layer's segment B ends with the decoder's final
+  // LayerNorm of x -> fin_out [B][512] fp16 (layernorm_kernel's arithmetic), read by the
+  // vocabulary projection: no LayerNorm launch
+  const float* fing; const float* finb; _Float16* fin_out;
 };
 
 // The layer kernel's segment A runs the NEXT layer's weights over the same buffers: only
@@ -48,6 +52,11 @@ void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s);
 // segment B of layer l (b: its args, with layer l + 1's QKV weights and cache), the
 // self-attention of l + 1 and segment A of l + 1 (nx: its weights) in one launch
 void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s);
+// layer 0's head (g: segment A args of layer 0, with layer 0's LN1 / QKV weights and
+// cache in ln1g / ln1b / wqkv / bqkv / kc / vc): q, K/V[pos] = LN1(x) Wqkv^T + bqkv, the
+// self-attention and segment A of layer 0 in one launch (the QKV projection, self-attention
+// and segment A launches before the first cross-attention)
+void dec_head_launch(const DecSegArgs& g, int grid, hipStream_t s);
 // JANUS_PHASE_PROF builds: the stamp buffer for layer l when JANUS_SEG_PROF=l, else null
 long long* dec_seg_prof_target(int l);
 

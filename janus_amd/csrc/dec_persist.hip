@@ -676,6 +676,37 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
     LngW w;
     LngOut o{a.qkv, 3 * kD, a.kc, a.vc, a.pos, a.n_ctx, a.roff};
     lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, pst, 30);
+  } else if (a.fin_out) {
+    // phase 5 of the last layer: the decoder's final LayerNorm, one wave per row, with
+    // layernorm_kernel's arithmetic (ln_sum4 / ln_sq4 / ln_norm4, butterfly sums), x read
+    // sc1 (rows other blocks' phase 4 just wrote)
+    grid_barrier(a.bar, e0 + 4, a.err, st);
+    sink ^= touched;
+    touched = 0u;
+    const int row = (int)blockIdx.x * (kNT / 64) + wv;
+    if (row < B) {  // wave-uniform
+      float4 v[2], gg[2], bb[2];
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = lane + 64 * k;
+        v[k] = as_f4(ld_sc1(rx, (uint32_t)(row * kD + 4 * c) * 4));
+        gg[k] = reinterpret_cast<const float4*>(a.fing)[c];
+        bb[k] = reinterpret_cast<const float4*>(a.finb)[c];
+        s += ln_sum4(v[k]);
+      }
+      s = wave_sum_f32(s);
+      const float mean = s / kD;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) q += ln_sq4(v[k], mean);
+      q = wave_sum_f32(q);
+      const float rstd = rsqrtf(q / kD + 1e-5f);
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        reinterpret_cast<half4*>(a.fin_out + (int64_t)row * kD)[lane + 64 * k] =
+            ln_norm4(v[k], mean, rstd, gg[k], bb[k]);
+    }
   }
 }
 
@@ -892,6 +923,32 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
   grid_exit(bsg.bar);
 }
 
+// Layer 0's head: the QKV projection of layer 0 (segment B's phase 5 over the embedded
+// rows) | barrier 1 | the self-attention | barrier 2 | segment A of layer 0 — the three
+// launches before the first cross-attention as one grid.
+__global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float seg_smem[];
+  long long* st = seg_stamps(g.prof, 0);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  uint32_t touched = 0u, sink = 0u;
+  {
+    _Float16* sA = reinterpret_cast<_Float16*>(seg_smem + kRedF);
+    float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
+    LngW w;
+    LngOut o{g.qkv, 3 * kD, g.kc, g.vc, g.pos, g.n_ctx, g.roff};
+    lng_phase<LE_QKV>(w, g.wqkv, 3 * kD, g.MT, g.B, rsrc(g.x, (uint32_t)g.B * kD * 4), g.ln1g, g.ln1b,
+                      g.bqkv, o, sA, patch, lane, wv, [] {}, nullptr, 30);
+  }
+  grid_barrier(g.bar, 1, g.err, st);
+  touched = touch_splitk(g.wo, kD, g.MT);
+  attn_phase(g, seg_smem, lane, wv);
+  grid_barrier(g.bar, 2, g.err, st);
+  seg_a_body(g, seg_smem, st, nullptr, 2, touched, sink);
+  SEG_SINK(g, touched, sink);
+  SEG_END(st);
+  grid_exit(g.bar);
+}
+
 int dec_seg_grid(int B, int cus) {
   // rows in 16-row tiles, rounded to a power of two (<= 8); groups of 16-column tiles per
   // m-tile NG in {32, 16} (a divisor of 96, 128 and 256 tiles: QKV, fc1, qk) with
@@ -939,6 +996,15 @@ void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipSt
   JANUS_CHECK(2 * ((b.B + 1) / 2) <= grid && b.wqkv != nullptr && b.qkv != nullptr,
               "decoder layer kernel: a block per row pair and head group, and a next layer");
   dec_layer_kernel<<<grid, kNT, kSegLds, s>>>(b, nx);
+  JANUS_LAUNCH_CHECK();
+}
+
+void dec_head_launch(const DecSegArgs& g, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_head_kernel); attr = true; }
+  JANUS_CHECK(2 * ((g.B + 1) / 2) <= grid && g.wqkv != nullptr && g.qkv != nullptr,
+              "decoder head kernel: a block per row pair and head group, and layer 0's QKV");
+  dec_head_kernel<<<grid, kNT, kSegLds, s>>>(g);
   JANUS_LAUNCH_CHECK();
 }
 

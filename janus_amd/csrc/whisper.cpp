@@ -650,7 +650,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && xabs && !shared && !fused_ln &&
                        !ln_fuse && !rln && ngroups == 0 && npairs == 0;
   // persistent = 2: segment B of layer l, the self-attention of l + 1 and its segment A as
-  // ONE launch per layer step (dec_layer_kernel): 29 -> 19 launches per position
+  // ONE launch per layer step (dec_layer_kernel): 29 -> 19 launches per position; layer
+  // 0's QKV, self-attention and segment A as one head kernel and the final LayerNorm as the
+  // last segment B's phase: 16
   const bool layerk = persist && opt->persistent >= 2 && 2 * ((B + 1) / 2) <= seg_grid;
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
@@ -682,21 +684,34 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     g.pos = pos; g.n_ctx = NC; g.roff = roff;
     g.bar = Z.d_segbar.as<unsigned>(); g.err = Z.d_segerr.as<unsigned>();
     g.prof = dec_seg_prof_target(l);
+    if (layerk && l + 1 == nl && !lnp_fin) {  // the final LayerNorm as the last segment's phase
+      g.fing = fin_g; g.finb = fin_b; g.fin_out = a;
+    }
+    return g;
+  };
+  // layer 0's head kernel: segment A args of layer 0 with layer 0's own LN1 / QKV / cache
+  auto head_args = [&](int pos) {
+    DecSegArgs g = seg_args(0, pos);
+    DecLayer& L0 = w->dec[0];
+    g.ln1g = L0.ln1g; g.ln1b = L0.ln1b; g.wqkv = L0.wqkv.as<_Float16>(); g.bqkv = L0.bqkv.as<float>();
+    g.qkv = qkv; g.kc = Z.d_kc.as<_Float16>(); g.vc = Z.d_vc.as<_Float16>();
+    g.fing = nullptr; g.finb = nullptr; g.fin_out = nullptr;
     return g;
   };
   auto step = [&](int pos) {
     if (!(fuse_se && pos >= sample_begin && pos > 0))
       embed_launch(w->tok16.as<_Float16>(), pos_emb, tokens, maxlen, pos, d, x,
                    fused_ln ? lnp : nullptr, B, s, w->dec[0].ln1g, w->dec[0].ln1b,
-                   (ln_fuse || embed_ln) ? a : nullptr, roff);
+                   (ln_fuse || (embed_ln && !layerk)) ? a : nullptr, roff);
     for (int l = 0; l < nl; ++l) {
       DecLayer& L = w->dec[l];
       _Float16* kc = Z.d_kc.as<_Float16>() + (int64_t)l * B * NC * d;
       _Float16* vc = Z.d_vc.as<_Float16>() + (int64_t)l * B * NC * d;
       _Float16* ck = Z.d_ck.as<_Float16>() + (int64_t)l * Me * d;
       _Float16* cv = Z.d_cv.as<_Float16>() + (int64_t)l * Me * d;
-      if (persist && l > 0) {
-        // q and this layer's K/V cache row came from the previous layer's segment B
+      if (persist && (l > 0 || layerk)) {
+        // q and this layer's K/V cache row came from the previous layer's segment B (layer
+        // 0 with the layer kernel: from the head kernel below)
       } else if (fused_ln) {
         gemm_skinny_ln_launch(EPI_QKV, lnargs(L.ln1g, L.ln1b, L.wqkv.as<_Float16>(), L.bqkv.as<float>(),
                                               qkv, 3 * d, 3 * d, kc, vc, pos), s);
@@ -719,12 +734,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       }
       // (layer kernel: layers > 0 got their self-attention and segment A in the previous
       // layer's launch)
-      if (!(layerk && l > 0))
+      if (!layerk)
         decode_attention_split_launch(qkv, 3 * d, kc, vc, (int64_t)NC * d, d, pos + 1, o, d, B, H, scale,
                                       part_o, part_ml, s, roff, max_roff);
       if (persist) {
         const DecSegArgs g = seg_args(l, pos);
-        if (!(layerk && l > 0)) dec_seg_a_launch(g, seg_grid, s);
+        if (!layerk) dec_seg_a_launch(g, seg_grid, s);
+        else if (l == 0) dec_head_launch(head_args(pos), seg_grid, s);
         xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
                      s, true, nullptr, 0);
         if (layerk && l + 1 < nl) {
@@ -796,7 +812,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
             l + 1 < nl ? w->dec[l + 1].ln1b : fin_b);
     }
     if (pos + 1 < sample_begin) return;  // still inside the prompt
-    if (!ln_fuse && !lnp_fin) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
+    if (!ln_fuse && !lnp_fin && !layerk) layernorm_launch(x, fin_g, fin_b, a, B, d, 1e-5f, s);
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
                           lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap,
@@ -806,7 +822,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
                           Z.d_nsp.as<float>(), w->tok16.as<_Float16>(), pos_emb, d, x,
                           fused_ln ? lnp : nullptr, w->dec[0].ln1g, w->dec[0].ln1b,
-                          (ln_fuse || embed_ln) ? a : nullptr, roff);
+                          (ln_fuse || (embed_ln && !layerk)) ? a : nullptr, roff);
     else
       select_partials_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                              maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
