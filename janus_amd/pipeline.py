@@ -177,7 +177,7 @@ class JanusPipeline:
         self.keep_encoder_output = False
         self.last_encoder_output = None
         # serving-step geometry. The staggered step's decoder runs persistent segments
-        # (janus_decode_options.persistent; 2 = one launch per layer step, 19 launches per
+        # (janus_decode_options.persistent; 2 = one launch per layer step, 16 launches per
         # position: 246.5-248.5 vs 248.9-250.1 ms per step in three same-box rounds,
         # profiles/r05_layer_kernel_ab.txt)
         self.tuning = tuning if tuning is not None else ServingTuning()
