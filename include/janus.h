@@ -262,7 +262,10 @@ typedef struct {
                               grid, the final LayerNorm the last segment's phase): 16
                               launches per position (every row's keys in two
                               parts cut by its own length, merged in order: rows stay
-                              independent of their neighbours) */
+                              independent of their neighbours).
+                              3: as 2, with the cross-attention as the last phase of the
+                              head / layer grids: 10 launches per position, measured level
+                              with 2 */
   uint32_t path_flags;     /* alternative decoder paths (JANUS_DEC_PATH_* bits), for the
                               parity tests that hold every path bit-identical and for A/B
                               measurements; 0 = the measured default */

@@ -31,6 +31,9 @@ struct DecSegArgs {
   // LayerNorm of x -> fin_out [B][512] fp16 (layernorm_kernel's arithmetic), read by the
   // vocabulary projection: no LayerNorm launch
   const float* fing; const float* finb; _Float16* fin_out;
+  // [enc != null] the layer / head kernel ends with the cross-attention of the layer whose
+  // segment A it ran (xattn_body, one key split: xqk -> xc), as a phase after a barrier
+  const _Float16* enc; int Te;                               // enc [B][Te][512]
 };
 
 // The layer kernel's segment A runs the NEXT layer's weights over the same buffers: only

@@ -37,6 +37,7 @@
 #include "mfma.h"
 #include "kernels.h"
 #include "dec_persist.h"
+#include "xattn_body.h"
 #include <algorithm>
 #include <cstdlib>
 
@@ -454,7 +455,9 @@ __device__ __forceinline__ void lng_phase(LngW& W, const _Float16* wt, int N, in
                      (uint32_t)(((grow * o.n_ctx + cpos) * kD + (col % kD)) * 2));
           }
         } else {
-          *reinterpret_cast<half4*>(o.out + (int64_t)grow * o.ldo + col) = h;
+          // write-through: the layer kernel's cross-attention phase reads xqk in the launch
+          st_sc1_8(__builtin_bit_cast(u32x2v, h), rsrc(o.out, (uint32_t)B * o.ldo * 2),
+                   (uint32_t)((grow * o.ldo + col) * 2));
         }
       }
     }
@@ -877,6 +880,18 @@ __device__ __forceinline__ void attn_phase(const DecSegArgs& g, float* lds, int 
   }
 }
 
+// Cross-attention phase (layer / head kernel, after segment A): block b takes row b with
+// xattn_kernel's one-split body (xattn_body.h), its query rows read sc1 (written by this
+// launch's segment A), c written to xc for the next launch's segment B.
+constexpr int kXattnLds = XGeo<kD, 64>::LDS;
+__device__ __forceinline__ void xattn_phase(const DecSegArgs& g, float* lds) {
+  const int b = blockIdx.x;
+  if (b >= g.B) return;  // block-uniform
+  xattn_body<kD, 64, false, true, false, true>(g.xqk, g.enc, g.Te, 8, (g.Te + 63) / 64 * 64, nullptr, nullptr,
+                                               nullptr, const_cast<_Float16*>(g.xc), 0, 1, b,
+                                               reinterpret_cast<_Float16*>(lds));
+}
+
 // the touched dwords feed a store no reader looks at (word 150 of the counter block is
 // unused), taken with probability 2^-32: the loads cannot be dropped
 #define SEG_SINK(A, T, S) do { if (((S) ^ (T)) == 0x5eed5eedu) (A).bar[150] = 1u; } while (0)
@@ -918,6 +933,10 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
   DecSegArgs asg = bsg;
   asg.wo = nx.wo; asg.bo = nx.bo; asg.ln2g = nx.ln2g; asg.ln2b = nx.ln2b; asg.wqk = nx.wqk; asg.bqk = nx.bqk;
   seg_a_body(asg, seg_smem, st, nullptr, 6, touched, sink);
+  if (bsg.enc) {
+    grid_barrier(bsg.bar, 8, bsg.err, st);
+    xattn_phase(asg, seg_smem);
+  }
   SEG_SINK(bsg, touched, sink);
   SEG_END(st);
   grid_exit(bsg.bar);
@@ -944,6 +963,10 @@ __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
   attn_phase(g, seg_smem, lane, wv);
   grid_barrier(g.bar, 2, g.err, st);
   seg_a_body(g, seg_smem, st, nullptr, 2, touched, sink);
+  if (g.enc) {
+    grid_barrier(g.bar, 4, g.err, st);
+    xattn_phase(g, seg_smem);
+  }
   SEG_SINK(g, touched, sink);
   SEG_END(st);
   grid_exit(g.bar);
@@ -972,8 +995,12 @@ bool dec_seg_supported(int d, int H, int B, int cus) {
   return d == kD && H == 8 && dec_seg_grid(B, cus) > 0;
 }
 
-static void seg_attr(const void* k) {
-  JANUS_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds));
+static void seg_attr(const void* k, size_t lds = kSegLds) {
+  JANUS_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+}
+// the layer and head kernels with the cross-attention phase: its LDS tile on top
+static size_t layer_lds(const DecSegArgs& a) {
+  return a.enc ? std::max(kSegLds, (size_t)kXattnLds) : kSegLds;
 }
 
 void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s) {
@@ -992,19 +1019,21 @@ void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s) {
 
 void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s) {
   static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_layer_kernel); attr = true; }
+  if (!attr) { seg_attr((const void*)dec_layer_kernel, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
   JANUS_CHECK(2 * ((b.B + 1) / 2) <= grid && b.wqkv != nullptr && b.qkv != nullptr,
               "decoder layer kernel: a block per row pair and head group, and a next layer");
-  dec_layer_kernel<<<grid, kNT, kSegLds, s>>>(b, nx);
+  JANUS_CHECK(!b.enc || (b.B <= grid && b.Te > 0), "decoder layer kernel: a block per row for the cross-attention");
+  dec_layer_kernel<<<grid, kNT, layer_lds(b), s>>>(b, nx);
   JANUS_LAUNCH_CHECK();
 }
 
 void dec_head_launch(const DecSegArgs& g, int grid, hipStream_t s) {
   static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_head_kernel); attr = true; }
+  if (!attr) { seg_attr((const void*)dec_head_kernel, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
   JANUS_CHECK(2 * ((g.B + 1) / 2) <= grid && g.wqkv != nullptr && g.qkv != nullptr,
               "decoder head kernel: a block per row pair and head group, and layer 0's QKV");
-  dec_head_kernel<<<grid, kNT, kSegLds, s>>>(g);
+  JANUS_CHECK(!g.enc || (g.B <= grid && g.Te > 0), "decoder head kernel: a block per row for the cross-attention");
+  dec_head_kernel<<<grid, kNT, layer_lds(g), s>>>(g);
   JANUS_LAUNCH_CHECK();
 }
 

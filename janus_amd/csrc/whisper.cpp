@@ -654,6 +654,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // 0's QKV, self-attention and segment A as one head kernel and the final LayerNorm as the
   // last segment B's phase: 16
   const bool layerk = persist && opt->persistent >= 2 && 2 * ((B + 1) / 2) <= seg_grid;
+  // persistent = 3: the cross-attention as the head / layer kernel's last phase (10 launches
+  // per position); the decoder side measured level with 16 (369.1-369.3 vs 368.4-369.4 ms
+  // over 447 positions, profiles/r05_xattn_phase_ab.txt): a grid barrier costs what the
+  // launch boundary it replaces did
+  const bool xfuse = layerk && opt->persistent >= 3 && B <= seg_grid;
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
     if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed
@@ -687,6 +692,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     if (layerk && l + 1 == nl && !lnp_fin) {  // the final LayerNorm as the last segment's phase
       g.fing = fin_g; g.finb = fin_b; g.fin_out = a;
     }
+    if (xfuse) { g.enc = enc; g.Te = Te; }  // the cross-attention as the layer / head kernel's last phase
     return g;
   };
   // layer 0's head kernel: segment A args of layer 0 with layer 0's own LN1 / QKV / cache
@@ -741,8 +747,9 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         const DecSegArgs g = seg_args(l, pos);
         if (!layerk) dec_seg_a_launch(g, seg_grid, s);
         else if (l == 0) dec_head_launch(head_args(pos), seg_grid, s);
-        xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
-                     s, true, nullptr, 0);
+        if (!xfuse)  // (persistent 3: the cross-attention ran as the head / layer kernel's last phase)
+          xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
+                       s, true, nullptr, 0);
         if (layerk && l + 1 < nl) {
           DecLayer& N = w->dec[l + 1];
           const DecSegNext nx{N.wo.as<_Float16>(), N.bo, N.ln2g, N.ln2b, N.wqk.as<_Float16>(), N.bqk.as<float>()};
@@ -841,7 +848,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
       (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
       (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows, (int64_t)roff,
-      (int64_t)max_roff, (int64_t)persist + (int64_t)layerk, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
+      (int64_t)max_roff, (int64_t)persist + (int64_t)layerk + (int64_t)xfuse, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
       (int64_t)Z.d_segerr.p};
   arrival.now();  // all lanes' allocations done: captures may start
   if (Z.graphs.size() > 512) {

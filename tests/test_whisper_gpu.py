@@ -499,7 +499,7 @@ def test_layernorm_placements_bit_identical(base_engine, gpu, flags):
     assert torch.equal(t1, t2.cpu()) and torch.equal(n1, n2.cpu()) and torch.equal(s1, s2.cpu())
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_persistent_segments_vs_oracle(base_engine, gpu, mode):
     """The persistent decoder segments (janus_decode_options.persistent: per layer two
     resident-grid launches with in-launch barriers instead of ten launches) decode base.en
@@ -533,7 +533,7 @@ def test_persistent_segments_vs_oracle(base_engine, gpu, mode):
         assert abs(a - c) <= 5e-3 * c + 1e-12, (b, a, c)
 
 
-@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2)])
+@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2), (64, 3)])
 def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode):
     """Continuous batching through the persistent segments: two slot sets of `rows` rows
     (2 x 64 = the bench's decoder call), each batch started fresh in one call and continued
