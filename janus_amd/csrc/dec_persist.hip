@@ -897,6 +897,7 @@ __device__ __forceinline__ void xattn_phase(const DecSegArgs& g, float* lds) {
 #define SEG_SINK(A, T, S) do { if (((S) ^ (T)) == 0x5eed5eedu) (A).bar[150] = 1u; } while (0)
 
 __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
+  JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(a.prof, 0);
   uint32_t touched = 0u, sink = 0u;
@@ -907,6 +908,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
 }
 
 __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
+  JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(a.prof, 1);
   uint32_t touched = 0u, sink = 0u;
@@ -920,6 +922,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
 // and K/V rows write-through) | barrier 5 | the self-attention of layer l + 1 | barrier 6 |
 // segment A of layer l + 1 — the launches between two cross-attentions as one grid.
 __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSegNext nx) {
+  JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(bsg.prof, 2);
   const int lane = threadIdx.x & 63, wv = wave_id();
@@ -946,6 +949,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
 // rows) | barrier 1 | the self-attention | barrier 2 | segment A of layer 0 — the three
 // launches before the first cross-attention as one grid.
 __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
+  JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(g.prof, 0);
   const int lane = threadIdx.x & 63, wv = wave_id();

@@ -406,6 +406,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     const float* __restrict__ ln_g, const float* __restrict__ ln_b, int rot,
     const uint32_t* __restrict__ seeds, int pos) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
+  JANUS_DEC_WAVE_PRIO();
   constexpr int K = NKS * 32;
   constexpr int kLgWaves = lg_waves(K);
   constexpr int AP = K + 16;  // row pitch (halves): 16*AP bytes with AP/8 % 4 == 2 -> conflict-free
@@ -817,6 +818,7 @@ __global__ __launch_bounds__(256) void select_embed_kernel(
     int d, float* __restrict__ x, float2* __restrict__ part, const float* __restrict__ ln_g,
     const float* __restrict__ ln_b, _Float16* __restrict__ ln_out, const int32_t* __restrict__ roff) {
   __shared__ int s_tok;
+  JANUS_DEC_WAVE_PRIO();
   const int t = select_row(parts, nblk, R, rules, tokens, ld, pos, done, sum_lp, n_tok, plen, nsp, roff);
   const int pb = pos + (roff ? roff[blockIdx.x] : 0);
   if (pb + 1 >= ld) return;  // a staggered row past its last position: nothing to embed

@@ -67,6 +67,16 @@ __device__ __forceinline__ float xshfl(float v) {
     return __builtin_bit_cast(float, (unsigned)((lane & 32) ? r[0] : r[1]));
   }
 }
+// Wave priority of the decoder's kernels: the YIN blocks that share the decoder's CUs keep
+// priority 0, so the latency-bound decoder phases win the issue arbitration on a shared
+// SIMD and YIN takes the cycles they leave (decoder side -4 to -5 ms per step at the same
+// YIN share; with a sixth packet of vocoder work moved to it, 241.4-241.7 vs 243.6-244.0 ms
+// per step, profiles/r05_dec_prio_ab.txt). -DJANUS_DEC_PRIO=0 builds the old order.
+#ifndef JANUS_DEC_PRIO
+#define JANUS_DEC_PRIO 3
+#endif
+#define JANUS_DEC_WAVE_PRIO() __builtin_amdgcn_s_setprio(JANUS_DEC_PRIO)
+
 template <int O>
 __device__ __forceinline__ int xshfl_i(int v) {
   return __builtin_bit_cast(int, xshfl<O>(__builtin_bit_cast(float, v)));  // moves only: bits kept

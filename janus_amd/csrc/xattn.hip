@@ -71,6 +71,7 @@ __global__ __launch_bounds__(CH * 8, PF2 ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
     _Float16* __restrict__ out = nullptr) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  JANUS_DEC_WAVE_PRIO();
   xattn_body<D, CH, PAIR, DIRECT, PF2>(qk, enc, Te, H, kps, part_c, part_ml, pairs, out, blockIdx.x,
                                        gridDim.x, blockIdx.y, smem);
 }

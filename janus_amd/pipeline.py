@@ -39,7 +39,7 @@ class ServingTuning:
     the A/B tools build one with ``from_env`` (JANUS_<FIELD> in upper case) and pass it in."""
     persistent: int = 2             # staggered decoder: janus_decode_options.persistent
     stagger_sets: int = 2           # decoder slot sets per staggered call (>= 2)
-    voc_dec_utts: int = 5           # staggered: packets rendered on the decoder's CUs
+    voc_dec_utts: int = 6           # staggered: packets rendered on the decoder's CUs
     yin_dec_utts: Optional[int] = None  # YIN utterances on the decoder side (None: the
                                     # staggered step's controller; 0 in the other steps)
     yin_beside: int = 128           # staggered: YIN grid cap beside the decoder (0 = after it)
@@ -585,7 +585,9 @@ class JanusPipeline:
         # decoder segments: 3 / 4 / 5 -> 252.2-252.7 / 251.2-251.3 / 251.9-252.3 ms per step,
         # profiles/r05_voc_dec_sweep2.txt; with the layer-step grid and the DPP reductions the
         # decoder side has slack at 4 (YIN split pinned at 63): 4 / 5 / 6 / 8 -> 246.4-247.7 /
-        # 244.7-245.4 / 245.7-246.8 / 249.3-249.8, profiles/r05_voc_dec_sweep3.txt)
+        # 244.7-245.4 / 245.7-246.8 / 249.3-249.8, profiles/r05_voc_dec_sweep3.txt; with the
+        # decoder's waves at priority 3 over the YIN blocks beside them, 6: see mfma.h
+        # JANUS_DEC_PRIO)
         kv = 0
         pk_dec = []
         wav_b = pcm_b = None

@@ -72,7 +72,7 @@ def test_serving_tuning_from_env():
     the pipeline itself reads no environment."""
     from janus_amd.pipeline import ServingTuning
     t = ServingTuning.from_env({})
-    assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 5
+    assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 6
     t = ServingTuning.from_env({"JANUS_STAGGER_SETS": "3", "JANUS_YIN_DEC_UTTS": "5",
                                 "JANUS_HOST_PREFETCH": "0", "JANUS_YIN_SIDE": "beside",
                                 "JANUS_OTHER": "1"})

@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench A/B over env settings / builds, timed steps only (--no-idle-latency):
-#   tools/gpu_ab_env.sh tag default env:A=1,B=2 lib:libx.so ...
+#   tools/gpu_ab_env.sh tag default env:A=1,B=2 lib:libx.so lib:libx.so+env:A=1 ...
 # (env: comma-separated NAME=VALUE pairs: ServingTuning fields, or kernel switches with a
 # -DJANUS_AB_KNOBS lib; lib: an alternative in-tree build, JANUS_LIB)
 # AB_REPS rounds (default 2), AB_STEPS timed steps (default 5). One line per run:
@@ -17,7 +17,9 @@ for v in "$@"; do
   case "$v" in
     default) ;;
     env:*) envs="${v#env:}"; envs="${envs//,/ }" ;;
-    lib:*) export JANUS_LIB="${v#lib:}" ;;
+    lib:*) l="${v#lib:}"
+           case "$l" in *+env:*) envs="${l#*+env:}"; envs="${envs//,/ }"; l="${l%%+env:*}" ;; esac
+           export JANUS_LIB="$l" ;;
   esac
   name=$(echo "$v" | tr -c 'A-Za-z0-9_=.\n' '_')
   out=gpurun_out/ab_${tag}_${name}_$rep
