@@ -65,15 +65,15 @@ void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int 
   JANUS_LAUNCH_CHECK();
 }
 
-template <int D, int CH, bool PAIR = false, bool DIRECT = false, bool PF2 = false>
+template <int D, int CH, bool PAIR = false, bool DIRECT = false, bool PF2 = false, bool ROWLD = false>
 __global__ __launch_bounds__(CH * 8, PF2 ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2)) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
     _Float16* __restrict__ out = nullptr) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   JANUS_DEC_WAVE_PRIO();
-  xattn_body<D, CH, PAIR, DIRECT, PF2>(qk, enc, Te, H, kps, part_c, part_ml, pairs, out, blockIdx.x,
-                                       gridDim.x, blockIdx.y, smem);
+  xattn_body<D, CH, PAIR, DIRECT, PF2, false, ROWLD>(qk, enc, Te, H, kps, part_c, part_ml, pairs, out,
+                                                     blockIdx.x, gridDim.x, blockIdx.y, smem);
 }
 
 // GROUP (r04): up to 2*NMT decoder rows attending to the same encoder row — the best_of = 5
@@ -524,6 +524,11 @@ int xattn_split_count(int Te, int requested) {
   return std::max(n, 1);
 }
 
+#ifndef JANUS_XATTN_FRAG
+constexpr bool kXattnRow = true;   // one-split D = 512: whole-row loads (ROWLD)
+#else
+constexpr bool kXattnRow = false;  // A/B build: the fragment-pattern loads
+#endif
 #ifndef JANUS_XATTN_PF1
 constexpr bool kXattnPF2 = true;
 #else
@@ -536,8 +541,14 @@ static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, in
   const int chunks = (Te + CH - 1) / CH;
   const int kps = (chunks + nsplit - 1) / nsplit * CH;
   const bool direct = out != nullptr;
-  auto kern = direct ? xattn_kernel<D, CH, false, true, kXattnPF2>
-              : pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
+  constexpr bool row = kXattnRow && D == 512 && CH == 64;
+  decltype(&xattn_kernel<D, CH, false>) kern;
+  if (direct) {
+    if constexpr (row) kern = xattn_kernel<D, CH, false, true, false, true>;
+    else kern = xattn_kernel<D, CH, false, true, kXattnPF2>;
+  } else {
+    kern = pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;
+  }
   const int ai = direct ? 2 : pairs != nullptr;
   static bool attr[3] = {false, false, false};
   if (!attr[ai]) {

@@ -55,7 +55,11 @@ struct XGeo {
 // a phase, dec_persist.hip): split s of nsplit, MFMA-row group by (the utterance, or
 // pairs[by]), LDS at smem (XGeo::LDS bytes). SC1Q: the query rows were written by other
 // workgroups of the same launch — read them agent-coherent (sc1), not through a stale L2.
-template <int D, int CH, bool PAIR, bool DIRECT, bool PF2, bool SC1Q = false>
+// ROWLD (DIRECT, D = 512, CH = 64): each wave loads whole 1 KB key rows (8 keys of the
+// chunk, lane = 16-byte column) straight into their sE rows, and the S phase reads its B
+// fragments back from sE — the fragment-pattern loads touch 16 keys x 64 B per instruction
+// and stream ≈ 20 % slower per CU (tools/stream_probe.hip). One more barrier per chunk.
+template <int D, int CH, bool PAIR, bool DIRECT, bool PF2, bool SC1Q = false, bool ROWLD = false>
 __device__ __forceinline__ void xattn_body(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
@@ -102,8 +106,18 @@ __device__ __forceinline__ void xattn_body(
   }
   for (int i = tid; i < 16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
 
+  static_assert(!ROWLD || (D == 512 && CH == 64 && DIRECT && !PF2 && !PAIR && KS == CH / NW),
+                "row loads: one 1 KB key row per register slot");
   half8 ef[KS], eg[KS];  // eg: the second chunk in flight (PF2)
   auto load_to = [&](half8 (&dst)[KS], int t) __attribute__((always_inline)) {
+    if constexpr (ROWLD) {
+#pragma unroll
+      for (int i = 0; i < KS; ++i) {
+        const int key = min(t + (CH / NW) * w + i, t1 - 1);  // past the end: a finite row, masked
+        dst[i] = *reinterpret_cast<const half8*>(eb + (int64_t)key * D + 8 * lane);
+      }
+      return;
+    }
     // PF2: keys past the split's end load its last key instead (no branch around the loads,
     // so the wait before a chunk's first MFMA counts only the other chunk's loads as still
     // in flight); their scores are masked (-inf) and their P entries are 0, so those finite
@@ -138,16 +152,32 @@ __device__ __forceinline__ void xattn_body(
   auto chunk = [&](int t, half8 (&cur)[KS]) __attribute__((always_inline)) {
     // ---- S partial: rows = heads, cols = keys 16nt.., k = dims of half kh
     f32x4 accs = zero_f32x4();
+    if constexpr (ROWLD) {
+      // the wave's 8 key rows -> sE, the next chunk's rows in flight, then the S fragments
+      // from sE once every wave's rows are in
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) accs = mfma16(qa[ks], cur[ks], accs);
-    // E rows -> LDS (row-major) for the P.E product
+      for (int i = 0; i < KS; ++i)
+        *reinterpret_cast<half8*>(sE + ((CH / NW) * w + i) * QP + 8 * lane) = cur[i];
+      if (t + CH < t1) load_to(cur, t + CH);
+      __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = cur[ks];
+      for (int ks = 0; ks < KS; ++ks)
+        accs = mfma16(qa[ks], *reinterpret_cast<const half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg),
+                      accs);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) accs = mfma16(qa[ks], cur[ks], accs);
+      // E rows -> LDS (row-major) for the P.E product
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        *reinterpret_cast<half8*>(sE + (16 * nt + lr) * QP + kh * KH + 32 * ks + 8 * lg) = cur[ks];
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sS[(kh * 16 + 4 * lg + r) * CH + 16 * nt + lr] = accs[r];
-    if constexpr (PF2) load_to(cur, t + 2 * CH);        // in flight during the next chunk
-    else if (t + CH < t1) load_to(cur, t + CH);          // in flight during softmax + P.E
+    if constexpr (!ROWLD) {
+      if constexpr (PF2) load_to(cur, t + 2 * CH);        // in flight during the next chunk
+      else if (t + CH < t1) load_to(cur, t + CH);          // in flight during softmax + P.E
+    }
     __syncthreads();
 
     // ---- online softmax: wave w owns heads w, w + NW, ...; lane = key (lanes < CH)
