@@ -55,13 +55,10 @@ def parse():
                          "even); 0 = sequential step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     ap.add_argument("--stagger", type=int, default=int(os.environ.get("JANUS_STAGGER", "1")),
-                    help="1: continuous batching in the decoder (JanusPipeline.step_staggered): "
-                         "each step's decoder call advances batch i from position 0 and batch "
-                         "i-1 from the middle, 128 rows; still one batch in and one out per step. "
-                         "2: the same with the encoder on its own CU lane beside the decoder "
-                         "and the vocoder (JanusPipeline.step_pipelined, --enc-cus)")
-    ap.add_argument("--enc-cus", type=int, default=int(os.environ.get("JANUS_ENC_CUS", "4")),
-                    help="--stagger 2: CUs per XCD for the encoder lane, carved out of --overlap")
+                    help="1: continuous batching of windows in the decoder (JanusPipeline."
+                         "step_staggered): each step's decoder calls advance 2 slot sets of 64 "
+                         "rows; the first windows of batch i and the continuation windows of "
+                         "the seek loop enter as fresh rows; 0: the overlapped step")
     ap.add_argument("--no-idle-latency", action="store_true",
                     help="skip the flush and the three idle-pipeline latency steps after the timed "
                          "region (profiling runs: only priming, warm-up and timed overlapped steps "
@@ -87,6 +84,10 @@ def parse():
                     help="after the headline (T = 0) line, time this many steps of the same serving step with "
                          "faster-whisper's temperature fallback on and report them as "
                          "xrt_with_fallback (0: skip)")
+    ap.add_argument("--first-window-steps", type=int, default=5,
+                    help="after the headline, time this many steps decoding each clip's first "
+                         "window only (the r05 serving semantics) and report xrt_first_window "
+                         "(0: skip)")
     ap.add_argument("--fallback", action="store_true",
                     help="run faster-whisper's temperature fallback on windows failing their gates "
                          "(generate_with_fallback: 5 temperatures x best_of 5 sampled re-decodes); "
@@ -714,14 +715,11 @@ def main():
     last = {}
 
     def step():
-        if args.overlap > 0 and args.stagger == 2 and len(pipe.temperatures) == 1:
-            # three lanes: encoder of batch i, decoder of batches i-1 / i-2, vocoder of i-3
-            enc, wav, pcm16 = pipe.step_pipelined(pcm, offs, lengths, frames, args.overlap,
-                                                  args.enc_cus)
-        elif args.overlap > 0 and args.stagger:
-            # continuous batching: batch i's first half and batch i-1's second half of the
-            # decode in one decoder call, the vocoder of batch i-2 beside it (with the
-            # fallback on, the completing batch's failing windows re-decode after it)
+        if args.overlap > 0 and args.stagger:
+            # continuous batching of windows: batch i's first windows and the queued
+            # continuation windows of earlier batches in the decoder calls, the vocoder of the
+            # oldest finished batch beside them (with the fallback on, the completed windows
+            # that fail their gates re-decode first, on the whole GPU)
             enc, wav, pcm16 = pipe.step_staggered(pcm, offs, lengths, frames, args.overlap)
         elif args.overlap > 0:
             # steady-state serving pipeline: batch i through mel / encoder / decoder / YIN,
@@ -733,18 +731,20 @@ def main():
         last["pcm16"] = pcm16
         return enc
 
-    # overlapped: one priming step first (it fills the pipeline: encode only, no vocoder
-    # pass), then the W warm-up steps, each a full encode + decode like the timed ones
-    # decoder slot sets (staggered: tuning.stagger_sets batches per decoder call) and the
-    # pipeline depth (calls before the first batch comes out)
-    # (the three-lane step is greedy-only: with --fallback --stagger 2 the staggered step runs)
-    if args.fallback and args.stagger == 2:
-        args.stagger = 1
-    sets = (max(2, tuning.stagger_sets) if args.stagger == 1
-            else 2 if args.stagger == 2 else 1)
-    depth = (sets if args.stagger == 1 else 3 if args.stagger == 2 else 1) if args.overlap > 0 else 0
-    prime = depth
-    for _ in range(args.warmup + prime):
+    # priming: the pipeline's depth in steps (staggered: until the first batch comes out,
+    # 3 steps with two windows per clip), then the W warm-up steps, each a full step like
+    # the timed ones
+    sets = max(2, tuning.stagger_sets) if args.stagger else 1
+    calls = tuning.calls() if args.stagger else 1
+    depth = (pipe.staggered_depth() if args.stagger else 1) if args.overlap > 0 else 0
+    enc = None
+    for _ in range(depth):
+        enc = step()
+    guard = 0
+    while args.overlap > 0 and enc is None and guard < 8:   # longer seek loops fill later
+        enc = step()
+        guard += 1
+    for _ in range(args.warmup):
         enc = step()
     torch.cuda.synchronize()
     if use_dist:
@@ -763,7 +763,7 @@ def main():
         enc = step()
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
-        tok_counts.append(enc.n_tokens)  # bookkeeping reduced after the timed region
+        tok_counts.append(enc)  # bookkeeping reduced after the timed region
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -771,18 +771,34 @@ def main():
     pipe.vocoder.set_timing(False)
     yin_dec_utts = (getattr(pipe, "_stag", None) or {}).get("n_dec") if args.stagger == 1 else None
     sides = [(e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in (pipe.side_events or [])]
-    enc_side = [e[4].elapsed_time(e[5]) for e in (pipe.side_events or []) if len(e) >= 6]
     pipe.side_events = None
     dec_positions, dec_launches = pipe.whisper.decode_info()
-    tok_counts = [float(n.float().mean().item()) for n in tok_counts]
+    # tokens sampled per utterance over all of its windows, and the windows themselves
+    tok_counts = [float(np.mean(e.sampled)) for e in tok_counts]
+    windows = [int(x) for x in enc.windows]
     fams = pipe.vocoder.family_stats(reset=False)
     flops, kms, launches = pipe.vocoder.conv_stats(reset=True)
-    # faster-whisper's seek loop would decode a second window of every clip whose first
-    # window's seek (the last timestamp pair) stops short of its content (gate 7); the
-    # pipeline decodes first windows only, so these are counted, not decoded
+    # faster-whisper's seek loop decodes windows until every clip's seek has reached its
+    # content: clips of the last timed batch left short of it (0 when every window was decoded)
     content = [(n + 2) // 3 // 160 for n in lengths]
-    seek_extra = int(sum(1 for g, c in zip(enc.gates or [], content) if len(g) > 7 and g[7] < c))
-    flush = {0: pipe.flush, 1: pipe.flush_staggered, 2: pipe.flush_pipelined}
+    seek_extra = int(sum(1 for st, c in zip(enc.streams, content) if st.seek < c))
+    flush = {0: pipe.flush, 1: pipe.flush_staggered}
+
+    def timed_leg(n_steps, prime):
+        """n_steps timed steps of the current setting after `prime` untimed ones (the
+        pipeline's depth plus a warm step), then drained: (per-step seconds, last result)."""
+        r = None
+        for _ in range(prime):
+            r = step() or r
+        ts = []
+        for _ in range(n_steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = step() or r
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        flush[min(args.stagger, 1)](frames)
+        return ts, r
     # latency of one batch through an IDLE pipeline (encode then decode back to back, nothing
     # else on the GPU), beside the serving figure (an utterance's encode step + decode step)
     idle = []
@@ -796,7 +812,7 @@ def main():
         idle.append(time.perf_counter() - t0)
     # the latency operating point: the overlapped step (--stagger 0: an utterance's encode +
     # decode step, then its vocoder step) timed right after, beside the staggered headline
-    # (three steps per utterance): p50 of consecutive step pairs
+    # (four steps per utterance with two windows each): p50 of consecutive step pairs
     ov = None
     if args.overlap > 0 and args.stagger != 0 and not args.no_idle_latency and not args.fallback:
         ov_t = []
@@ -812,31 +828,33 @@ def main():
                                                         for i in range(len(ov_t) - 1)])) * 1000.0, 2),
               "step_ms": [round(v * 1000.0, 1) for v in ov_t],
               "xrt": round(B * args.seconds / float(np.mean(ov_t)), 2)}
+    # the r05 serving semantics beside the headline: each clip's FIRST window only (the seek
+    # loop stopped after it), the same staggered step with one decoder call per step
+    fw = None
+    if (args.overlap > 0 and args.stagger == 1 and pipe.tuning.all_windows
+            and not args.no_idle_latency and args.first_window_steps > 0):
+        pipe.tuning.all_windows = False
+        fw_t, fwr = timed_leg(args.first_window_steps, pipe.staggered_depth() + 1)
+        pipe.tuning.all_windows = True
+        fw = {"xrt": round(B * args.seconds / float(np.mean(fw_t)), 2),
+              "step_ms": [round(v * 1000.0, 1) for v in fw_t],
+              "windows_decoded": int(sum(fwr.windows)) if fwr is not None else None}
     # the same serving step with faster-whisper's temperature fallback on (the library
     # default; every window of the seeded synthetic model fails its gates, so each runs all
-    # five sampled temperatures x best_of 5): reported beside the T = 0 headline
+    # five sampled temperatures x best_of 5), every window of the seek loop: reported beside
+    # the T = 0 headline
     fb = None
     if (args.fallback_steps > 0 and not args.fallback and not args.no_idle_latency
             and args.overlap > 0):
         pipe.temperatures = TEMPERATURES
-        # the pipeline's depth in priming calls (the first output needs depth + 1 calls),
-        # plus one warm step (B = 320 sampled-decode graphs)
-        for _ in range(depth + 1):
-            step()
-        fb_t = []
-        for _ in range(args.fallback_steps):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            fenc = step()
-            torch.cuda.synchronize()
-            fb_t.append(time.perf_counter() - t0)
-        flush[min(args.stagger, 1)](frames)
+        fb_t, fenc = timed_leg(args.fallback_steps, depth + 1)
         pipe.temperatures = (0.0,)
         fb = {"xrt": round(B * args.seconds / float(np.mean(fb_t)), 2),
-              "step": {0: "overlapped", 1: "staggered", 2: "staggered"}[args.stagger],
+              "step": {0: "overlapped", 1: "staggered"}[args.stagger],
               "step_ms": [round(v * 1000.0, 1) for v in fb_t],
-              "sampled_decodes": int(sum(g[6] for g in fenc.gates or [])),
-              "windows_failing_t0": int(sum(g[0] for g in fenc.gates or []))}
+              "windows_decoded": int(sum(fenc.windows)) if fenc is not None else None,
+              "sampled_decodes": int(sum(s.fallback_decodes for s in fenc.streams)) if fenc else None,
+              "windows_failing_t0": int(sum(s.fallbacks for s in fenc.streams)) if fenc else None}
     # whole-job time = max over ranks; result gather (packet bytes) once, outside the timing
     total_t = torch.tensor([t_end - t_begin], dtype=torch.float64, device=dev)
     n_packets = sum(p is not None for p in enc.packets)
@@ -898,10 +916,9 @@ def main():
                        "model": args.model, "global_batch": world * B, "seq_len": 1500,
                        "parallelism": f"dp{world}", "max_length": args.max_length},
             "xrt_per_gpu": round(value / world, 2),
-            # overlapped: an utterance is encoded in one step and vocoded in the next
             # an utterance's steps: encode + decode, then vocoder (overlapped: 2 steps);
-            # staggered: encode + the N decode chunks, then the vocoder (N + 1 steps);
-            # pipelined: encode, first half, second half, vocoder (4 steps)
+            # staggered with two windows per clip: first window (one step), continuation
+            # window (two steps), then the vocoder (4 steps)
             "p50_latency_ms": round(float(np.median(
                 [sum(times[i:i + depth + 1]) for i in range(len(times) - depth)]
                 if args.overlap > 0 and len(times) > depth
@@ -920,11 +937,9 @@ def main():
             "p50_latency_idle_ms": round(float(np.median(idle)) * 1000.0, 2) if idle else None,
             # wall time of the two CU partitions per timed step (HIP events on each side's
             # stream): vocoder + YIN, greedy decoder
-            "side_ms": dict({"vocoder": [round(a, 1) for a, _ in sides],
-                             "decoder": [round(b, 1) for _, b in sides]},
-                            **({"encoder": [round(x, 1) for x in enc_side]} if enc_side else {}))
-            if sides else None,
-            "enc_cus": args.enc_cus if args.stagger == 2 else None,
+            "side_ms": {"vocoder": [round(a, 1) for a, _ in sides],
+                        "decoder": [round(b, 1) for _, b in sides]} if sides else None,
+            "decoder_calls_per_step": calls if args.stagger else 1,
             # staggered step: utterances whose YIN ran on the decoder side in the last timed
             # step (self-balancing split, JanusPipeline._yin_split)
             "yin_dec_utts": yin_dec_utts,
@@ -942,12 +957,20 @@ def main():
                       "fallback_run": bool(args.fallback),
                       "sampled_decodes": int(sum(g[6] for g in enc.gates or []))},
             "stats_gathered": n_stats,
-            # second windows faster-whisper's seek loop would run on the last timed batch
-            # (the first window's seek stops at a timestamp pair short of the clip's
-            # content); counted, not decoded: the pipeline decodes first windows only
+            # faster-whisper's seek loop over every clip (transcriber.py:53-57): the windows
+            # the last timed batch decoded (a first window per clip, then one from the seek
+            # its last timestamp pair left), and clips left short of their content (0)
+            "all_windows": bool(pipe.tuning.all_windows),
+            "windows_decoded": int(sum(windows)),
+            "windows_per_utt": round(float(np.mean(windows)), 3),
             "seek_windows_extra": seek_extra,
-            # the overlapped step with the temperature fallback on (5 temperatures x best_of
-            # 5 re-decodes of every failing window; rank 0's figure, per GPU)
+            # the same staggered step decoding each clip's FIRST window only (the r05 serving
+            # semantics, one decoder call per step), timed after the headline
+            "xrt_first_window": fw["xrt"] if fw else None,
+            "first_window": fw,
+            # the headline step with the temperature fallback on (5 temperatures x best_of
+            # 5 re-decodes of every failing window, every window of the seek loop; rank 0's
+            # figure, per GPU)
             "xrt_with_fallback": fb["xrt"] if fb else None,
             "fallback": fb,
             "host_edges_ms": {"pcm_upload": round(t_up * 1000.0, 1),
@@ -975,10 +998,10 @@ def main():
                 # HBM roofline (algorithmic bytes per position / decoder-side time per
                 # position; launches per position from the captured decode graphs)
                 "decoder": decoder_roofline(
-                    pipe.whisper.cfg, sets * B, dec_positions, dec_launches,
+                    pipe.whisper.cfg, sets * B, (calls if args.stagger else 1) * dec_positions,
+                    (calls if args.stagger else 1) * dec_launches,
                     float(np.mean([b for _, b in sides])) if sides else None,
-                    round(1.0 - cu_share - (args.enc_cus * 8 / n_cus if args.stagger == 2 else 0), 4)
-                    if args.overlap > 0 else 1.0,
+                    round(1.0 - cu_share, 4) if args.overlap > 0 else 1.0,
                     tkv_positions=(sets * dec_positions - 1) if args.stagger else None),
             },
             "cpu_baseline": None,

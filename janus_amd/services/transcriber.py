@@ -223,15 +223,22 @@ def split_window(tk, tokens, seek, segment_size):
 class _Stream:
     """generate_segments state of one utterance."""
 
-    def __init__(self, audio16k):
+    def __init__(self, audio16k=None, content_frames=None):
         self.audio = audio16k
-        self.content_frames = len(audio16k) // HOP
+        self.content_frames = len(audio16k) // HOP if content_frames is None else int(content_frames)
         self.seek = 0
         self.all_tokens = []
         self.prompt_reset_since = 0
         self.segments = []
         self.windows = self.fallbacks = self.skips = 0
         self.fallback_decodes = 0      # sampled decodes (temperature steps) run
+        self.window_tokens = []        # the settled tokens of every window, in order
+        self.window_rows = []          # every window's T = 0 decode: (tokens, avg_logprob, nsp)
+        self.sampled = 0               # tokens sampled at T = 0 over every window (incl. eot)
+
+    def transcript(self):
+        """transcribe_buffer's join of the segments (transcriber.py:59-64)."""
+        return ' '.join(s.text.strip() for s in self.segments).strip()
 
     @property
     def active(self):
@@ -246,11 +253,14 @@ class _Stream:
         return p + list(tk.sot_sequence)
 
 
-def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of, **dec_kw):
+def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of,
+              enc_rows=None, **dec_kw):
     """Run the temperature fallback for the windows of one round: first [Candidate] (T = 0
     results), keys [(utt, window)]; returns each window's settled Candidate. The
     hypotheses of every window still failing at a temperature go out as one sampled batch
-    (chunks of FALLBACK_ROWS rows)."""
+    (chunks of FALLBACK_ROWS rows). ``enc_rows``: window j's encoder output is enc[enc_rows[j]]
+    (default enc[j])."""
+    er = list(range(len(first))) if enc_rows is None else list(enc_rows)
     results = [[c] for c in first]
     final = [settle(r, temperatures) if not r[0].needs_fallback else None for r in results]
     # the shared-encoder PAIR path (H <= 8, d <= 512) reads each window's output in place;
@@ -272,7 +282,7 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
             seeds = [fallback_seed(keys[j][0], keys[j][1], ti, h) for j in js for h in range(best_of)]
             out = engine.decode_ex(enc, prompts=rows_prompts, max_length=max_length,
                                    temperature=T, seeds=seeds,
-                                   enc_index=[j for j in js for _ in range(best_of)], **dec_kw).rows()
+                                   enc_index=[er[j] for j in js for _ in range(best_of)], **dec_kw).rows()
             for k, j in enumerate(js):
                 toks, avg_lp, nsp = best_hypothesis(out[k * best_of:(k + 1) * best_of])
                 results[j].append(candidate(tk, toks, avg_lp, nsp, T))
@@ -280,6 +290,86 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
             if not results[j][-1].needs_fallback or ti == len(temperatures) - 1:
                 final[j] = settle(results[j], temperatures)
     return final, [len(r) - 1 for r in results]
+
+
+def settle_round(engine, tk, rows, prompts, keys, enc, max_length, temperatures=(0.0,),
+                 best_of: int = BEST_OF, enc_rows=None, **dec_kw):
+    """One round of generate_with_fallback: ``rows`` the T = 0 decode of the round's windows
+    ([(tokens, avg_logprob, no_speech_prob)], DecodeOut.rows()), ``prompts`` / ``keys`` [(utt, window)] per window,
+    ``enc`` the windows' encoder output (enc[enc_rows[j]] for window j). Returns (first,
+    final, sampled decodes) per window: the T = 0 Candidate, the settled one, and the number
+    of sampled re-decodes the fallback ran."""
+    first = [candidate(tk, toks, avg_lp, nsp, 0.0) for (toks, avg_lp, nsp) in rows]
+    if len(temperatures) > 1:
+        final, ndec = _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures,
+                                best_of, enc_rows=enc_rows, **dec_kw)
+    else:
+        final, ndec = first, [0] * len(first)
+    return first, final, ndec
+
+
+def advance(tk, s, size, c0, r, nd, sampled: int = 0):
+    """generate_segments' update of one utterance after its window [seek, seek + size) settled
+    (c0: the T = 0 Candidate, r: the settled one, nd: sampled re-decodes, sampled: tokens the
+    T = 0 decode emitted): the counters, the no-speech skip, the segments (start == end or
+    blank text dropped), the next seek and the prompt reset."""
+    s.windows += 1
+    s.fallbacks += int(c0.needs_fallback)
+    s.fallback_decodes += nd
+    s.sampled += int(sampled)
+    s.window_tokens.append(list(r.tokens))
+    s.window_rows.append((list(c0.tokens), c0.avg_logprob, c0.no_speech_prob))
+    # no-speech skip on the settled result (generate_segments after the fallback)
+    if r.no_speech_prob > NO_SPEECH_THRESHOLD and not r.avg_logprob > LOG_PROB_THRESHOLD:
+        s.skips += 1
+        s.seek += size
+        return
+    segs, nseek = split_window(tk, r.tokens, s.seek, size)
+    for (st, en, part) in segs:
+        txt = tk.decode(part)
+        if st == en or not txt.strip():
+            continue
+        s.all_tokens.extend(part)
+        s.segments.append(Segment(len(s.segments), s.seek, st, en, txt, part,
+                                  r.temperature, r.avg_logprob, r.compression_ratio,
+                                  r.no_speech_prob, c0.needs_fallback))
+    s.seek = nseek
+    # condition_on_previous_text: a result settled above prompt_reset_on_temperature
+    # restarts the prompt after these segments
+    if r.temperature > PROMPT_RESET_ON_TEMPERATURE:
+        s.prompt_reset_since = len(s.all_tokens)
+
+
+def gather_windows(items, n_frames: int = N_FRAMES, device=None):
+    """fp16 [len(items)][n_frames][80]: item j = (features [B][F][80] fp16 device tensor, row,
+    seek, size) -> features[row, seek:seek + size] followed by zeros (faster-whisper's
+    ``features[:, seek:seek + segment_size]`` + pad_or_trim). One index gather per distinct
+    features tensor (a serving batch's windows come out of one [B][F][80] tensor)."""
+    if not items:
+        return torch.zeros(0, n_frames, 80, dtype=torch.float16, device=device)
+    dev = items[0][0].device
+    out = torch.zeros(len(items), n_frames, 80, dtype=torch.float16, device=dev)
+    t = torch.arange(n_frames, device=dev)
+    groups = {}
+    for j, (f, row, seek, size) in enumerate(items):
+        groups.setdefault(id(f), (f, []))[1].append((j, int(row), int(seek), int(size)))
+    for f, lst in groups.values():
+        F = f.shape[1]
+        if len(lst) == 1:
+            j, row, seek, size = lst[0]
+            n = max(0, min(size, F - seek, n_frames))
+            if n > 0:
+                out[j, :n] = f[row, seek:seek + n]
+            continue
+        rows = torch.tensor([r for _, r, _, _ in lst], dtype=torch.int64, device=dev)
+        seeks = torch.tensor([s for _, _, s, _ in lst], dtype=torch.int64, device=dev)
+        sizes = torch.tensor([z for _, _, _, z in lst], dtype=torch.int64, device=dev)
+        src = seeks[:, None] + t[None, :]
+        valid = (t[None, :] < sizes[:, None]) & (src < F)
+        g = f[rows[:, None], torch.where(valid, src, 0)]          # [n][n_frames][80]
+        js = torch.tensor([j for j, _, _, _ in lst], dtype=torch.int64, device=dev)
+        out[js] = torch.where(valid[..., None], g, torch.zeros((), dtype=g.dtype, device=dev))
+    return out
 
 
 def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448,
@@ -303,7 +393,7 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
             continue
         pcm = torch.from_numpy(np.concatenate([st.audio, np.zeros(1, np.float32)])).to(dev)
         offs = torch.tensor([0, len(st.audio)], dtype=torch.int64, device=dev)
-        feats.append(engine.logmel_frames(pcm, offs, 1, 1, st.content_frames)[0])
+        feats.append(engine.logmel_frames(pcm, offs, 1, 1, st.content_frames))
     while True:
         act = [i for i, s in enumerate(streams) if s.active]
         if not act:
@@ -312,42 +402,16 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
             idx = act[c0:c0 + max_batch]
             grp = [streams[i] for i in idx]
             sizes = [s.window_size() for s in grp]
-            mel = torch.zeros(len(grp), N_FRAMES, 80, dtype=torch.float16, device=dev)
-            for j, (i, s, size) in enumerate(zip(idx, grp, sizes)):
-                mel[j, :size] = feats[i][s.seek:s.seek + size]      # pad_or_trim: zeros after
+            mel = gather_windows([(feats[i], 0, s.seek, size) for i, s, size in zip(idx, grp, sizes)])
             enc = engine.encode(mel)
             prompts = [s.prompt(tk, max_length) for s in grp]
             out = engine.decode_ex(enc, prompts=prompts, max_length=max_length)
-            first = [candidate(tk, toks, avg_lp, nsp, 0.0) for (toks, avg_lp, nsp) in out.rows()]
             keys = [(i, s.windows) for i, s in zip(idx, grp)]
-            if len(temperatures) > 1:
-                final, ndec = _fallback(engine, tk, enc, prompts, first, keys, max_length,
-                                        temperatures, best_of)
-            else:
-                final, ndec = first, [0] * len(first)
-            for s, size, c0r, r, nd in zip(grp, sizes, first, final, ndec):
-                s.windows += 1
-                s.fallbacks += int(c0r.needs_fallback)
-                s.fallback_decodes += nd
-                # no-speech skip on the settled result (generate_segments after the fallback)
-                if r.no_speech_prob > NO_SPEECH_THRESHOLD and not r.avg_logprob > LOG_PROB_THRESHOLD:
-                    s.skips += 1
-                    s.seek += size
-                    continue
-                segs, nseek = split_window(tk, r.tokens, s.seek, size)
-                for (st, en, part) in segs:
-                    txt = tk.decode(part)
-                    if st == en or not txt.strip():
-                        continue
-                    s.all_tokens.extend(part)
-                    s.segments.append(Segment(len(s.segments), s.seek, st, en, txt, part,
-                                              r.temperature, r.avg_logprob, r.compression_ratio,
-                                              r.no_speech_prob, c0r.needs_fallback))
-                s.seek = nseek
-                # condition_on_previous_text: a result settled above
-                # prompt_reset_on_temperature restarts the prompt after these segments
-                if r.temperature > PROMPT_RESET_ON_TEMPERATURE:
-                    s.prompt_reset_since = len(s.all_tokens)
+            first, final, ndec = settle_round(engine, tk, out.rows(), prompts, keys, enc, max_length,
+                                              temperatures, best_of)
+            n_tok = out.n_tokens.cpu().numpy()
+            for s, size, c0r, r, nd, nt in zip(grp, sizes, first, final, ndec, n_tok):
+                advance(tk, s, size, c0r, r, nd, nt)
     return streams
 
 
@@ -441,6 +505,6 @@ class Transcriber:
 
 
 __all__ = ["Transcriber", "WhisperModel", "Segment", "TranscriptionInfo", "read_wav_16k",
-           "generate_segments", "split_window", "compression_ratio", "gates", "nat",
+           "generate_segments", "settle_round", "advance", "gather_windows", "split_window", "compression_ratio", "gates", "nat",
            "Candidate", "candidate", "best_hypothesis", "settle", "fallback_seed", "TEMPERATURES",
            "BEST_OF"]

@@ -158,6 +158,9 @@ class VocoderEngine:
         nat.call("janus_vocoder_create", ctypes.addressof(c), ctypes.addressof(h))
         self._h = h
         weights = dict(weights if weights is not None else load_weights(cfg, seed))
+        # host copy of what was uploaded: a second context with the same weights (the
+        # staggered step's decoder-side renders) is built from it, never re-derived
+        self.weights = weights
         from .whisper import mel_constants  # the speaker path's log-mel front end
         weights["mel.basis"], weights["mel.filters"] = mel_constants()
         for name, arr in weights.items():

@@ -301,7 +301,8 @@ def fallback_seed(utt, window, temp_index, hyp):
 
 
 def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=True,
-                        temperatures=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0), best_of=5, utt=0):
+                        temperatures=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0), best_of=5, utt=0,
+                        given=None):
     """faster-whisper generate_segments (beam_size=1, every other option at its default)
     over one 16 kHz utterance, restated with this module's log-mel / encoder / decoder,
     including generate_with_fallback: a window failing its gates (compression ratio > 2.4
@@ -311,14 +312,18 @@ def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=
     ratio <= 2.4 (else all) reported at the last temperature; a settled temperature above
     0.5 resets the prompt. ``utt``: the utterance index the noise seeds are keyed on.
     Returns (segments [(start, end, text, tokens)], dict(windows, needs_fallback, skips,
-    fallback_decodes)). The encoder output is rounded to fp16 (``enc_fp16``)."""
+    fallback_decodes, trace = [(seek, size, prompt)] per window)). The encoder output is
+    rounded to fp16 (``enc_fp16``). ``given``: per window (sampled tokens without eot,
+    avg_logprob, no-speech probability) of a decode done elsewhere (T = 0 only) — the loop's
+    seek / prompt / segment bookkeeping restated over another decoder's results, no model
+    run."""
     import zlib
     audio16k = np.asarray(audio16k, np.float32)
     tb = tk.timestamp_begin
     content = len(audio16k) // 160
-    features = logmel(audio16k, 1, filters, n_frames=None)   # the whole clip, once
+    features = logmel(audio16k, 1, filters, n_frames=None) if given is None else None
     seek, all_tokens, segs, reset_since = 0, [], [], 0
-    cnt = dict(windows=0, needs_fallback=0, skips=0, fallback_decodes=0)
+    cnt = dict(windows=0, needs_fallback=0, skips=0, fallback_decodes=0, trace=[])
 
     def judge(r, temp):
         toks = [t for t in r["tokens"] if t != tk.eot]
@@ -333,14 +338,23 @@ def transcribe_segments(audio16k, W, cfg, tk, filters, max_length=448, enc_fp16=
 
     while seek < content:
         size = min(3000, content - seek)
-        mel = window(features, seek)[None]
-        enc = encoder(mel, W, cfg)
-        if enc_fp16:
-            enc = enc.half().float()
         prev = all_tokens[reset_since:]
         prompt = ([tk.sot_prev if hasattr(tk, "sot_prev") else 50360] +
                   prev[-(max_length // 2 - 1):] if prev else []) + list(tk.sot_sequence)
-        r0 = judge(greedy_cached(enc, W, cfg, tk, max_length, prompts=[prompt], no_speech=50361)[0], 0.0)
+        cnt["trace"].append((seek, size, list(prompt)))
+        if given is not None:
+            if cnt["windows"] >= len(given):
+                raise ValueError("given: fewer windows than the seek loop runs")
+            g_toks, g_lp, g_nsp = given[cnt["windows"]]
+            r0 = judge(dict(tokens=list(g_toks), sum_lp=float(g_lp) * (len(g_toks) + 1),
+                            nsp=float(g_nsp)), 0.0)
+            temperatures = (0.0,)
+        else:
+            mel = window(features, seek)[None]
+            enc = encoder(mel, W, cfg)
+            if enc_fp16:
+                enc = enc.half().float()
+            r0 = judge(greedy_cached(enc, W, cfg, tk, max_length, prompts=[prompt], no_speech=50361)[0], 0.0)
         results, final = [r0], (r0 if not r0["needs"] else None)
         for ti in range(1, len(temperatures)):
             if final is not None:

@@ -72,10 +72,12 @@ def test_serving_tuning_from_env():
     the pipeline itself reads no environment."""
     from janus_amd.pipeline import ServingTuning
     t = ServingTuning.from_env({})
-    assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 6
+    assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 0
+    assert t.all_windows and t.calls() == 2 and ServingTuning(all_windows=False).calls() == 1
     t = ServingTuning.from_env({"JANUS_STAGGER_SETS": "3", "JANUS_YIN_DEC_UTTS": "5",
                                 "JANUS_HOST_PREFETCH": "0", "JANUS_YIN_SIDE": "beside",
-                                "JANUS_OTHER": "1"})
+                                "JANUS_OTHER": "1", "JANUS_ALL_WINDOWS": "0"})
     assert (t.stagger_sets, t.yin_dec_utts, t.host_prefetch, t.yin_side) == (3, 5, False, "beside")
+    assert not t.all_windows and t.calls() == 1
     src = open(os.path.join(os.path.dirname(__file__), "..", "janus_amd", "pipeline.py")).read()
     assert "os.environ.get(" not in src

@@ -101,41 +101,57 @@ def test_overlapped_step_matches_sequential(gpu, yin_dec):
         assert torch.equal(pcm16, seq[i][2])
 
 
+def _batch(gpu, seeds_secs):
+    utts = [synth_speech(sd, sec) for sd, sec in seeds_secs]
+    lengths = [len(u) for u in utts]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
+    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+    return utts, pcm, offs, lengths
+
+
+def _same_streams(a, b):
+    """Two seek-loop states equal: windows, counters, every window's settled tokens and
+    every segment (times, text, tokens)."""
+    assert a.windows == b.windows and a.seek == b.seek
+    assert (a.fallbacks, a.skips, a.fallback_decodes) == (b.fallbacks, b.skips, b.fallback_decodes)
+    assert a.window_tokens == b.window_tokens
+    assert [(g.seek, g.start, g.end, g.text, g.tokens) for g in a.segments] == \
+        [(g.seek, g.start, g.end, g.text, g.tokens) for g in b.segments]
+
+
 @pytest.mark.parametrize("sets,voc_dec", [(2, 0), (3, 0), (4, 0), (2, 1), (2, 3)])
 def test_staggered_step_matches_sequential(gpu, sets, voc_dec):
-    """The continuous-batching serving step (step_staggered: the decoder advances batch i's
-    rows from position 0 and batch i-m's from position mS, m < N, in one call, N·B rows;
-    N = tuning.stagger_sets) produces, per batch and N steps later, the same packets and
-    waveforms as the back-to-back step of that batch alone; flush_staggered drains. With
-    tuning.voc_dec_utts = k the batch's last k packets render on the decoder's CUs through a
-    second vocoder context: the waveforms are still bit-identical, in packet order."""
+    """The continuous-batching serving step (step_staggered: windows enter N slot sets of B
+    rows as fresh rows — each batch's first windows, then its clips' continuation windows from
+    the seek the previous window ended at — and every decoder call advances all sets;
+    N = tuning.stagger_sets) produces, per batch and in order, the same seek loops (windows,
+    tokens, segments), packets and waveforms as the back-to-back step of that batch alone;
+    flush_staggered drains. With tuning.voc_dec_utts = k the batch's last k packets render on
+    the decoder's CUs through a second vocoder context: the waveforms are still
+    bit-identical, in packet order."""
     pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,),
                          tuning=ServingTuning(stagger_sets=sets, voc_dec_utts=voc_dec))
-    batches = []
-    for i in range(3):
-        utts = [synth_speech(700 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]
-        lengths = [len(u) for u in utts]
-        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
-        pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
-        batches.append((pcm, offs, lengths))
+    batches = [_batch(gpu, [(700 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)])[1:] for i in range(3)]
     frames = 16
     seq = []
     for pcm, offs, lengths in batches:
         enc = pipe.encode(pcm, offs, lengths, timestamp=5.0)
         wav, pcm16, _ = pipe.decode(enc.packets, frames)
-        seq.append((enc.packets, wav, pcm16, enc.tokens.cpu()))
+        seq.append((enc, wav, pcm16))
     outs = [pipe.step_staggered(pcm, offs, lengths, frames, 16, timestamp=5.0)
             for pcm, offs, lengths in batches]
-    n = int(sets)
-    assert all(o == (None, None, None) for o in outs[:n])
+    assert outs[0] == (None, None, None)
     done = [o for o in outs if o[0] is not None] + pipe.flush_staggered(frames)
     assert len(done) == 3
     for i, (res, wav, pcm16) in enumerate(done):
-        assert res.packets == seq[i][0], i
-        n = res.n_tokens.cpu()
-        for j in range(len(n)):
-            k = 1 + int(n[j])
-            assert torch.equal(res.tokens.cpu()[j, :k], seq[i][3][j, :k])
+        ref = seq[i][0]
+        assert res.packets == ref.packets, i
+        for a, b in zip(res.streams, ref.streams):
+            _same_streams(a, b)
+        assert torch.equal(res.n_tokens, ref.n_tokens)
+        for j in range(len(res.n_tokens)):
+            k = 1 + int(res.n_tokens[j])
+            assert torch.equal(res.tokens[j, :k], ref.tokens[j, :k])
         if seq[i][1] is None:
             assert wav is None
             continue
@@ -143,67 +159,77 @@ def test_staggered_step_matches_sequential(gpu, sets, voc_dec):
         assert torch.equal(pcm16, seq[i][2])
 
 
-def test_pipelined_step_matches_sequential(gpu):
-    """The three-lane serving step (step_pipelined: encoder of batch i on its own CU lane,
-    the continuous-batch decoder of batches i-1 / i-2 and the vocoder of batch i-3 beside
-    it) produces, per batch and three steps later, the same packets, tokens and waveforms
-    as the back-to-back step of that batch alone; flush_pipelined drains the rest."""
+def test_staggered_windows_match_seek_loop(gpu):
+    """Clips of several windows (5 s, 35 s, 70 s at max_length 24: one, two and three or more
+    windows of faster-whisper's seek loop) through the staggered step, batch after batch:
+    every clip's seek loop — windows, seeks, <|startofprev|> prompts, segments, transcript —
+    equals the drop-in's generate_segments on the same 16 kHz audio (transcriber.py:53-64),
+    and the packet is the JanusPacket of that transcript. The continuation windows of
+    different batches share decoder groups (the queue), so batches finish in order only
+    after their last clip's last window."""
+    from janus_amd.services.transcriber import generate_segments
     pipe = JanusPipeline("tiny.en", max_length=24, temperatures=(0.0,))
-    batches = []
-    for i in range(4):
-        utts = [synth_speech(900 + 10 * i + k, 1.5 + 0.5 * k) for k in range(3)]
-        lengths = [len(u) for u in utts]
-        offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
-        pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
-        batches.append((pcm, offs, lengths))
-    frames = 16
-    seq = []
-    for pcm, offs, lengths in batches:
-        enc = pipe.encode(pcm, offs, lengths, timestamp=5.0)
-        wav, pcm16, _ = pipe.decode(enc.packets, frames)
-        seq.append((enc.packets, wav, pcm16, enc.tokens.cpu()))
-    outs = [pipe.step_pipelined(pcm, offs, lengths, frames, 16, 4, timestamp=5.0)
-            for pcm, offs, lengths in batches]
-    assert all(o == (None, None, None) for o in outs[:3])
-    done = [outs[3]] + pipe.flush_pipelined(frames)
-    assert len(done) == 4
-    for i, (res, wav, pcm16) in enumerate(done):
-        assert res.packets == seq[i][0], i
-        n = res.n_tokens.cpu()
-        for j in range(len(n)):
-            k = 1 + int(n[j])
-            assert torch.equal(res.tokens.cpu()[j, :k], seq[i][3][j, :k])
-        if seq[i][1] is None:
-            assert wav is None
-            continue
-        torch.testing.assert_close(wav, seq[i][1], rtol=0, atol=0)
-        assert torch.equal(pcm16, seq[i][2])
+    specs = [[(1100 + 10 * i, 5.0), (1101 + 10 * i, 35.0), (1102 + 10 * i, 70.0)] for i in range(2)]
+    batches = [_batch(gpu, sp) for sp in specs]
+    frames = 8
+    got = []
+    for utts, pcm, offs, lengths in batches:
+        r = pipe.step_staggered(pcm, offs, lengths, frames, 16, timestamp=7.0)
+        if r[0] is not None:
+            got.append(r)
+    got += pipe.flush_staggered(frames)
+    assert len(got) == 2
+    for (utts, pcm, offs, lengths), (res, wav, _) in zip(batches, got):
+        ref = generate_segments(pipe.whisper, [np.ascontiguousarray(u[::3]) for u in utts],
+                                max_length=24, temperatures=(0.0,))
+        assert [s.windows for s in ref][2] >= 3
+        for b, (a, r) in enumerate(zip(res.streams, ref)):
+            _same_streams(a, r)
+            text = r.transcript()
+            assert res.texts[b] == text
+            tags = OracleProsody(48000).analyze_buffer(utts[b])[0]
+            assert res.packets[b] == (opk.serialize(text, 0, tags, "auto", 7.0) if text.strip() else None)
+
+
+def test_voc_dec_explicit_weights(gpu):
+    """The staggered step's second vocoder context renders with the primary engine's own
+    weights: a pipeline built with explicit (non-seeded, not from JANUS_VOCODER_DIR)
+    vocoder weights gives bit-identical waveforms with voc_dec_utts = 2 and = 0."""
+    from janus_amd import vocoder as jv
+    W = jv.synthetic_weights(jv.FireflyConfig(), seed=1234)
+    W = {k: (v * 1.01).astype(np.float32) if k.endswith("weight") else v for k, v in W.items()}
+    out = {}
+    for kv in (0, 2):
+        pipe = JanusPipeline("tiny.en", max_length=12, temperatures=(0.0,), vocoder_weights=W,
+                             tuning=ServingTuning(voc_dec_utts=kv))
+        _, pcm, offs, lengths = _batch(gpu, [(1300 + k, 1.0 + 0.5 * k) for k in range(3)])
+        r = [pipe.step_staggered(pcm, offs, lengths, 8, 16, timestamp=1.0)]
+        r += pipe.flush_staggered(8)
+        out[kv] = [x for x in r if x[0] is not None]
+    assert len(out[0]) == len(out[2]) == 1
+    torch.testing.assert_close(out[2][0][1], out[0][0][1], rtol=0, atol=0)
+    assert torch.equal(out[2][0][2], out[0][0][2])
 
 
 def test_pipeline_fallback_matches_seek_loop(gpu):
     """The batched pipeline with faster-whisper's fallback (temperatures 0 ... 1.0, best_of
     5: every window of the seeded synthetic model fails at T = 0) settles each utterance
     exactly as the drop-in seek loop (generate_segments) does on the same 16 kHz audio:
-    same avg_logprob, temperature, number of sampled decodes and seek after the window;
-    the overlapped serving step (re-decodes on the decoder's CU partition) and the
-    staggered (continuous-batching) step — whose failing windows leave the continuous
-    batch and re-decode on the whole GPU in decoder state slot 1 — give the same
-    packets, batch after batch."""
+    same windows, tokens, segments, temperatures and sampled decodes; the overlapped
+    serving step and the staggered (continuous-batching) step — whose completed windows
+    that fail their gates re-decode on the whole GPU in decoder state slot 1 before their
+    clips' continuation windows are queued — give the same packets, batch after batch."""
     from janus_amd.services.transcriber import TEMPERATURES, generate_segments
     pipe = JanusPipeline("tiny.en", max_length=12, temperatures=TEMPERATURES)
-    utts = [synth_speech(500 + k, 2.0 + 3 * k) for k in range(3)]
-    lengths = [len(u) for u in utts]
-    offs = torch.tensor(np.concatenate([[0], np.cumsum(lengths)]), dtype=torch.int64, device=gpu)
-    pcm = torch.from_numpy(np.concatenate(utts + [np.zeros(1, np.float32)])).to(gpu)
+    utts, pcm, offs, lengths = _batch(gpu, [(500 + k, 2.0 + 3 * k) for k in range(3)])
     res = pipe.encode(pcm, offs, lengths, timestamp=5.0)
     streams = generate_segments(pipe.whisper, [np.ascontiguousarray(u[::3]) for u in utts],
                                 max_length=12)
     for b, st in enumerate(streams):
         needs0, skip, avg, cr, nsp, temp, ndec, seek = res.gates[b]
-        assert st.windows == 1 and needs0 and ndec == st.fallback_decodes == 5
-        assert seek >= min(3000, len(utts[b][::3]) // 160)   # one window: its seek ends the clip
-        if st.segments:
-            assert st.segments[0].avg_logprob == avg and st.segments[0].temperature == temp == 1.0
+        assert needs0 and ndec == 5
+        _same_streams(res.streams[b], st)
+        assert res.texts[b] == st.transcript()
     outs = [pipe.step_overlapped(pcm, offs, lengths, 16, 16, timestamp=5.0)]
     outs.append(pipe.flush(16))
     assert outs[1][0].packets == res.packets
