@@ -4,14 +4,19 @@ Workload (BASELINE.json metric "xRT (audio-s/wall-s) per GPU, 30s clips batch=64
 per GPU, 64 seeded synthetic 30 s utterances at 48 kHz (janus_amd/workload.py) already
 resident in HBM. One step = the whole batch through
   encode: log-mel([::3]) -> Whisper base.en encoder -> greedy decoder (<= 448 tokens,
-          timestamp rules) -> detokenize -> YIN + RMS prosody -> MessagePack packets
+          timestamp rules) over EVERY window of faster-whisper's seek loop
+          (transcriber.py:53-57: the first 30 s window, then a window from the seek its
+          last timestamp pair left, with the <|startofprev|> prompt) -> segments joined
+          -> YIN + RMS prosody -> MessagePack packets
   decode: unpack -> "(emotion) text" prompt -> front end -> Firefly-GAN vocoder
           (30 s = 2584 latent frames -> 1 323 008 samples @ 44.1 kHz, f32 + int16)
-Default (--overlap 16): the steady-state serving pipeline — each step encodes batch i
-and renders the packets of batch i-1, so every timed step carries one full encode and
-one full decode of 64 utterances (a warm-up step primes it). After the encoder, the
-greedy decoder runs on 16 CUs of each XCD and the vocoder + YIN on the other 16
-(CU-masked streams). --overlap 0 runs encode and decode of one batch back to back.
+Default (--stagger 1): the steady-state serving pipeline (JanusPipeline.step_staggered):
+each step encodes batch i, runs ONE decoder call of 2 slot sets x 128 rows (a set takes
+batch i's first windows together with an earlier batch's continuation windows; each set
+advances 224 positions per call, a window completes in two calls) on 16 CUs of each XCD,
+and renders the batch whose windows all settled on the other 16 (CU-masked streams);
+every timed step takes in, decodes and renders 64 utterances' worth of windows (128 on
+the synthetic weights). --stagger 0: the overlapped step; --overlap 0: back to back.
 Weights are seeded synthetic tensors of the real shapes (no checkpoints offline).
 Multi-GPU: one process per GPU, utterances sharded with no data-path collective; packet
 bytes are all-gathered once after the timed steps (RCCL over xGMI).
@@ -75,6 +80,9 @@ def parse():
     ap.add_argument("--stream-async", type=int, default=1,
                     help="config 5: 1 = encode + render on a worker stream while the next "
                          "blocks are ingested (StreamingEncoder(asynchronous=True))")
+    ap.add_argument("--stream-t0", action="store_true",
+                    help="config 5: decode at T = 0 only (default: faster-whisper's temperature "
+                         "fallback, as the reference's transcribe_buffer runs it)")
     ap.add_argument("--duplex", type=int, default=1,
                     help="config 5: render every packet through the receiver's vocoder")
     ap.add_argument("--launch-check", action="store_true",
@@ -551,11 +559,13 @@ def run_config5(args, rank, world, use_dist, dev):
     audio = np.stack([channel_audio(s, total) for s in mine])
     S = len(mine)
     w = WhisperEngine(CONFIGS[args.model], seed=0)
-    temps = TEMPERATURES if args.fallback else (0.0,)
+    # the reference's decode semantics by default (transcribe_buffer -> transcribe with
+    # faster-whisper's temperature fallback, engine.py:510-527); --stream-t0: T = 0 only
+    temps = (0.0,) if args.stream_t0 else TEMPERATURES
     rx = None
     if args.duplex:
-        from janus_amd.pipeline import JanusPipeline
-        rx = JanusPipeline(args.model, max_length=8)   # its vocoder renders the far end
+        from janus_amd.pipeline import PacketRenderer
+        rx = PacketRenderer()   # the far end's vocoder alone (no second Whisper engine)
     enc = StreamingEncoder(S, w, max_length=args.max_length, asynchronous=bool(args.stream_async),
                            receiver=rx, temperatures=temps)
     # warm-up: one block of speech + silence on a scratch encoder (graph capture, allocations)
@@ -619,7 +629,8 @@ def run_config5(args, rank, world, use_dist, dev):
            "worker_max_queue": int(counts[1]), "wall_s": round(t_total, 2),
            "audio_s": round(n_blocks * args.block_ms / 1000.0, 2),
            "realtime": bool(p99 < args.block_ms and pp99 < args.block_ms),
-           "fallback": bool(args.fallback), "extra_seek_windows": int(counts[2]),
+           "fallback": not args.stream_t0, "temperatures": list(temps),
+           "extra_seek_windows": int(counts[2]),
            "roofline": None,
            "roofline_note": "real-time arrival: per-phrase batches of a few 1.5-6 s phrases, "
                             "latency-bound; the kernels' rooflines are the config-4 line's",

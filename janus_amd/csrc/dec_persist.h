@@ -7,7 +7,7 @@
 namespace janus {
 
 struct DecSegArgs {
-  int B, MT;                 // rows (<= 128), 16-row tiles (power of two >= B / 16)
+  int B, MT;                 // rows (<= 256), 16-row tiles (power of two >= B / 16)
   float* x;                  // [B][512] fp32 residual stream (read-modify-write)
   // segment A: x += o Wo^T + bo; xqk = LN2(x) Wqk^T + bqk
   const _Float16* o; const _Float16* wo; const float* bo;
@@ -45,11 +45,14 @@ struct DecSegNext {
   const _Float16* wqk; const float* bqk;
 };
 
-// 16-row tiles for B rows (0: unsupported, B > 128)
+// 16-row tiles for B rows (0: unsupported, B > 256)
 int dec_seg_mtiles(int B);
 // blocks of the resident grid on a partition of `cus` CUs (0: unsupported)
 int dec_seg_grid(int B, int cus);
 bool dec_seg_supported(int d, int H, int B, int cus);
+// the resident grid fits: blocks per CU (occupancy of the segment kernels with their LDS)
+// times the partition's CUs cover `grid`
+bool dec_seg_resident(int grid, int cus);
 void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s);
 void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s);
 // segment B of layer l (b: its args, with layer l + 1's QKV weights and cache), the

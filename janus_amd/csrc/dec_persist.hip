@@ -96,6 +96,14 @@ __device__ __forceinline__ float4 as_f4(u32x4v v) { return __builtin_bit_cast(fl
 #define SEG_END(ST) do { (void)(ST); } while (0)
 #endif
 
+// Memory-model invariant (the barrier itself carries no acquire / release fence, which on
+// gfx950 would write back and invalidate the L2 at every barrier): EVERY byte handed off
+// between phases is stored with st_sc1 / st_sc1_8 and loaded with ld_sc1 (or the sc1
+// arguments of the raw buffer builtins), so it goes to and comes from the coherent level
+// whatever XCD the other block ran on; the s_waitcnt vmcnt(0) below retires the stores
+// before the arrival, and the asm memory clobbers keep the compiler from moving loads above
+// the poll. A phase that reads a handed-off buffer with a plain load would see stale L2 data
+// from another XCD: new phases must use ld_sc1 for such reads.
 __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned epoch, unsigned* err,
                                              long long* st = nullptr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -535,17 +543,29 @@ __device__ __forceinline__ void splitk8_pair(const _Float16* wt, int pair, int M
   }
 }
 
-// one pair per block: the grid always has at least 16 * MT blocks (dec_seg_grid)
-template <int KSW, int EPI, bool GROUP, class Pre>
+// one pair per block while the grid has at least 16 * MT blocks; two (pairs b and b + G)
+// at MT = 16 on a 128-block grid (dec_seg_grid): the second pair's weights are issued right
+// after the first pair's MFMAs (its pre()), in flight during the first pair's reduction and
+// epilogue. Each tile's arithmetic is the one-pair form's, so a row's result does not depend
+// on how many rows the call carries.
+template <int KSW, int EPI, bool GROUP, bool BIG, class Pre>
 __device__ __forceinline__ void splitk_phase(const SplitW<KSW>& W, const _Float16* wt, int K,
                                              int MT, __amdgpu_buffer_rsrc_t ra, int lda,
                                              const float* bias, __amdgpu_buffer_rsrc_t rx,
                                              __amdgpu_buffer_rsrc_t ro, float* red, int lane, int wv,
                                              Pre&& pre, long long* st = nullptr, int si = 0) {
-  const int p0 = blockIdx.x;
-  if (p0 >= 16 * MT) { pre(); return; }  // 32 column tiles x MT row tiles / 2
-  splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre, st, si);
-  (void)wt;
+  const int P = 16 * MT;  // 32 column tiles x MT row tiles / 2
+  const int p0 = blockIdx.x, p1 = p0 + (int)gridDim.x;
+  if (p0 >= P) { pre(); return; }
+  if (!BIG || p1 >= P) {
+    splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre, st, si);
+    return;
+  }
+  if constexpr (!BIG) return;
+  SplitW<KSW> W2;
+  splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true,
+                               [&] { splitk_prefetch<KSW>(W2, wt, K, p1, MT, lane, wv); }, st, si);
+  splitk_pair<KSW, EPI, GROUP>(W2, p1, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre, st, si);
 }
 
 }  // namespace
@@ -581,6 +601,7 @@ __device__ __forceinline__ long long* seg_stamps(long long* prof, int k) {
 // Segment A after barrier epoch e0: x += o Wo^T + bo | barrier e0 + 1 | xqk = LN2(x) Wqk^T +
 // bqk. touched: the previous phase's L2 touch (folded into sink here, after the barrier that
 // ended that phase); pst: in-phase stamps (stand-alone kernels only).
+template <bool BIG>
 __device__ __forceinline__ void seg_a_body(const DecSegArgs& a, float* seg_smem, long long* st,
                                            long long* pst, unsigned e0, uint32_t& touched,
                                            uint32_t& sink) {
@@ -593,14 +614,14 @@ __device__ __forceinline__ void seg_a_body(const DecSegArgs& a, float* seg_smem,
   const bool first = (int)blockIdx.x < 16 * MT;
   // the qk projection (N = 8d) at two m-tiles per block where one would leave a wave two
   // weight tiles in a row (dec_seg_mb2): one weight round trip instead of two
-  const bool mb2 = dec_seg_mb2(8 * kD, MT);
+  const bool mb2 = BIG || dec_seg_mb2(8 * kD, MT);
   sink ^= touched;
   touched = mb2 ? touch_lng<2>(a.wqk, 8 * kD, MT) : touch_lng<1>(a.wqk, 8 * kD, MT);
   // phase 1: x += o Wo^T + bo (o from the self-attention launch / phase)
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.wo, kD, blockIdx.x, MT, lane, wv);
-    splitk_phase<4, SE_RESID, false>(w, a.wo, kD, MT, rsrc(a.o, (uint32_t)B * kD * 2), kD, a.bo, rx, rx,
+    splitk_phase<4, SE_RESID, false, BIG>(w, a.wo, kD, MT, rsrc(a.o, (uint32_t)B * kD * 2), kD, a.bo, rx, rx,
                                      red, lane, wv, [] {}, pst, 18);
   }
   grid_barrier(a.bar, e0 + 1, a.err, st);
@@ -619,6 +640,7 @@ __device__ __forceinline__ void seg_a_body(const DecSegArgs& a, float* seg_smem,
 
 // Segment B after barrier epoch e0 (phases 1-4, barriers e0 + 1 .. e0 + 3, and with the next
 // layer's weights phase 5 behind barrier e0 + 4).
+template <bool BIG>
 __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem, long long* st,
                                            long long* pst, unsigned e0, uint32_t& touched,
                                            uint32_t& sink) {
@@ -636,17 +658,17 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.wv, kD, blockIdx.x, MT, lane, wv);
-    splitk_phase<4, SE_F16_SC1, true>(w, a.wv, kD, MT, rsrc(a.xc, (uint32_t)B * 8 * kD * 2), 8 * kD, a.bv,
+    splitk_phase<4, SE_F16_SC1, true, BIG>(w, a.wv, kD, MT, rsrc(a.xc, (uint32_t)B * 8 * kD * 2), 8 * kD, a.bv,
                                       rx, rom, red, lane, wv, [] {}, pst, 18);
   }
   grid_barrier(a.bar, e0 + 1, a.err, st);
   sink ^= touched;
-  touched = touch_lng(a.w1, 4 * kD, MT);
+  touched = BIG ? touch_lng<2>(a.w1, 4 * kD, MT) : touch_lng<1>(a.w1, 4 * kD, MT);
   // phase 2: x += o' Wo_c^T + bo_c
   {
     SplitW<4> w;
     if (first) splitk_prefetch<4>(w, a.woc, kD, blockIdx.x, MT, lane, wv);
-    splitk_phase<4, SE_RESID, false>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {}, pst, 21);
+    splitk_phase<4, SE_RESID, false, BIG>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {}, pst, 21);
   }
   grid_barrier(a.bar, e0 + 2, a.err, st);
   sink ^= touched;
@@ -655,20 +677,30 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   {
     LngW w;
     LngOut o{a.f, 4 * kD, nullptr, nullptr, 0, 0, nullptr};
-    lng_phase<LE_GELU_SC1>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {}, pst, 24);
+    if constexpr (BIG)
+      lng_phase<LE_GELU_SC1, 2>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {}, pst, 24);
+    else
+      lng_phase<LE_GELU_SC1>(w, a.w1, 4 * kD, MT, B, rx, a.ln3g, a.ln3b, a.b1, o, sA, patch, lane, wv, [] {}, pst, 24);
   }
   grid_barrier(a.bar, e0 + 3, a.err, st);
   sink ^= touched;
-  touched = a.wqkv ? touch_lng(a.wqkv, 3 * kD, MT) : 0u;
+  touched = !a.wqkv ? 0u : BIG ? touch_lng<2>(a.wqkv, 3 * kD, MT) : touch_lng<1>(a.wqkv, 3 * kD, MT);
   // phase 4: x += f W2^T + b2 (K = 4d: eighths of K shared by the pair's two tiles, or
   // 16 k-steps per quarter when the pair spans two column tiles, MT = 1)
   if (MT % 2 == 0) {
-    if (first)
+    if constexpr (BIG) {
+      // two pairs per block (MT = 16 on a 128-block grid): the reduction tile is reused
+      for (int p = blockIdx.x; p < 16 * MT; p += gridDim.x) {
+        if (p != (int)blockIdx.x) __syncthreads();
+        splitk8_pair(a.w2, p, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
+      }
+    } else if (first) {
       splitk8_pair(a.w2, blockIdx.x, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
+    }
   } else {
     SplitW<16> w;
     if (first) splitk_prefetch<16>(w, a.w2, 4 * kD, blockIdx.x, MT, lane, wv);
-    splitk_phase<16, SE_RESID, false>(w, a.w2, 4 * kD, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), 4 * kD, a.b2,
+    splitk_phase<16, SE_RESID, false, false>(w, a.w2, 4 * kD, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), 4 * kD, a.b2,
                                       rx, rx, red, lane, wv, [] {}, pst, 27);
   }
   // phase 5 (all but the last layer): the next layer's q and K/V cache rows (write-through)
@@ -678,7 +710,10 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
     touched = 0u;
     LngW w;
     LngOut o{a.qkv, 3 * kD, a.kc, a.vc, a.pos, a.n_ctx, a.roff};
-    lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, pst, 30);
+    if constexpr (BIG)
+      lng_phase<LE_QKV, 2>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, pst, 30);
+    else
+      lng_phase<LE_QKV>(w, a.wqkv, 3 * kD, MT, B, rx, a.ln1g, a.ln1b, a.bqkv, o, sA, patch, lane, wv, [] {}, pst, 30);
   } else if (a.fin_out) {
     // phase 5 of the last layer: the decoder's final LayerNorm, one wave per row, with
     // layernorm_kernel's arithmetic (ln_sum4 / ln_sq4 / ln_norm4, butterfly sums), x read
@@ -826,10 +861,8 @@ __device__ __forceinline__ void attn_store(const DecSegArgs& g, int b, int h, co
 // — and each finishes its first-part row with the partner's second part through LDS.
 __device__ __forceinline__ int attn_split(int n) { return min(n, 64 * ((n + 127) / 128)); }
 
-__device__ __forceinline__ void attn_phase(const DecSegArgs& g, float* lds, int lane, int wv) {
+__device__ __forceinline__ void attn_block(const DecSegArgs& g, float* lds, int lane, int wv, int j) {
   const int B = g.B, H2 = (B + 1) >> 1;
-  const int j = blockIdx.x;
-  if (j >= 2 * H2) return;  // block-uniform
   const int p = j % H2;
   const int h = (j >= H2 ? 4 : 0) + (wv & 3);
   const bool hasb = p + H2 < B;
@@ -880,39 +913,66 @@ __device__ __forceinline__ void attn_phase(const DecSegArgs& g, float* lds, int 
   }
 }
 
+// blocks j < 2 ceil(B / 2); at 256 rows on a 128-block grid each block takes j and j + G (the
+// LDS hand-off slots are reused: a barrier between the two)
+template <bool BIG>
+__device__ __forceinline__ void attn_phase(const DecSegArgs& g, float* lds, int lane, int wv) {
+  const int n = 2 * ((g.B + 1) >> 1);
+  if constexpr (!BIG) {
+    if ((int)blockIdx.x < n) attn_block(g, lds, lane, wv, blockIdx.x);  // block-uniform
+  } else {
+    for (int j = blockIdx.x; j < n; j += gridDim.x) {  // block-uniform
+      if (j != (int)blockIdx.x) __syncthreads();
+      attn_block(g, lds, lane, wv, j);
+    }
+  }
+}
+
 // Cross-attention phase (layer / head kernel, after segment A): block b takes row b with
 // xattn_kernel's one-split body (xattn_body.h), its query rows read sc1 (written by this
 // launch's segment A), c written to xc for the next launch's segment B.
 constexpr int kXattnLds = XGeo<kD, 64>::LDS;
+template <bool BIG>
 __device__ __forceinline__ void xattn_phase(const DecSegArgs& g, float* lds) {
-  const int b = blockIdx.x;
-  if (b >= g.B) return;  // block-uniform
-  xattn_body<kD, 64, false, true, false, true>(g.xqk, g.enc, g.Te, 8, (g.Te + 63) / 64 * 64, nullptr, nullptr,
-                                               nullptr, const_cast<_Float16*>(g.xc), 0, 1, b,
-                                               reinterpret_cast<_Float16*>(lds));
+  if constexpr (!BIG) {
+    const int b = blockIdx.x;
+    if (b >= g.B) return;  // block-uniform
+    xattn_body<kD, 64, false, true, false, true>(g.xqk, g.enc, g.Te, 8, (g.Te + 63) / 64 * 64, nullptr, nullptr,
+                                                 nullptr, const_cast<_Float16*>(g.xc), 0, 1, b,
+                                                 reinterpret_cast<_Float16*>(lds));
+  } else {
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {  // block-uniform
+      if (b != (int)blockIdx.x) __syncthreads();
+      xattn_body<kD, 64, false, true, false, true>(g.xqk, g.enc, g.Te, 8, (g.Te + 63) / 64 * 64, nullptr, nullptr,
+                                                   nullptr, const_cast<_Float16*>(g.xc), 0, 1, b,
+                                                   reinterpret_cast<_Float16*>(lds));
+    }
+  }
 }
 
 // the touched dwords feed a store no reader looks at (word 150 of the counter block is
 // unused), taken with probability 2^-32: the loads cannot be dropped
 #define SEG_SINK(A, T, S) do { if (((S) ^ (T)) == 0x5eed5eedu) (A).bar[150] = 1u; } while (0)
 
+template <bool BIG>
 __global__ __launch_bounds__(kNT, 4) void dec_seg_a_kernel(DecSegArgs a) {
   JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(a.prof, 0);
   uint32_t touched = 0u, sink = 0u;
-  seg_a_body(a, seg_smem, st, st, 0, touched, sink);
+  seg_a_body<BIG>(a, seg_smem, st, st, 0, touched, sink);
   SEG_SINK(a, touched, sink);
   SEG_END(st);
   grid_exit(a.bar);
 }
 
+template <bool BIG>
 __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
   JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(a.prof, 1);
   uint32_t touched = 0u, sink = 0u;
-  seg_b_body(a, seg_smem, st, st, 0, touched, sink);
+  seg_b_body<BIG>(a, seg_smem, st, st, 0, touched, sink);
   SEG_SINK(a, touched, sink);
   SEG_END(st);
   grid_exit(a.bar);
@@ -921,24 +981,25 @@ __global__ __launch_bounds__(kNT, 4) void dec_seg_b_kernel(DecSegArgs a) {
 // One launch per layer step (r05): segment B of layer l (its phase 5 writes layer l + 1's q
 // and K/V rows write-through) | barrier 5 | the self-attention of layer l + 1 | barrier 6 |
 // segment A of layer l + 1 — the launches between two cross-attentions as one grid.
+template <bool BIG>
 __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSegNext nx) {
   JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
   long long* st = seg_stamps(bsg.prof, 2);
   const int lane = threadIdx.x & 63, wv = wave_id();
   uint32_t touched = 0u, sink = 0u;
-  seg_b_body(bsg, seg_smem, st, nullptr, 0, touched, sink);
+  seg_b_body<BIG>(bsg, seg_smem, st, nullptr, 0, touched, sink);
   grid_barrier(bsg.bar, 5, bsg.err, st);
   sink ^= touched;
   touched = touch_splitk(nx.wo, kD, bsg.MT);
-  attn_phase(bsg, seg_smem, lane, wv);
+  attn_phase<BIG>(bsg, seg_smem, lane, wv);
   grid_barrier(bsg.bar, 6, bsg.err, st);
   DecSegArgs asg = bsg;
   asg.wo = nx.wo; asg.bo = nx.bo; asg.ln2g = nx.ln2g; asg.ln2b = nx.ln2b; asg.wqk = nx.wqk; asg.bqk = nx.bqk;
-  seg_a_body(asg, seg_smem, st, nullptr, 6, touched, sink);
+  seg_a_body<BIG>(asg, seg_smem, st, nullptr, 6, touched, sink);
   if (bsg.enc) {
     grid_barrier(bsg.bar, 8, bsg.err, st);
-    xattn_phase(asg, seg_smem);
+    xattn_phase<BIG>(asg, seg_smem);
   }
   SEG_SINK(bsg, touched, sink);
   SEG_END(st);
@@ -948,6 +1009,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
 // Layer 0's head: the QKV projection of layer 0 (segment B's phase 5 over the embedded
 // rows) | barrier 1 | the self-attention | barrier 2 | segment A of layer 0 — the three
 // launches before the first cross-attention as one grid.
+template <bool BIG>
 __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
   JANUS_DEC_WAVE_PRIO();
   extern __shared__ __attribute__((aligned(16))) float seg_smem[];
@@ -959,17 +1021,22 @@ __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
     float* patch = reinterpret_cast<float*>(sA + kSegRows * kAP);
     LngW w;
     LngOut o{g.qkv, 3 * kD, g.kc, g.vc, g.pos, g.n_ctx, g.roff};
-    lng_phase<LE_QKV>(w, g.wqkv, 3 * kD, g.MT, g.B, rsrc(g.x, (uint32_t)g.B * kD * 4), g.ln1g, g.ln1b,
-                      g.bqkv, o, sA, patch, lane, wv, [] {}, nullptr, 30);
+    const auto rx0 = rsrc(g.x, (uint32_t)g.B * kD * 4);
+    if constexpr (BIG)
+      lng_phase<LE_QKV, 2>(w, g.wqkv, 3 * kD, g.MT, g.B, rx0, g.ln1g, g.ln1b, g.bqkv, o, sA, patch, lane, wv,
+                           [] {}, nullptr, 30);
+    else
+      lng_phase<LE_QKV>(w, g.wqkv, 3 * kD, g.MT, g.B, rx0, g.ln1g, g.ln1b, g.bqkv, o, sA, patch, lane, wv,
+                        [] {}, nullptr, 30);
   }
   grid_barrier(g.bar, 1, g.err, st);
   touched = touch_splitk(g.wo, kD, g.MT);
-  attn_phase(g, seg_smem, lane, wv);
+  attn_phase<BIG>(g, seg_smem, lane, wv);
   grid_barrier(g.bar, 2, g.err, st);
-  seg_a_body(g, seg_smem, st, nullptr, 2, touched, sink);
+  seg_a_body<BIG>(g, seg_smem, st, nullptr, 2, touched, sink);
   if (g.enc) {
     grid_barrier(g.bar, 4, g.err, st);
-    xattn_phase(g, seg_smem);
+    xattn_phase<BIG>(g, seg_smem);
   }
   SEG_SINK(g, touched, sink);
   SEG_END(st);
@@ -985,11 +1052,14 @@ int dec_seg_grid(int B, int cus) {
   // NG >= 16: at least 16 * MT blocks, one split-K tile pair each
   for (int ng : {32, 16})
     if (MT * ng <= cus) return MT * ng;
+  // 256 rows on a half-chip partition: 128 blocks, two split-K pairs / attention blocks per
+  // block, the LayerNorm GEMM phases at two m-tiles per block (dec_seg_mb2)
+  if (MT == 16 && 8 * MT <= cus) return 8 * MT;
   return 0;
 }
 
 int dec_seg_mtiles(int B) {
-  if (B <= 0 || B > 128) return 0;
+  if (B <= 0 || B > 256) return 0;
   int mt = 1;
   while (mt * 16 < B) mt *= 2;
   return mt;
@@ -1002,43 +1072,85 @@ bool dec_seg_supported(int d, int H, int B, int cus) {
 static void seg_attr(const void* k, size_t lds = kSegLds) {
   JANUS_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 }
+
+bool dec_seg_resident(int grid, int cus) {
+  // the most demanding launch: the layer kernel with the cross-attention's LDS tile
+  static int per_cu = -1;
+  if (per_cu < 0) {
+    const size_t lds = std::max(kSegLds, (size_t)kXattnLds);
+    int a = 0, b = 0;
+    seg_attr((const void*)dec_layer_kernel<false>, lds);
+    seg_attr((const void*)dec_layer_kernel<true>, lds);
+    JANUS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, dec_layer_kernel<false>, kNT, lds));
+    JANUS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, dec_layer_kernel<true>, kNT, lds));
+    per_cu = std::min(a, b);
+  }
+  return per_cu >= 1 && (int64_t)per_cu * cus >= grid;
+}
 // the layer and head kernels with the cross-attention phase: its LDS tile on top
 static size_t layer_lds(const DecSegArgs& a) {
   return a.enc ? std::max(kSegLds, (size_t)kXattnLds) : kSegLds;
 }
 
+// BIG: 256 rows on a 128-block grid (two split-K pairs / attention blocks per block)
+static bool seg_big(const DecSegArgs& a, int grid) { return grid < 16 * a.MT; }
+
+template <bool BIG>
+static void seg_a_go(const DecSegArgs& a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_seg_a_kernel<BIG>); attr = true; }
+  dec_seg_a_kernel<BIG><<<grid, kNT, kSegLds, s>>>(a);
+  JANUS_LAUNCH_CHECK();
+}
 void dec_seg_a_launch(const DecSegArgs& a, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_seg_a_kernel); attr = true; }
-  dec_seg_a_kernel<<<grid, kNT, kSegLds, s>>>(a);
-  JANUS_LAUNCH_CHECK();
+  if (seg_big(a, grid)) seg_a_go<true>(a, grid, s);
+  else seg_a_go<false>(a, grid, s);
 }
 
+template <bool BIG>
+static void seg_b_go(const DecSegArgs& a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_seg_b_kernel<BIG>); attr = true; }
+  dec_seg_b_kernel<BIG><<<grid, kNT, kSegLds, s>>>(a);
+  JANUS_LAUNCH_CHECK();
+}
 void dec_seg_b_launch(const DecSegArgs& a, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_seg_b_kernel); attr = true; }
-  dec_seg_b_kernel<<<grid, kNT, kSegLds, s>>>(a);
-  JANUS_LAUNCH_CHECK();
+  if (seg_big(a, grid)) seg_b_go<true>(a, grid, s);
+  else seg_b_go<false>(a, grid, s);
 }
 
+template <bool BIG>
+static void layer_go(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) { seg_attr((const void*)dec_layer_kernel<BIG>, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
+  dec_layer_kernel<BIG><<<grid, kNT, layer_lds(b), s>>>(b, nx);
+  JANUS_LAUNCH_CHECK();
+}
 void dec_layer_launch(const DecSegArgs& b, const DecSegNext& nx, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_layer_kernel, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
-  JANUS_CHECK(2 * ((b.B + 1) / 2) <= grid && b.wqkv != nullptr && b.qkv != nullptr,
+  const bool big = seg_big(b, grid);
+  const int cover = big ? 2 * grid : grid;
+  JANUS_CHECK(2 * ((b.B + 1) / 2) <= cover && b.wqkv != nullptr && b.qkv != nullptr,
               "decoder layer kernel: a block per row pair and head group, and a next layer");
-  JANUS_CHECK(!b.enc || (b.B <= grid && b.Te > 0), "decoder layer kernel: a block per row for the cross-attention");
-  dec_layer_kernel<<<grid, kNT, layer_lds(b), s>>>(b, nx);
-  JANUS_LAUNCH_CHECK();
+  JANUS_CHECK(!b.enc || (b.B <= cover && b.Te > 0), "decoder layer kernel: a block per row for the cross-attention");
+  if (big) layer_go<true>(b, nx, grid, s);
+  else layer_go<false>(b, nx, grid, s);
 }
 
-void dec_head_launch(const DecSegArgs& g, int grid, hipStream_t s) {
+template <bool BIG>
+static void head_go(const DecSegArgs& g, int grid, hipStream_t s) {
   static bool attr = false;
-  if (!attr) { seg_attr((const void*)dec_head_kernel, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
-  JANUS_CHECK(2 * ((g.B + 1) / 2) <= grid && g.wqkv != nullptr && g.qkv != nullptr,
-              "decoder head kernel: a block per row pair and head group, and layer 0's QKV");
-  JANUS_CHECK(!g.enc || (g.B <= grid && g.Te > 0), "decoder head kernel: a block per row for the cross-attention");
-  dec_head_kernel<<<grid, kNT, layer_lds(g), s>>>(g);
+  if (!attr) { seg_attr((const void*)dec_head_kernel<BIG>, std::max(kSegLds, (size_t)kXattnLds)); attr = true; }
+  dec_head_kernel<BIG><<<grid, kNT, layer_lds(g), s>>>(g);
   JANUS_LAUNCH_CHECK();
+}
+void dec_head_launch(const DecSegArgs& g, int grid, hipStream_t s) {
+  const bool big = seg_big(g, grid);
+  const int cover = big ? 2 * grid : grid;
+  JANUS_CHECK(2 * ((g.B + 1) / 2) <= cover && g.wqkv != nullptr && g.qkv != nullptr,
+              "decoder head kernel: a block per row pair and head group, and layer 0's QKV");
+  JANUS_CHECK(!g.enc || (g.B <= cover && g.Te > 0), "decoder head kernel: a block per row for the cross-attention");
+  if (big) head_go<true>(g, grid, s);
+  else head_go<false>(g, grid, s);
 }
 
 #ifdef JANUS_PHASE_PROF

@@ -69,10 +69,13 @@ __device__ __forceinline__ void embed_row(const _Float16* __restrict__ tok_emb,
   __shared__ float red[2][4];
   // every token read here was written by a selection or the prompt: the context rejects a
   // staggered row continued past where its slot stands (janus_whisper_decode_stand), so
-  // the -1 fill is never embedded (JANUS_DEBUG_ASSERT builds check it)
+  // the -1 fill is never embedded (JANUS_DEBUG_ASSERT builds check it). Release builds
+  // still clamp: a path that missed the host check embeds token 0 (wrong text, no fault)
+  // instead of reading before tok_emb
 #ifdef JANUS_DEBUG_ASSERT
   assert(tok >= 0);
 #endif
+  tok = max(tok, 0);
   float v0 = 0.f, v1 = 0.f;
   for (int base = 0; base < d; base += 512) {
     const int col = base + 2 * threadIdx.x;   // 8 lanes = one 16-column piece

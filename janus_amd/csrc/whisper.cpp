@@ -456,7 +456,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   Z.d_part_ml.ensure(sizeof(float) * (int64_t)B * max_split * H * 2);
   // cu_count: the CUs the caller's stream may use (a CU-masked partition); 0 = read it
   // from the stream's CU mask
-  const int cus = opt->cu_count > 0 ? opt->cu_count : stream_cu_count(s);
+  // (a caller's cu_count larger than its stream's CU mask is clamped to the mask)
+  const int cus = opt->cu_count > 0 ? std::min(opt->cu_count, stream_cu_count(s)) : stream_cu_count(s);
   // launch geometry from the options (janus_decode_options.logits_blocks / msplit_rows_n;
   // measured defaults: DESIGN.md §5b / §5d)
   const int lg_cap = opt->logits_blocks > 0 ? opt->logits_blocks : cus;
@@ -646,19 +647,22 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // self-attention (value projection, cross O + residual, LN3, fc1, fc2 + residual, LN1,
   // QKV) as two resident grids; the cross-attention then runs at one key split (its
   // output written directly). Shapes it does not cover keep the launch path.
-  const int seg_grid = opt->persistent ? dec_seg_grid(B, cus) : 0;
-  const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && xabs && !shared && !fused_ln &&
-                       !ln_fuse && !rln && ngroups == 0 && npairs == 0;
+  // (resident grids need every block co-resident: the kernels' occupancy must admit one
+  // block per CU of the partition, and a multi-lane call, whose lanes run concurrently on
+  // the same CUs, keeps the launch path)
+  const int seg_grid = opt->persistent && latch == nullptr ? dec_seg_grid(B, cus) : 0;
+  const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && dec_seg_resident(seg_grid, cus) &&
+                       xabs && !shared && !fused_ln && !ln_fuse && !rln && ngroups == 0 && npairs == 0;
   // persistent = 2: segment B of layer l, the self-attention of l + 1 and its segment A as
   // ONE launch per layer step (dec_layer_kernel): 29 -> 19 launches per position; layer
   // 0's QKV, self-attention and segment A as one head kernel and the final LayerNorm as the
   // last segment B's phase: 16
-  const bool layerk = persist && opt->persistent >= 2 && 2 * ((B + 1) / 2) <= seg_grid;
+  const bool layerk = persist && opt->persistent >= 2 && 2 * ((B + 1) / 2) <= 2 * seg_grid;
   // persistent = 3: the cross-attention as the head / layer kernel's last phase (10 launches
   // per position); the decoder side measured level with 16 (369.1-369.3 vs 368.4-369.4 ms
   // over 447 positions, profiles/r05_xattn_phase_ab.txt): a grid barrier costs what the
   // launch boundary it replaces did
-  const bool xfuse = layerk && opt->persistent >= 3 && B <= seg_grid;
+  const bool xfuse = layerk && opt->persistent >= 3 && B <= 2 * seg_grid;
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
     if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed
@@ -1089,7 +1093,12 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     JANUS_CHECK(opt->state_slot >= 0 && opt->state_slot < 8, "decode: state_slot must be 0 .. 7");
     const int slot = opt->state_slot;
     if (slot > 0) nlanes = 1;
-    while ((int)w->lanes.size() < std::max(nlanes, slot + 1)) w->lanes.emplace_back(new DecLane());
+    // storage: state slots 0..7 are lanes[0..7]; the extra workers of a multi-lane call
+    // (lanes 1..7) live in lanes[8..14], so they never overwrite a slot's KV caches,
+    // tokens, graphs or stand (the staggered step's fallback keeps state in slot 1)
+    auto lane_of = [](int i) { return i == 0 ? 0 : 7 + i; };
+    const int need = std::max(slot + 1, nlanes > 1 ? lane_of(nlanes - 1) + 1 : 1);
+    while ((int)w->lanes.size() < need) w->lanes.emplace_back(new DecLane());
     w->last_slot = slot;
     if (nlanes == 1 && (s != nullptr || slot > 0)) {
       JANUS_CHECK(s != nullptr, "decode: a state slot > 0 needs a non-null stream");
@@ -1114,7 +1123,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
         if (!((mask[c / 32] >> (c % 32)) & 1u)) masked = true;
     }
     for (int i = 0; i < nlanes; ++i) {
-      DecLane& Z = *w->lanes[i];
+      DecLane& Z = *w->lanes[lane_of(i)];
       if (Z.stream && Z.stream_mask != (masked ? mask : std::vector<uint32_t>())) {
         JANUS_HIP(hipStreamSynchronize(Z.stream));
         JANUS_HIP(hipStreamDestroy(Z.stream));
@@ -1141,7 +1150,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     JANUS_HIP(hipGetDevice(&dev));
     auto run = [&](int i) {
       const int b0 = (int)((int64_t)batch * i / nlanes), b1 = (int)((int64_t)batch * (i + 1) / nlanes);
-      DecLane& Z = *w->lanes[i];
+      DecLane& Z = *w->lanes[lane_of(i)];
       try {
         JANUS_HIP(hipSetDevice(dev));  // a fresh host thread starts on device 0
         janus_decode_rows sub{};
@@ -1169,7 +1178,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
     run(0);
     for (auto& t : th) t.join();
     for (int i = 0; i < nlanes; ++i) {
-      DecLane& Z = *w->lanes[i];
+      DecLane& Z = *w->lanes[lane_of(i)];
       JANUS_HIP(hipEventRecord(Z.ev_done, Z.stream));
       JANUS_HIP(hipStreamWaitEvent(s, Z.ev_done, 0));
     }

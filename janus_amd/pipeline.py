@@ -45,8 +45,12 @@ class ServingTuning:
     stagger_sets: int = 2           # decoder slot sets per staggered call (>= 2)
     all_windows: bool = True        # the whole seek loop (False: each clip's first window only,
                                     # the r05 serving semantics, kept as a comparison leg)
-    calls_per_step: int = 0         # staggered decoder calls per step (0: 2 with all_windows,
-                                    # the continuation windows' share; 1 without)
+    set_batches: int = 0            # staggered: rows per decoder slot set, in batches of B
+                                    # (0: 2 with all_windows — a batch's first windows and an
+                                    # earlier batch's continuation windows enter together —, 1
+                                    # without)
+    calls_per_step: int = 0         # staggered decoder calls per step (0: the windows a step
+                                    # takes in, 2 per clip with all_windows, / set_batches)
     voc_dec_utts: int = 0           # staggered: packets rendered on the decoder's CUs
     yin_dec_utts: Optional[int] = None  # YIN utterances on the decoder side (None: the
                                     # staggered step's controller; 0 in the other steps)
@@ -78,8 +82,13 @@ class ServingTuning:
                 kw[f.name] = int(v)
         return cls(**kw)
 
+    def batches_per_set(self):
+        return self.set_batches if self.set_batches > 0 else (2 if self.all_windows else 1)
+
     def calls(self):
-        return self.calls_per_step if self.calls_per_step > 0 else (2 if self.all_windows else 1)
+        if self.calls_per_step > 0:
+            return self.calls_per_step
+        return max(1, (2 if self.all_windows else 1) // self.batches_per_set())
 
 
 class EncodeResult:
@@ -598,11 +607,12 @@ class JanusPipeline(PacketRenderer):
         if st is None:
             n = max(2, self.tuning.stagger_sets)
             d = self.whisper.cfg.d_model
-            st = self._stag = {"B": B, "n": n, "k": 0, "sets": [None] * n, "pos": [0] * n,
+            R = B * self.tuning.batches_per_set()
+            st = self._stag = {"B": B, "R": R, "n": n, "k": 0, "sets": [None] * n, "pos": [0] * n,
                                "started": False, "queue": collections.deque(), "completed": [],
                                "serial": 0,
                                "finished": collections.deque(), "calls": self.tuning.calls(),
-                               "enc": torch.zeros(n * B, self.whisper.cfg.n_audio_ctx, d,
+                               "enc": torch.zeros(n * R, self.whisper.cfg.n_audio_ctx, d,
                                                   dtype=torch.float16, device=dev)}
         return st
 
@@ -612,11 +622,15 @@ class JanusPipeline(PacketRenderer):
                 or st["finished"])
 
     def staggered_depth(self):
-        """Staggered calls before the first batch comes out when every clip has two windows
-        (30 s clips on the synthetic weights): 3 with the continuation windows' calls, 2
-        (the r05 step) with first windows only."""
+        """Steps before the first batch comes out when every clip has two windows (30 s clips
+        on the synthetic weights): a window group completes N - 1 calls after it entered and
+        is absorbed at the next step; with all windows the continuation windows enter in the
+        step that absorbed the first ones (one call per step: 2N; two calls per step, the
+        second taking them: N + 1); first windows only: N."""
         n = max(2, self.tuning.stagger_sets)
-        return n + 1 if self.tuning.all_windows else n
+        if not self.tuning.all_windows:
+            return n
+        return 2 * n if self.tuning.calls() == 1 else n + 1
 
     def _absorb(self, st):
         """Host part of the windows the previous step's decoder calls completed: each
@@ -647,7 +661,9 @@ class JanusPipeline(PacketRenderer):
             prompts = [it.prompt for it in items]
             keys = [it.key for it in items]
             with torch.cuda.stream(self._hi_stream(self.device)):   # re-decodes: whole GPU
-                first, final, ndec = settle_round(w, tk, rows, prompts, keys, rec["enc"], L,
+                enc = (torch.cat([t[r0:r0 + c] for t, r0, c in rec["enc"]])
+                       if len(self.temperatures) > 1 else None)
+                first, final, ndec = settle_round(w, tk, rows, prompts, keys, enc, L,
                                                   self.temperatures, BEST_OF, **fb_kw)
             for j, (it, c0, r, nd) in enumerate(zip(items, first, final, ndec)):
                 b, s = it.batch, it.batch.streams[it.u]
@@ -737,12 +753,12 @@ class JanusPipeline(PacketRenderer):
         # its first windows completed, enter in that step's second call)
         pend = ([_Window(nb, u, 0, nb.streams[u].window_size(), list(tk.sot_sequence), (u, 0))
                  for u in range(B) if nb.streams[u].active] if nb is not None else [])
-        first_n = len(pend)
         pend += list(st["queue"])
         st["queue"].clear()
+        R = st["R"]
         groups = []
         for c in range(C):
-            g, pend = pend[:B], pend[B:]
+            g, pend = pend[:R], pend[R:]
             groups.append(g if g else None)
         st["queue"].extend(pend)
         # encoder outputs of the groups: the first windows' rows of enc1, the continuation
@@ -754,24 +770,24 @@ class JanusPipeline(PacketRenderer):
                 mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in conts])
                 enc2 = w.encode(mel2)
             ci = {id(it): i for i, it in enumerate(conts)}
-            gencs = []
-            for gi, g in enumerate(groups):
-                if g is None:
-                    gencs.append(None)
-                    continue
-                src = [(enc1, it.u) if id(it) not in ci else (enc2, ci[id(it)]) for it in g]
-                if all(t is enc1 for t, _ in src) and [r for _, r in src] == list(range(B))[:len(g)]:
-                    gencs.append(enc1[:len(g)])
-                elif all(t is enc2 for t, _ in src) and [r for _, r in src] == list(
-                        range(src[0][1], src[0][1] + len(g))):
-                    gencs.append(enc2[src[0][1]:src[0][1] + len(g)])
+        # each group's encoder rows as runs of consecutive rows of enc1 / enc2 [(tensor,
+        # first row, rows)], copied straight into the slot set's rows by its call
+        gencs = []
+        for g in groups:
+            runs = []
+            for it in g or []:
+                src, r = (enc2, ci[id(it)]) if id(it) in ci else (enc1, it.u)
+                if runs and runs[-1][0] is src and runs[-1][1] + runs[-1][2] == r:
+                    runs[-1][2] += 1
                 else:
-                    gencs.append(torch.stack([t[r] for t, r in src]))
+                    runs.append([src, r, 1])
+            gencs.append(runs if g else None)
         if self.keep_encoder_output:   # parity checks: every window's encoder rows and inputs
             log = self.__dict__.setdefault("window_log", {})
-            for g, e in zip(groups, gencs):
-                for j, it in enumerate(g or []):
-                    log[(it.batch.serial, it.u, it.key[1])] = (e[j], list(it.prompt), it.seek, it.size)
+            for g, runs in zip(groups, gencs):
+                rows = [t[r0 + i] for t, r0, c in (runs or []) for i in range(c)]
+                for it, e in zip(g or [], rows):
+                    log[(it.batch.serial, it.u, it.key[1])] = (e, list(it.prompt), it.seek, it.size)
         # the oldest finished batch on the host (its windows all settled)
         fin = st["finished"].popleft() if st["finished"] else None
         res_prev = self._finish_batch(fin) if fin is not None else None
@@ -874,18 +890,21 @@ class JanusPipeline(PacketRenderer):
             pcm16 = pcm_b if pcm16 is None else torch.cat([pcm16, pcm_b])
         return res_prev, wav, pcm16
 
-    def _stag_call(self, st, g, genc, S, c):
+    def _stag_call(self, st, g, runs, S, c):
         """One staggered decoder call on the current (decoder) stream: group ``g`` (a list of
         windows, or None) enters the fresh slot set (its encoder rows copied into the set's
         rows of the call's encoder buffer; its prompts), every other set continues; the set
         whose group completes gets its results copied to the host behind the call."""
         w, L, tk = self.whisper, self.max_length, self.whisper.tokenizer
-        B, n = st["B"], st["n"]
+        B, n = st["R"], st["n"]     # rows per slot set
         k = st["k"]
         f = k % n
         ds = torch.cuda.current_stream()
         if g is not None:
-            st["enc"][f * B:f * B + len(g)].copy_(genc)
+            o = f * B
+            for t, r0, cnt in runs:
+                st["enc"][o:o + cnt].copy_(t[r0:r0 + cnt])
+                o += cnt
         pos = st["pos"]
         set_offs, jc = stagger_plan(st["sets"], pos, st["started"], k, S, g is not None)
         offs = [o for o in set_offs for _ in range(B)]
@@ -913,7 +932,7 @@ class JanusPipeline(PacketRenderer):
             st["sets"][jc] = None
         if g is not None:
             st["sets"][f] = {"born": k, "items": g, "plens": [len(it.prompt) for it in g],
-                             "enc": genc}
+                             "enc": runs}
         st["k"] = k + 1
 
     # YIN of one 30 s utterance on a 16-CU-per-XCD partition (26 ms for 64, either side)

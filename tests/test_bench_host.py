@@ -73,7 +73,8 @@ def test_serving_tuning_from_env():
     from janus_amd.pipeline import ServingTuning
     t = ServingTuning.from_env({})
     assert t == ServingTuning() and t.persistent == 2 and t.stagger_sets == 2 and t.voc_dec_utts == 0
-    assert t.all_windows and t.calls() == 2 and ServingTuning(all_windows=False).calls() == 1
+    assert t.all_windows and t.batches_per_set() == 2 and t.calls() == 1
+    assert ServingTuning(all_windows=False).calls() == 1 and ServingTuning(set_batches=1).calls() == 2
     t = ServingTuning.from_env({"JANUS_STAGGER_SETS": "3", "JANUS_YIN_DEC_UTTS": "5",
                                 "JANUS_HOST_PREFETCH": "0", "JANUS_YIN_SIDE": "beside",
                                 "JANUS_OTHER": "1", "JANUS_ALL_WINDOWS": "0"})

@@ -533,12 +533,15 @@ def test_persistent_segments_vs_oracle(base_engine, gpu, mode):
         assert abs(a - c) <= 5e-3 * c + 1e-12, (b, a, c)
 
 
-@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2), (64, 3)])
+@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2), (64, 3), (128, 1), (128, 2),
+                                       (128, 3)])
 def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode):
     """Continuous batching through the persistent segments: two slot sets of `rows` rows
-    (2 x 64 = the bench's decoder call), each batch started fresh in one call and continued
-    in the next, equal a full persistent decode of that batch alone bit for bit — a row's
-    arithmetic in the segments does not depend on the rows beside it or on the grid."""
+    (2 x 128 = the bench's decoder call: each set a batch's first windows and an earlier
+    batch's continuation windows; 256 rows run the 128-block grid with two split-K pairs and
+    attention blocks per block), each batch started fresh in one call and continued in the
+    next, equal a full persistent decode of that batch alone bit for bit — a row's arithmetic
+    in the segments does not depend on the rows beside it or on the grid."""
     eng, _ = base_engine
     L, S = 40, 20
     batches = []
