@@ -251,8 +251,9 @@ typedef struct {
                               (0 = auto: 1024 on <= 128 CUs, else none; -1 = never) */
   int persistent;          /* 1: the launches between a layer's self- and cross-attention
                               run as two resident-grid launches with in-launch barriers
-                              (d_model 512, 8 heads, <= 128 rows, >= 16 CUs per 16 rows; the
-                              other shapes keep the launch path): 29 launches per position
+                              (d_model 512, 8 heads, <= 256 rows, >= 16 CUs per 16 rows up to
+                              128 rows, 128 CUs at 256 rows; the other shapes keep the launch
+                              path): 29 launches per position
                               at base.en instead of 75. Same arithmetic per row except the
                               GEMMs' k order (fp32-rounding level, not bit-identical to 0).
                               2: one launch per layer step — segment B of layer l, the
@@ -291,6 +292,9 @@ typedef struct {
                                                1 LN1, 2 LN2, 4 LN3, 8 final) instead of the
                                                default 9 up to 64 rows, 0 above */
 #define JANUS_DEC_PATH_LN_MASK(m)   (JANUS_DEC_PATH_LN_PROLOGUE | (((uint32_t)(m) & 15u) << 12))
+#define JANUS_DEC_PATH_SEG_2CU      0x10000u /* persistent segments at 256 rows: two blocks
+                                               per CU instead of one block per CU taking two
+                                               blocks' work */
 
 /*
  * Batched greedy decoding (temperature 0) with the Whisper logit rules

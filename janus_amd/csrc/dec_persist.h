@@ -47,8 +47,9 @@ struct DecSegNext {
 
 // 16-row tiles for B rows (0: unsupported, B > 256)
 int dec_seg_mtiles(int B);
-// blocks of the resident grid on a partition of `cus` CUs (0: unsupported)
-int dec_seg_grid(int B, int cus);
+// blocks of the resident grid on a partition of `cus` CUs (0: unsupported); 256 rows run
+// one block per CU taking two blocks' work, or with `two_per_cu` two blocks per CU
+int dec_seg_grid(int B, int cus, bool two_per_cu = false);
 bool dec_seg_supported(int d, int H, int B, int cus);
 // the resident grid fits: blocks per CU (occupancy of the segment kernels with their LDS)
 // times the partition's CUs cover `grid`

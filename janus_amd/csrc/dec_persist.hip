@@ -1043,7 +1043,9 @@ __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
   grid_exit(g.bar);
 }
 
-int dec_seg_grid(int B, int cus) {
+static int seg_per_cu();
+
+int dec_seg_grid(int B, int cus, bool two_per_cu) {
   // rows in 16-row tiles, rounded to a power of two (<= 8); groups of 16-column tiles per
   // m-tile NG in {32, 16} (a divisor of 96, 128 and 256 tiles: QKV, fc1, qk) with
   // MT * NG <= the partition's CUs: one block per CU, every block co-resident
@@ -1052,9 +1054,15 @@ int dec_seg_grid(int B, int cus) {
   // NG >= 16: at least 16 * MT blocks, one split-K tile pair each
   for (int ng : {32, 16})
     if (MT * ng <= cus) return MT * ng;
-  // 256 rows on a half-chip partition: 128 blocks, two split-K pairs / attention blocks per
-  // block, the LayerNorm GEMM phases at two m-tiles per block (dec_seg_mb2)
-  if (MT == 16 && 8 * MT <= cus) return 8 * MT;
+  if (MT == 16) {
+    // 256 rows on a half-chip partition: 128 blocks taking two split-K pairs / attention
+    // blocks each, the LayerNorm GEMM phases at two m-tiles per block (1452 us per position
+    // in the staggered step); or (two_per_cu) 256 blocks, two per CU (the segment kernels'
+    // 128 VGPRs and LDS admit two: 16 waves per CU), each with the 128-row grid's one-pair
+    // work (1492 us; profiles/r06_seg_grid_ab.txt)
+    if (two_per_cu && 16 * MT <= 2 * cus && seg_per_cu() >= 2) return 16 * MT;
+    if (8 * MT <= cus) return 8 * MT;
+  }
   return 0;
 }
 
@@ -1073,8 +1081,11 @@ static void seg_attr(const void* k, size_t lds = kSegLds) {
   JANUS_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 }
 
-bool dec_seg_resident(int grid, int cus) {
-  // the most demanding launch: the layer kernel with the cross-attention's LDS tile
+bool dec_seg_resident(int grid, int cus) { return (int64_t)seg_per_cu() * cus >= grid; }
+
+// co-resident blocks per CU of the segment kernels: the most demanding launch, the layer
+// kernel with the cross-attention's LDS tile
+static int seg_per_cu() {
   static int per_cu = -1;
   if (per_cu < 0) {
     const size_t lds = std::max(kSegLds, (size_t)kXattnLds);
@@ -1085,7 +1096,7 @@ bool dec_seg_resident(int grid, int cus) {
     JANUS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, dec_layer_kernel<true>, kNT, lds));
     per_cu = std::min(a, b);
   }
-  return per_cu >= 1 && (int64_t)per_cu * cus >= grid;
+  return per_cu;
 }
 // the layer and head kernels with the cross-attention phase: its LDS tile on top
 static size_t layer_lds(const DecSegArgs& a) {

@@ -410,6 +410,17 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     const uint32_t* __restrict__ seeds, int pos) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   JANUS_DEC_WAVE_PRIO();
+  // row group blockIdx.y: rows [64 y, 64 y + 64) of the call (one launch for every group:
+  // a group's blocks start while the previous group's last blocks drain)
+  {
+    const int r0 = (int)blockIdx.y * 64;
+    A += (int64_t)r0 * lda;
+    rules += r0;
+    parts += (int64_t)r0 * gridDim.x;
+    if (lnx) lnx += (int64_t)r0 * ldx;
+    if (seeds) seeds += r0;
+    B = min(64, B - r0);
+  }
   constexpr int K = NKS * 32;
   constexpr int kLgWaves = lg_waves(K);
   constexpr int AP = K + 16;  // row pitch (halves): 16*AP bytes with AP/8 % 4 == 2 -> conflict-free
@@ -676,11 +687,9 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
     if (!no_rot && rem > 0 && nspec > 0 && rem + nspec + (R.blank >= 0 ? 1 + R.blank / 16 : 0) <= stride)
       rot = ((s0 - rem) % ntiles + ntiles) % ntiles;
   }
-  for (int r0 = 0; r0 < B; r0 += 64)  // 64 rows per launch
-    kern<<<grid, nw * 64, lds, s>>>(A + (int64_t)r0 * lda, lda, W, V, std::min(64, B - r0), R,
-                                          smask, rules + r0, parts + (int64_t)r0 * grid, ntiles,
-                                          lnx ? lnx + (int64_t)r0 * ldx : nullptr, ldx, ln_g, ln_b, rot,
-                                          seeds ? seeds + r0 : nullptr, pos);
+  // 64 rows per row group (blockIdx.y), every group in one launch
+  kern<<<dim3(grid, (B + 63) / 64), nw * 64, lds, s>>>(A, lda, W, V, B, R, smask, rules, parts, ntiles, lnx, ldx,
+                                                      ln_g, ln_b, rot, seeds, pos);
   JANUS_LAUNCH_CHECK();
 }
 

@@ -650,7 +650,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // (resident grids need every block co-resident: the kernels' occupancy must admit one
   // block per CU of the partition, and a multi-lane call, whose lanes run concurrently on
   // the same CUs, keeps the launch path)
-  const int seg_grid = opt->persistent && latch == nullptr ? dec_seg_grid(B, cus) : 0;
+  const int seg_grid = opt->persistent && latch == nullptr ? dec_seg_grid(B, cus, path(JANUS_DEC_PATH_SEG_2CU)) : 0;
   const bool persist = seg_grid > 0 && dec_seg_supported(d, H, B, cus) && dec_seg_resident(seg_grid, cus) &&
                        xabs && !shared && !fused_ln && !ln_fuse && !rln && ngroups == 0 && npairs == 0;
   // persistent = 2: segment B of layer l, the self-attention of l + 1 and its segment A as

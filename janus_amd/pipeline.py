@@ -59,6 +59,7 @@ class ServingTuning:
     yin_blocks: int = 0             # overlapped step: YIN grid cap on the vocoder side (0 = none)
     yin_beside_blocks: int = 128    # overlapped step, yin_side "beside": its grid cap
     xattn_splits: Optional[int] = None  # cross-attention key splits (None: 1 staggered, 4 else)
+    dec_path_flags: int = 0         # staggered decoder: janus_decode_options.path_flags (A/Bs)
     fallback_full: bool = True      # overlapped step: seek rounds / fallback on the whole GPU
     fallback_xattn_splits: int = 4
     host_prefetch: bool = True      # staggered: D2H of the completed windows behind their call
@@ -833,8 +834,10 @@ class JanusPipeline(PacketRenderer):
                 # stream over the decoder's CUs with its grid capped at tuning.yin_beside blocks
                 # (default 128; 0: after the calls): the latency-bound decoder leaves issue
                 # slots free (profiles/r04_yin_beside_ab.json)
+                # (not beside a 256-row call: its resident grid holds two blocks on every
+                # CU of the partition, the YIN blocks would keep them from co-residing)
                 yb = self.tuning.yin_beside
-                beside = yb > 0 and n_dec > 0
+                beside = yb > 0 and n_dec > 0 and st["n"] * st["R"] <= 128
                 if beside:
                     ys = self._yin_s.stream
                     ys.wait_stream(ds)
@@ -915,7 +918,7 @@ class JanusPipeline(PacketRenderer):
                 prompts[f * B + j] = it.prompt
         dec = w.decode_ex(st["enc"], prompts=prompts, max_length=L, pos_offset=offs, steps=S,
                           xattn_splits=self._xsplits(1), cu_count=self._dec_s.n_cus,
-                          persistent=self.tuning.persistent)
+                          persistent=self.tuning.persistent, path_flags=self.tuning.dec_path_flags)
         st["started"] = True
         # where each set's rows stand now (offset + S, or fewer when every row finished and
         # the call stopped early), as the context recorded it

@@ -533,15 +533,16 @@ def test_persistent_segments_vs_oracle(base_engine, gpu, mode):
         assert abs(a - c) <= 5e-3 * c + 1e-12, (b, a, c)
 
 
-@pytest.mark.parametrize("rows,mode", [(40, 1), (64, 1), (40, 2), (64, 2), (64, 3), (128, 1), (128, 2),
-                                       (128, 3)])
-def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode):
+@pytest.mark.parametrize("rows,mode,flags", [(40, 1, 0), (64, 1, 0), (40, 2, 0), (64, 2, 0), (64, 3, 0),
+                                             (128, 1, 0), (128, 2, 0), (128, 3, 0), (128, 2, 0x10000)])
+def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode, flags):
     """Continuous batching through the persistent segments: two slot sets of `rows` rows
     (2 x 128 = the bench's decoder call: each set a batch's first windows and an earlier
-    batch's continuation windows; 256 rows run the 128-block grid with two split-K pairs and
-    attention blocks per block), each batch started fresh in one call and continued in the
-    next, equal a full persistent decode of that batch alone bit for bit — a row's arithmetic
-    in the segments does not depend on the rows beside it or on the grid."""
+    batch's continuation windows; 256 rows run a 128-block grid with two split-K pairs and
+    attention blocks per block, or with DEC_PATH_SEG_2CU two blocks per CU), each batch
+    started fresh in one call and continued in the next, equal a full persistent decode of
+    that batch alone bit for bit — a row's arithmetic in the segments does not depend on the
+    rows beside it or on the grid."""
     eng, _ = base_engine
     L, S = 40, 20
     batches = []
@@ -569,7 +570,7 @@ def test_persistent_staggered_bit_identical(base_engine, gpu, rows, mode):
         if call == 0:
             offs = [0] * (2 * rows)
         out = eng.decode_ex(torch.cat(rows_enc), max_length=L, pos_offset=offs, steps=S, persistent=mode,
-                            cu_count=128)
+                            cu_count=128, path_flags=flags)
         if call > 0 and sets[cont] is not None:
             bi = sets[cont]
             sl = slice(cont * rows, cont * rows + rows)
