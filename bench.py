@@ -58,7 +58,7 @@ def parse():
                     help="CUs per XCD (of 32) for the greedy decoder in the overlapped serving step "
                          "(vocoder of batch i-1 on the rest; multiples of 4 keep every shader engine "
                          "even); 0 = sequential step")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
     ap.add_argument("--stagger", type=int, default=int(os.environ.get("JANUS_STAGGER", "1")),
                     help="1: continuous batching of windows in the decoder (JanusPipeline."
                          "step_staggered): each step's decoder calls advance 2 slot sets of 64 "
