@@ -66,7 +66,7 @@ void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int 
 }
 
 template <int D, int CH, bool PAIR = false, bool DIRECT = false, bool PF2 = false, bool ROWLD = false>
-__global__ __launch_bounds__(CH * 8, PF2 ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2)) void xattn_kernel(
+__global__ __launch_bounds__(CH * 8, (PF2 && !ROWLD) ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2)) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
     _Float16* __restrict__ out = nullptr) {
@@ -529,6 +529,14 @@ constexpr bool kXattnRow = true;   // one-split D = 512: whole-row loads (ROWLD)
 #else
 constexpr bool kXattnRow = false;  // A/B build: the fragment-pattern loads
 #endif
+// one-split row loads with two chunks in flight per wave (two register sets of 8 rows):
+// 158 VGPRs, one block per CU — measured slower at 256 rows (decoder 1539 vs 1444 us per
+// position in the staggered step, profiles/r06_xattn_ab.txt); A/B build only
+#ifdef JANUS_XATTN_ROW2
+constexpr bool kXattnRowPF2 = true;
+#else
+constexpr bool kXattnRowPF2 = false;
+#endif
 #ifndef JANUS_XATTN_PF1
 constexpr bool kXattnPF2 = true;
 #else
@@ -544,7 +552,8 @@ static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, in
   constexpr bool row = kXattnRow && D == 512 && CH == 64;
   decltype(&xattn_kernel<D, CH, false>) kern;
   if (direct) {
-    if constexpr (row) kern = xattn_kernel<D, CH, false, true, false, true>;
+    if constexpr (row) kern = kXattnRowPF2 ? xattn_kernel<D, CH, false, true, true, true>
+                                           : xattn_kernel<D, CH, false, true, false, true>;
     else kern = xattn_kernel<D, CH, false, true, kXattnPF2>;
   } else {
     kern = pairs ? xattn_kernel<D, CH, true> : xattn_kernel<D, CH, false>;

@@ -106,7 +106,7 @@ __device__ __forceinline__ void xattn_body(
   }
   for (int i = tid; i < 16 * PP; i += NW * 64) sP[i] = (_Float16)0.0f;  // P rows >= H stay zero
 
-  static_assert(!ROWLD || (D == 512 && CH == 64 && DIRECT && !PF2 && !PAIR && KS == CH / NW),
+  static_assert(!ROWLD || (D == 512 && CH == 64 && DIRECT && !PAIR && KS == CH / NW),
                 "row loads: one 1 KB key row per register slot");
   half8 ef[KS], eg[KS];  // eg: the second chunk in flight (PF2)
   auto load_to = [&](half8 (&dst)[KS], int t) __attribute__((always_inline)) {
@@ -158,7 +158,9 @@ __device__ __forceinline__ void xattn_body(
 #pragma unroll
       for (int i = 0; i < KS; ++i)
         *reinterpret_cast<half8*>(sE + ((CH / NW) * w + i) * QP + 8 * lane) = cur[i];
-      if (t + CH < t1) load_to(cur, t + CH);
+      // (PF2: the chunk two ahead — the other register set holds the next one's rows)
+      if constexpr (PF2) load_to(cur, t + 2 * CH);
+      else if (t + CH < t1) load_to(cur, t + CH);
       __syncthreads();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
