@@ -295,6 +295,9 @@ typedef struct {
 #define JANUS_DEC_PATH_SEG_2CU      0x10000u /* persistent segments at 256 rows: two blocks
                                                per CU instead of one block per CU taking two
                                                blocks' work */
+#define JANUS_DEC_PATH_XFWD         0x20000u /* persistent segments: every layer's one-split
+                                               cross-attention over the key chunks first to
+                                               last (default: odd layers last to first) */
 
 /*
  * Batched greedy decoding (temperature 0) with the Whisper logit rules

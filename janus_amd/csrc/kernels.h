@@ -125,7 +125,7 @@ void xattn_absorb(const float* wq, const float* bq, const float* wk, int D, int 
 // row b reads enc row b.
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
                   int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
-                  bool combine = true, const int4* pairs = nullptr, int npairs = 0);
+                  bool combine = true, const int4* pairs = nullptr, int npairs = 0, bool rev = false);
 // Groups of <= 6 decoder rows sharing an encoder row, one block per (split, group):
 // groups [device] int [ngroups][8] = {e, row_0 .. row_5 (-1: none), -}; partials as
 // xattn_launch(combine = false) writes them (merged by xattn_combine_vproj_launch).

@@ -663,6 +663,11 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   // over 447 positions, profiles/r05_xattn_phase_ab.txt): a grid barrier costs what the
   // launch boundary it replaces did
   const bool xfuse = layerk && opt->persistent >= 3 && B <= 2 * seg_grid;
+  // odd layers' cross-attention sweeps the encoder output's key chunks last to first, so it
+  // starts on what the layer before it read last, still in the Infinity Cache (at 256 rows a
+  // layer reads 393 MB, past its 256 MB): decoder 1472 -> 1394 us per position in the
+  // staggered step (profiles/r06_xattn_ab.txt); JANUS_DEC_PATH_XFWD keeps every sweep forwards
+  const bool xrev = !path(JANUS_DEC_PATH_XFWD);
   if (persist) {
     Z.d_omid.ensure(sizeof(_Float16) * B * d);
     if (!Z.d_segbar.p) {  // barrier counters start at zero; the kernels leave them zeroed
@@ -753,7 +758,7 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
         else if (l == 0) dec_head_launch(head_args(pos), seg_grid, s);
         if (!xfuse)  // (persistent 3: the cross-attention ran as the head / layer kernel's last phase)
           xattn_launch(g.xqk, enc, B, Te, d, H, 1, Z.d_xpc.as<float>(), Z.d_xpml.as<float>(), Z.d_xc.as<_Float16>(),
-                       s, true, nullptr, 0);
+                       s, true, nullptr, 0, xrev && (l & 1));
         if (layerk && l + 1 < nl) {
           DecLayer& N = w->dec[l + 1];
           const DecSegNext nx{N.wo.as<_Float16>(), N.bo, N.ln2g, N.ln2b, N.wqk.as<_Float16>(), N.bqk.as<float>()};

@@ -69,11 +69,11 @@ template <int D, int CH, bool PAIR = false, bool DIRECT = false, bool PF2 = fals
 __global__ __launch_bounds__(CH * 8, (PF2 && !ROWLD) ? 1 : (CH == 32 ? (D > 512 ? 2 : 3) : 2)) void xattn_kernel(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
-    _Float16* __restrict__ out = nullptr) {
+    _Float16* __restrict__ out = nullptr, int rev = 0) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   JANUS_DEC_WAVE_PRIO();
   xattn_body<D, CH, PAIR, DIRECT, PF2, false, ROWLD>(qk, enc, Te, H, kps, part_c, part_ml, pairs, out,
-                                                     blockIdx.x, gridDim.x, blockIdx.y, smem);
+                                                     blockIdx.x, gridDim.x, blockIdx.y, smem, rev != 0);
 }
 
 // GROUP (r04): up to 2*NMT decoder rows attending to the same encoder row — the best_of = 5
@@ -545,7 +545,7 @@ constexpr bool kXattnPF2 = false;  // A/B build: one chunk in flight
 template <int D, int CH>
 static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, int H, int nsplit,
                       float* part_c, float* part_ml, hipStream_t s, const int4* pairs, int npairs,
-                      _Float16* out = nullptr) {
+                      _Float16* out = nullptr, bool rev = false) {
   const int chunks = (Te + CH - 1) / CH;
   const int kps = (chunks + nsplit - 1) / nsplit * CH;
   const bool direct = out != nullptr;
@@ -566,7 +566,7 @@ static void xattn_cfg(const _Float16* qk, const _Float16* enc, int B, int Te, in
     attr[ai] = true;
   }
   kern<<<dim3(nsplit, pairs ? npairs : B), CH * 8, XGeo<D, CH>::LDS, s>>>(qk, enc, Te, H, kps, part_c,
-                                                                         part_ml, pairs, out);
+                                                                         part_ml, pairs, out, rev ? 1 : 0);
   JANUS_LAUNCH_CHECK();
 }
 
@@ -576,7 +576,7 @@ bool xattn_supported(int D, int H) {
 
 void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D, int H,
                   int nsplit, float* part_c, float* part_ml, _Float16* out, hipStream_t s,
-                  bool combine, const int4* pairs, int npairs) {
+                  bool combine, const int4* pairs, int npairs, bool rev) {
   JANUS_CHECK(xattn_supported(D, H), "xattn: need D = 64 H in {384, 512, 768}");
   if (B <= 0 || Te <= 0) return;
   JANUS_CHECK(nsplit >= 1 && nsplit <= 63, "xattn: 1..63 key splits");
@@ -586,7 +586,7 @@ void xattn_launch(const _Float16* qk, const _Float16* enc, int B, int Te, int D,
   // one key split with the merge requested: the kernel writes c itself (DIRECT), no merge
   if (combine && nsplit == 1 && !pairs && !ch32 && D <= 512) {
     if (D == 384) xattn_cfg<384, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out);
-    else xattn_cfg<512, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out);
+    else xattn_cfg<512, 64>(qk, enc, B, Te, H, 1, part_c, part_ml, s, nullptr, 0, out, rev);
     return;
   }
   if (D == 384) {

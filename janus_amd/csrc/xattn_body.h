@@ -63,7 +63,7 @@ template <int D, int CH, bool PAIR, bool DIRECT, bool PF2, bool SC1Q = false, bo
 __device__ __forceinline__ void xattn_body(
     const _Float16* __restrict__ qk, const _Float16* __restrict__ enc, int Te, int H, int kps,
     float* __restrict__ part_c, float* __restrict__ part_ml, const int4* __restrict__ pairs,
-    _Float16* __restrict__ out, int s, int nsplit, int by, _Float16* smem) {
+    _Float16* __restrict__ out, int s, int nsplit, int by, _Float16* smem, bool rev = false) {
   using G = XGeo<D, CH>;
   constexpr int QP = G::QP, PP = G::PP, KH = G::KH, KS = G::KS, NT = G::NT, NW = G::NW,
                 NKT = G::NKT, HPW = G::HPW;
@@ -144,7 +144,13 @@ __device__ __forceinline__ void xattn_body(
 #pragma unroll
   for (int i = 0; i < HPW; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
 
-  if (PF2 || t0 < t1) load_to(ef, t0);
+  // rev (row loads, one chunk in flight): the chunks last to first — a decoder layer whose
+  // predecessor swept the encoder output forwards starts on the chunks it read last, still in
+  // the Infinity Cache (the 256-row call's 393 MB per layer do not fit it)
+  const int tl = t0 + ((t1 - t0 - 1) / CH) * CH;   // the last chunk's first key
+  const bool rv = ROWLD && !PF2 && rev;
+  const int tfirst = rv ? tl : t0, dt = rv ? -CH : CH;
+  if (PF2 || t0 < t1) load_to(ef, tfirst);
   if (PF2) load_to(eg, t0 + CH);
   __syncthreads();
   // one chunk of CH keys whose E fragments are in `cur`; `cur` is refilled with the chunk
@@ -160,7 +166,7 @@ __device__ __forceinline__ void xattn_body(
         *reinterpret_cast<half8*>(sE + ((CH / NW) * w + i) * QP + 8 * lane) = cur[i];
       // (PF2: the chunk two ahead — the other register set holds the next one's rows)
       if constexpr (PF2) load_to(cur, t + 2 * CH);
-      else if (t + CH < t1) load_to(cur, t + CH);
+      else if (t + dt < t1 && t + dt >= t0) load_to(cur, t + dt);
       __syncthreads();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -247,7 +253,7 @@ __device__ __forceinline__ void xattn_body(
     }
     if (t < t1) chunk(t, ef);
   } else {
-    for (int t = t0; t < t1; t += CH) chunk(t, ef);
+    for (int t = tfirst; t < t1 && t >= t0; t += dt) chunk(t, ef);
   }
 
   if constexpr (DIRECT) {

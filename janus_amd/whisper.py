@@ -77,6 +77,7 @@ DEC_PATH_NO_SEL_EMBED = 0x0200
 DEC_PATH_NO_EMBED_LN = 0x0400
 DEC_PATH_LN_PROLOGUE = 0x0800
 DEC_PATH_SEG_2CU = 0x10000
+DEC_PATH_XFWD = 0x20000
 
 
 def dec_path_ln_mask(m: int) -> int:

@@ -105,7 +105,7 @@ def test_decode_path_flags_match_header():
     from janus_amd import whisper as w
     src = open(os.path.join(HEADER_DIR, "janus.h")).read()
     flags = dict(re.findall(r"#define JANUS_DEC_PATH_([A-Z0-9_]+)\s+(0x[0-9a-fA-F]+)u", src))
-    assert len(flags) == 13
+    assert len(flags) == 14
     for name, v in flags.items():
         assert getattr(w, "DEC_PATH_" + name) == int(v, 16), name
     assert w.dec_path_ln_mask(9) == 0x0800 | (9 << 12)
