@@ -51,6 +51,11 @@ class ServingTuning:
                                     # without)
     calls_per_step: int = 0         # staggered decoder calls per step (0: the windows a step
                                     # takes in, 2 per clip with all_windows, / set_batches)
+    cont_encode: str = "hi"         # staggered: continuation windows encoded on the whole GPU
+                                    # before this step's call ("hi"), or on the vocoder's CUs,
+                                    # entering the next step's call ("voc": its traffic beside
+                                    # the decoder costs more, 344.9 vs 333.8 ms per step,
+                                    # profiles/r06_cont_encode_ab.txt)
     voc_dec_utts: int = 0           # staggered: packets rendered on the decoder's CUs
     yin_dec_utts: Optional[int] = None  # YIN utterances on the decoder side (None: the
                                     # staggered step's controller; 0 in the other steps)
@@ -75,7 +80,7 @@ class ServingTuning:
             v = env.get("JANUS_" + f.name.upper())
             if v is None:
                 continue
-            if f.name == "yin_side":
+            if f.name in ("yin_side", "cont_encode"):
                 kw[f.name] = v
             elif f.name in ("fallback_full", "host_prefetch", "side_timing", "all_windows"):
                 kw[f.name] = v not in ("", "0")
@@ -207,6 +212,8 @@ class _Window:
     size: int
     prompt: list
     key: tuple        # (utterance, window counter): the fallback's noise seeds
+    enc: object = None   # its encoder output: row `erow` of this fp16 [n][1500][d] tensor
+    erow: int = 0
 
 
 def _window(batch, u, tk, max_length):
@@ -611,6 +618,7 @@ class JanusPipeline(PacketRenderer):
             R = B * self.tuning.batches_per_set()
             st = self._stag = {"B": B, "R": R, "n": n, "k": 0, "sets": [None] * n, "pos": [0] * n,
                                "started": False, "queue": collections.deque(), "completed": [],
+                               "ready": collections.deque(),
                                "serial": 0,
                                "finished": collections.deque(), "calls": self.tuning.calls(),
                                "enc": torch.zeros(n * R, self.whisper.cfg.n_audio_ctx, d,
@@ -619,8 +627,8 @@ class JanusPipeline(PacketRenderer):
 
     @staticmethod
     def _stag_busy(st):
-        return (any(x is not None for x in st["sets"]) or st["queue"] or st["completed"]
-                or st["finished"])
+        return (any(x is not None for x in st["sets"]) or st["queue"] or st["ready"]
+                or st["completed"] or st["finished"])
 
     def staggered_depth(self):
         """Steps before the first batch comes out when every clip has two windows (30 s clips
@@ -631,7 +639,8 @@ class JanusPipeline(PacketRenderer):
         n = max(2, self.tuning.stagger_sets)
         if not self.tuning.all_windows:
             return n
-        return 2 * n if self.tuning.calls() == 1 else n + 1
+        late = 1 if self.tuning.cont_encode == "voc" else 0   # encoded a step before entering
+        return (2 * n if self.tuning.calls() == 1 else n + 1) + late
 
     def _absorb(self, st):
         """Host part of the windows the previous step's decoder calls completed: each
@@ -749,35 +758,38 @@ class JanusPipeline(PacketRenderer):
             st["serial"] += 1
         # the windows the previous step completed, on the host while the encoder runs
         self._absorb(st)
-        # this step's groups: the new batch's first windows, then the queued continuation
-        # windows, oldest first (so a batch's continuation windows, queued at the step after
-        # its first windows completed, enter in that step's second call)
-        pend = ([_Window(nb, u, 0, nb.streams[u].window_size(), list(tk.sot_sequence), (u, 0))
+        # this step's groups: the new batch's first windows, then the continuation windows,
+        # oldest first — with cont_encode "voc" those encoded on the vocoder's CUs during the
+        # previous step (st["ready"]), with "hi" the queued ones, encoded below on the whole GPU
+        pend = ([_Window(nb, u, 0, nb.streams[u].window_size(), list(tk.sot_sequence), (u, 0), enc1, u)
                  for u in range(B) if nb.streams[u].active] if nb is not None else [])
-        pend += list(st["queue"])
-        st["queue"].clear()
+        late = self.tuning.cont_encode == "voc"
+        src_q = st["ready"] if late else st["queue"]
+        pend += list(src_q)
+        src_q.clear()
         R = st["R"]
         groups = []
         for c in range(C):
             g, pend = pend[:R], pend[R:]
             groups.append(g if g else None)
-        st["queue"].extend(pend)
-        # encoder outputs of the groups: the first windows' rows of enc1, the continuation
-        # windows encoded here from their clips' features (one encoder call)
-        conts = [it for g in groups if g for it in g if it.batch is not nb or it.key[1] > 0]
-        with torch.cuda.stream(hi):
-            enc2 = None
-            if conts:
-                mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in conts])
-                enc2 = w.encode(mel2)
-            ci = {id(it): i for i, it in enumerate(conts)}
-        # each group's encoder rows as runs of consecutive rows of enc1 / enc2 [(tensor,
-        # first row, rows)], copied straight into the slot set's rows by its call
+        src_q.extend(pend)
+        if not late:
+            # the groups' continuation windows encoded here from their clips' features (one
+            # encoder call on the whole GPU, before the decoder call)
+            conts = [it for g in groups if g for it in g if it.enc is None]
+            with torch.cuda.stream(hi):
+                if conts:
+                    mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in conts])
+                    enc2 = w.encode(mel2)
+                    for i, it in enumerate(conts):
+                        it.enc, it.erow = enc2, i
+        # each group's encoder rows as runs of consecutive rows of the windows' encoder
+        # outputs [(tensor, first row, rows)], copied straight into the slot set's rows by its call
         gencs = []
         for g in groups:
             runs = []
             for it in g or []:
-                src, r = (enc2, ci[id(it)]) if id(it) in ci else (enc1, it.u)
+                src, r = it.enc, it.erow
                 if runs and runs[-1][0] is src and runs[-1][1] + runs[-1][2] == r:
                     runs[-1][2] += 1
                 else:
@@ -817,6 +829,16 @@ class JanusPipeline(PacketRenderer):
         pk_dec = []
         wav_b = pcm_b = None
         with torch.cuda.stream(vs):
+            if late and st["queue"]:
+                # the continuation windows queued by this step's host part, encoded on the
+                # vocoder's CUs (its side has the slack): they enter the next step's call
+                todo = list(st["queue"])
+                st["queue"].clear()
+                mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in todo])
+                enc2 = w.encode(mel2)
+                for i, it in enumerate(todo):
+                    it.enc, it.erow = enc2, i
+                st["ready"].extend(todo)
             if res_prev is not None:
                 pk = res_prev.packets
                 kv = min(len(pk), max(0, self.tuning.voc_dec_utts))
