@@ -198,6 +198,16 @@ __device__ __forceinline__ uint32_t touch_splitk(const _Float16* wt, int K, int 
   return l2_touch(wt + (int64_t)16 * n0 * K, (uint32_t)(n1 - n0 + 1) * 16 * K * 2, p % share, share);
 }
 
+// 256 rows on the 128-block grid (BIG): block b = xcd + 8 j takes column tile
+// n = xcd + 8 (j / 4) and the m-tiles 4 (j % 4) .. + 3 of it, so the four blocks of a column
+// tile sit on one XCD (its weights come into that XCD's L2 once) and each block reads its
+// weight fragments once for four m-tiles
+__device__ __forceinline__ int quad_col() { return (int)(blockIdx.x & 7) + 8 * ((int)(blockIdx.x >> 3) >> 2); }
+__device__ __forceinline__ int quad_m0() { return 4 * (((int)blockIdx.x >> 3) & 3); }
+__device__ __forceinline__ uint32_t touch_quad(const _Float16* wt, int K) {
+  return l2_touch(wt + (int64_t)16 * quad_col() * K, (uint32_t)16 * K * 2, ((int)blockIdx.x >> 3) & 3, 4);
+}
+
 // ------------------------------------------------------------------ split-K phase
 // out[R][512] from A[R][K] . W[512][K]^T: tiles of 16 rows x 16 columns, each over K in
 // four quarters (one wave per quarter), two tiles per block (8 waves); pair p of the
@@ -211,9 +221,9 @@ struct SplitW {
 
 template <int KSW>
 __device__ __forceinline__ void splitk_prefetch(SplitW<KSW>& W, const _Float16* wt, int K,
-                                                int pair, int MT, int lane, int wv) {
+                                                int pair, int MT, int lane, int wv, bool quad = false) {
   const int t = 2 * pair + (wv >> 2), kp = wv & 3;
-  const int n = t / MT;
+  const int n = quad ? quad_col() : t / MT;
   const _Float16* wr = wt + (int64_t)(16 * n + (lane & 15)) * K + kp * (K / 4) + 8 * (lane >> 4);
 #pragma unroll
   for (int s = 0; s < KSW; ++s) W.w[s] = *reinterpret_cast<const half8*>(wr + 32 * s);
@@ -543,29 +553,168 @@ __device__ __forceinline__ void splitk8_pair(const _Float16* wt, int pair, int M
   }
 }
 
-// one pair per block while the grid has at least 16 * MT blocks; two (pairs b and b + G)
-// at MT = 16 on a 128-block grid (dec_seg_grid): the second pair's weights are issued right
-// after the first pair's MFMAs (its pre()), in flight during the first pair's reduction and
-// epilogue. Each tile's arithmetic is the one-pair form's, so a row's result does not depend
-// on how many rows the call carries.
+// BIG (MT = 16 on the 128-block grid): the block's four m-tiles of its column tile (quad_col,
+// quad_m0), wave (tsub, kp) computing k-quarter kp of m-tiles m0 + tsub and m0 + 2 + tsub
+// with ONE set of weight fragments; every load of the phase out before the MFMAs, one
+// reduction of the four tiles. Each tile's arithmetic (k-quarter products, the fixed-order
+// sum ((k0 + k1) + k2) + k3, bias, epilogue) is splitk_pair's.
+template <int KSW, int EPI, bool GROUP, class Pre>
+__device__ __forceinline__ void splitk_quad(const SplitW<KSW>& W, int K, __amdgpu_buffer_rsrc_t ra, int lda,
+                                            const float* bias, __amdgpu_buffer_rsrc_t rx,
+                                            __amdgpu_buffer_rsrc_t ro, float* red, int lane, int wv,
+                                            Pre&& pre, long long* st, int si) {
+  static_assert(KSW <= 8, "quad split-K: A of both m-tiles in registers");
+  const int tsub = wv >> 2, kp = wv & 3;
+  const int n = quad_col(), mq = quad_m0();
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const int acol = (GROUP ? (16 * n / 64) * kD : 0) + kp * (K / 4) + kc8;
+  half8 a[2][KSW];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const uint32_t ab = (uint32_t)(((16 * (mq + 2 * v + tsub) + lr) * lda + acol) * 2);
+#pragma unroll
+    for (int s = 0; s < KSW; ++s) a[v][s] = as_h8(ld_sc1(ra, ab + 64 * s));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc[2] = {zero_f32x4(), zero_f32x4()};
+#pragma unroll
+  for (int s = 0; s < KSW; ++s)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[v] = mfma16(a[v][s], W.w[s], acc[v]);
+  __builtin_amdgcn_sched_barrier(0);  // keep the next phase's loads below the MFMAs
+  pre();
+  __builtin_amdgcn_sched_barrier(0);
+  // red[tile 2v + tsub][kp][16][17]
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    float* rp = red + ((2 * v + tsub) * 4 + kp) * 16 * 17;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rp[(4 * (lane >> 4) + r) * 17 + lr] = acc[v][r];
+  }
+  SEG_STAMP(st, si);
+  __syncthreads();
+  SEG_STAMP(st, si + 1);
+  const int tid = threadIdx.x;
+  if (tid < 256) {
+    const int es = tid >> 6, q = tid & 63;   // tile es = m-tile mq + es
+    const int em = mq + es;
+    const int row = q >> 2, c4 = 4 * (q & 3);
+    const float* r0 = red + (es * 4) * 16 * 17 + row * 17 + c4;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s = r0[i] + r0[16 * 17 + i];
+      s += r0[2 * 16 * 17 + i];
+      s += r0[3 * 16 * 17 + i];
+      v[i] = s + bias[16 * n + c4 + i];
+    }
+    const uint32_t eoff = (uint32_t)((16 * em + row) * kD + 16 * n + c4);
+    if constexpr (EPI == SE_RESID) {
+      const float4 xv = as_f4(ld_sc1(rx, eoff * 4));
+      const float4 y = make_float4(xv.x + v[0], xv.y + v[1], xv.z + v[2], xv.w + v[3]);
+      st_sc1(__builtin_bit_cast(u32x4v, y), rx, eoff * 4);
+    } else {
+      const half4 h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      st_sc1_8(__builtin_bit_cast(u32x2v, h), ro, eoff * 2);
+    }
+  }
+  __syncthreads();  // red is reused by the next phase
+}
+
+// fc2 (K = 4d) on the quads: splitk8_pair's arithmetic for the m-tile pairs (m0, m0 + 1) and
+// (m0 + 2, m0 + 3) of the block's column tile, the weight fragments loaded once; the second
+// pair's activation fragments are issued right after the first pair's MFMAs, in flight during
+// its reduction and epilogue
+template <bool PREV>
+__device__ __forceinline__ void splitk8_quad(const _Float16* wt, __amdgpu_buffer_rsrc_t ra, const float* bias,
+                                             __amdgpu_buffer_rsrc_t rx, float* red, int lane, int wv,
+                                             long long* st, int si) {
+  constexpr int K = 4 * kD, KS = K / 8 / 32;  // 8 k-steps per wave
+  const int n = quad_col(), mq = quad_m0();
+  const int lr = lane & 15, kc8 = 8 * (lane >> 4);
+  const int k0 = wv * (K / 8) + kc8;
+  half8 w[KS], a0[KS], a1[KS];
+  const _Float16* wr = wt + (int64_t)(16 * n + lr) * K + k0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) w[s] = *reinterpret_cast<const half8*>(wr + 32 * s);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int m0 = mq + 2 * v;
+    const uint32_t ab0 = (uint32_t)(((16 * m0 + lr) * K + k0) * 2);
+    const uint32_t ab1 = ab0 + (uint32_t)(16 * K * 2);
+    if (v == 0 || !PREV) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a0[s] = as_h8(ld_sc1(ra, ab0 + 64 * s));
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a1[s] = as_h8(ld_sc1(ra, ab1 + 64 * s));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc0 = zero_f32x4(), acc1 = zero_f32x4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc0 = mfma16(a0[s], w[s], acc0);
+      acc1 = mfma16(a1[s], w[s], acc1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (v == 0 && PREV) {  // the second pair's rows, during this pair's reduction
+      const uint32_t nb0 = ab0 + (uint32_t)(2 * 16 * K * 2), nb1 = nb0 + (uint32_t)(16 * K * 2);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a0[s] = as_h8(ld_sc1(ra, nb0 + 64 * s));
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a1[s] = as_h8(ld_sc1(ra, nb1 + 64 * s));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (v == 1) __syncthreads();  // red of the first pair read
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[((0 * 8 + wv) * 16 + 4 * (lane >> 4) + r) * 17 + lr] = acc0[r];
+      red[((1 * 8 + wv) * 16 + 4 * (lane >> 4) + r) * 17 + lr] = acc1[r];
+    }
+    SEG_STAMP(st, si);
+    __syncthreads();
+    SEG_STAMP(st, si + 1);
+    if (tid < 128) {
+      const int es = tid >> 6, q = tid & 63;
+      const int em = m0 + es;
+      const int row = q >> 2, c4 = 4 * (q & 3);
+      const float* r0 = red + (es * 8) * 16 * 17 + row * 17 + c4;
+      const float4 b4 = *reinterpret_cast<const float4*>(bias + 16 * n + c4);
+      float vv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sum = r0[i];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) sum += r0[k * 16 * 17 + i];
+        vv[i] = sum;
+      }
+      vv[0] += b4.x; vv[1] += b4.y; vv[2] += b4.z; vv[3] += b4.w;
+      const uint32_t eoff = (uint32_t)((16 * em + row) * kD + 16 * n + c4);
+      const float4 xv = as_f4(ld_sc1(rx, eoff * 4));
+      const float4 y = make_float4(xv.x + vv[0], xv.y + vv[1], xv.z + vv[2], xv.w + vv[3]);
+      st_sc1(__builtin_bit_cast(u32x4v, y), rx, eoff * 4);
+    }
+  }
+}
+
+// one pair per block while the grid has at least 16 * MT blocks; BIG (MT = 16 on a
+// 128-block grid, dec_seg_grid): the block's column quad (splitk_quad). Each tile's
+// arithmetic is the one-pair form's, so a row's result does not depend on how many rows the
+// call carries.
 template <int KSW, int EPI, bool GROUP, bool BIG, class Pre>
 __device__ __forceinline__ void splitk_phase(const SplitW<KSW>& W, const _Float16* wt, int K,
                                              int MT, __amdgpu_buffer_rsrc_t ra, int lda,
                                              const float* bias, __amdgpu_buffer_rsrc_t rx,
                                              __amdgpu_buffer_rsrc_t ro, float* red, int lane, int wv,
                                              Pre&& pre, long long* st = nullptr, int si = 0) {
-  const int P = 16 * MT;  // 32 column tiles x MT row tiles / 2
-  const int p0 = blockIdx.x, p1 = p0 + (int)gridDim.x;
-  if (p0 >= P) { pre(); return; }
-  if (!BIG || p1 >= P) {
+  if constexpr (BIG) {
+    splitk_quad<KSW, EPI, GROUP>(W, K, ra, lda, bias, rx, ro, red, lane, wv, pre, st, si);
+  } else {
+    const int p0 = blockIdx.x;
+    if (p0 >= 16 * MT) { pre(); return; }  // 32 column tiles x MT row tiles / 2
     splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre, st, si);
-    return;
   }
-  if constexpr (!BIG) return;
-  SplitW<KSW> W2;
-  splitk_pair<KSW, EPI, GROUP>(W, p0, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true,
-                               [&] { splitk_prefetch<KSW>(W2, wt, K, p1, MT, lane, wv); }, st, si);
-  splitk_pair<KSW, EPI, GROUP>(W2, p1, MT, K, ra, lda, bias, rx, ro, red, lane, wv, true, pre, st, si);
+  (void)wt;
 }
 
 }  // namespace
@@ -620,7 +769,7 @@ __device__ __forceinline__ void seg_a_body(const DecSegArgs& a, float* seg_smem,
   // phase 1: x += o Wo^T + bo (o from the self-attention launch / phase)
   {
     SplitW<4> w;
-    if (first) splitk_prefetch<4>(w, a.wo, kD, blockIdx.x, MT, lane, wv);
+    if (first) splitk_prefetch<4>(w, a.wo, kD, blockIdx.x, MT, lane, wv, BIG);
     splitk_phase<4, SE_RESID, false, BIG>(w, a.wo, kD, MT, rsrc(a.o, (uint32_t)B * kD * 2), kD, a.bo, rx, rx,
                                      red, lane, wv, [] {}, pst, 18);
   }
@@ -653,11 +802,11 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   const auto rom = rsrc(a.omid, (uint32_t)B * kD * 2);
   const bool first = (int)blockIdx.x < 16 * MT;
   sink ^= touched;
-  touched = touch_splitk(a.woc, kD, MT);
+  touched = BIG ? touch_quad(a.woc, kD) : touch_splitk(a.woc, kD, MT);
   // phase 1: o' = c_h Wv_h^T + bv (c from the cross-attention launch), sc1 out
   {
     SplitW<4> w;
-    if (first) splitk_prefetch<4>(w, a.wv, kD, blockIdx.x, MT, lane, wv);
+    if (first) splitk_prefetch<4>(w, a.wv, kD, blockIdx.x, MT, lane, wv, BIG);
     splitk_phase<4, SE_F16_SC1, true, BIG>(w, a.wv, kD, MT, rsrc(a.xc, (uint32_t)B * 8 * kD * 2), 8 * kD, a.bv,
                                       rx, rom, red, lane, wv, [] {}, pst, 18);
   }
@@ -667,12 +816,12 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   // phase 2: x += o' Wo_c^T + bo_c
   {
     SplitW<4> w;
-    if (first) splitk_prefetch<4>(w, a.woc, kD, blockIdx.x, MT, lane, wv);
+    if (first) splitk_prefetch<4>(w, a.woc, kD, blockIdx.x, MT, lane, wv, BIG);
     splitk_phase<4, SE_RESID, false, BIG>(w, a.woc, kD, MT, rom, kD, a.boc, rx, rx, red, lane, wv, [] {}, pst, 21);
   }
   grid_barrier(a.bar, e0 + 2, a.err, st);
   sink ^= touched;
-  touched = touch_splitk(a.w2, 4 * kD, MT);
+  touched = BIG ? touch_quad(a.w2, 4 * kD) : touch_splitk(a.w2, 4 * kD, MT);
   // phase 3: f = gelu(LN3(x) W1^T + b1), sc1 out
   {
     LngW w;
@@ -689,11 +838,7 @@ __device__ __forceinline__ void seg_b_body(const DecSegArgs& a, float* seg_smem,
   // 16 k-steps per quarter when the pair spans two column tiles, MT = 1)
   if (MT % 2 == 0) {
     if constexpr (BIG) {
-      // two pairs per block (MT = 16 on a 128-block grid): the reduction tile is reused
-      for (int p = blockIdx.x; p < 16 * MT; p += gridDim.x) {
-        if (p != (int)blockIdx.x) __syncthreads();
-        splitk8_pair(a.w2, p, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
-      }
+      splitk8_quad<false>(a.w2, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
     } else if (first) {
       splitk8_pair(a.w2, blockIdx.x, MT, rsrc(a.f, (uint32_t)B * 4 * kD * 2), a.b2, rx, red, lane, wv, pst, 27);
     }
@@ -991,7 +1136,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_layer_kernel(DecSegArgs bsg, DecSe
   seg_b_body<BIG>(bsg, seg_smem, st, nullptr, 0, touched, sink);
   grid_barrier(bsg.bar, 5, bsg.err, st);
   sink ^= touched;
-  touched = touch_splitk(nx.wo, kD, bsg.MT);
+  touched = BIG ? touch_quad(nx.wo, kD) : touch_splitk(nx.wo, kD, bsg.MT);
   attn_phase<BIG>(bsg, seg_smem, lane, wv);
   grid_barrier(bsg.bar, 6, bsg.err, st);
   DecSegArgs asg = bsg;
@@ -1030,7 +1175,7 @@ __global__ __launch_bounds__(kNT, 4) void dec_head_kernel(DecSegArgs g) {
                         [] {}, nullptr, 30);
   }
   grid_barrier(g.bar, 1, g.err, st);
-  touched = touch_splitk(g.wo, kD, g.MT);
+  touched = BIG ? touch_quad(g.wo, kD) : touch_splitk(g.wo, kD, g.MT);
   attn_phase<BIG>(g, seg_smem, lane, wv);
   grid_barrier(g.bar, 2, g.err, st);
   seg_a_body<BIG>(g, seg_smem, st, nullptr, 2, touched, sink);
