@@ -546,11 +546,46 @@ def run_config5(args, rank, world, use_dist, dev):
     phrase's duration). After the run every rank's per-block push latencies and
     per-phrase duplex latencies (phrase complete -> packet + rendered audio) are
     all-gathered (RCCL), so rank 0 reports the node's p50 / p99 and whether every block
-    and phrase stayed inside the 320 ms block."""
+    and phrase stayed inside the 320 ms block. Two legs, the same channels: faster-whisper's
+    temperature fallback (the reference's transcribe_buffer, engine.py:510-527: the line's
+    value) and T = 0 alone (``t0``); --stream-t0 runs the T = 0 leg only."""
+    from janus_amd.services.transcriber import TEMPERATURES
+    legs = [("t0", (0.0,))] if args.stream_t0 else [("fallback", TEMPERATURES), ("t0", (0.0,))]
+    res = {name: _stream_leg(args, rank, world, use_dist, dev, temps) for name, temps in legs}
+    if rank != 0:
+        return
+    main_leg = res[legs[0][0]]
+    out = {"metric": "config 5: streaming duplex, 16 kHz channels x 320 ms chunks, per-phrase "
+                     "encode+decode p50 latency (phrase complete -> packet + rendered audio)",
+           "value": main_leg["phrase_p50_ms"], "unit": "ms", "n_gpus": world,
+           "steps": main_leg["blocks"], "warmup": 4, "ms_per_step": main_leg["p50_ms"],
+           "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+           "data": "synthetic seeded speech phrases with silences per channel; energy speech "
+                   "gate; seeded synthetic weights",
+           "config": {"workload": f"{args.streams * world} channels ({args.streams} per GPU, channel s "
+                                  f"on rank s mod {world}), {args.seconds:g} s of {args.block_ms} ms "
+                                  "blocks in real time", "model": args.model,
+                      "streams_total": args.streams * world, "parallelism": f"dp{world}",
+                      "max_length": args.max_length},
+           "streams_total": args.streams * world, "streams_per_gpu": args.streams,
+           "block_ms": args.block_ms, "asynchronous": bool(args.stream_async),
+           "duplex": bool(args.duplex), "leg": legs[0][0]}
+    out.update(main_leg)
+    if len(legs) > 1:
+        out["t0"] = res["t0"]
+    out["roofline"] = None
+    out["roofline_note"] = ("real-time arrival: per-phrase batches of a few 1.5-6 s phrases, "
+                            "latency-bound; the kernels' rooflines are the config-4 line's")
+    out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
+def _stream_leg(args, rank, world, use_dist, dev, temps):
+    """One config-5 run at the temperatures ``temps``: per-block push and per-phrase duplex
+    latencies gathered over the ranks (rank 0's dict; None elsewhere)."""
     from janus_amd.streaming import CHUNK, StreamingEncoder
     from janus_amd.whisper import CONFIGS, WhisperEngine
     from janus_amd.workload import channel_audio, synth_speech
-    from janus_amd.services.transcriber import TEMPERATURES
     per_block = int(round(args.block_ms / 32.0))          # 1536 samples = 32 ms
     n_blocks = int(args.seconds * 1000 / args.block_ms)
     total = n_blocks * per_block * CHUNK
@@ -559,9 +594,6 @@ def run_config5(args, rank, world, use_dist, dev):
     audio = np.stack([channel_audio(s, total) for s in mine])
     S = len(mine)
     w = WhisperEngine(CONFIGS[args.model], seed=0)
-    # the reference's decode semantics by default (transcribe_buffer -> transcribe with
-    # faster-whisper's temperature fallback, engine.py:510-527); --stream-t0: T = 0 only
-    temps = (0.0,) if args.stream_t0 else TEMPERATURES
     rx = None
     if args.duplex:
         from janus_amd.pipeline import PacketRenderer
@@ -590,6 +622,7 @@ def run_config5(args, rank, world, use_dist, dev):
     phrases += len(enc.flush())
     t_total = time.perf_counter() - t_start
     enc.close()
+    warm.close()
     lat, plat = list(enc.latencies), list(enc.phrase_latencies)
     counts = [phrases, enc.max_queue, enc.extra_windows]
     if use_dist:
@@ -601,41 +634,25 @@ def run_config5(args, rank, world, use_dist, dev):
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
         t_total = float(wall.item())
     if rank != 0:
-        return
+        return None
     lat = np.array(lat) * 1000.0
     plat = np.array(plat) * 1000.0 if len(plat) else np.zeros(1)
     p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
     pp50, pp99 = float(np.percentile(plat, 50)), float(np.percentile(plat, 99))
-    out = {"metric": "config 5: streaming duplex, 16 kHz channels x 320 ms chunks, per-phrase "
-                     "encode+decode p50 latency (phrase complete -> packet + rendered audio)",
-           "value": round(pp50, 2), "unit": "ms", "n_gpus": world, "steps": n_blocks, "warmup": 4,
-           "ms_per_step": round(p50, 3), "higher_is_better": False, "scaling": "weak",
-           "vs_baseline": None, "dtype": "fp16",
-           "data": "synthetic seeded speech phrases with silences per channel; energy speech "
-                   "gate; seeded synthetic weights",
-           "config": {"workload": f"{n_total} channels ({args.streams} per GPU, channel s on "
-                                  f"rank s mod {world}), {args.seconds:g} s of {args.block_ms} ms "
-                                  "blocks in real time", "model": args.model,
-                      "streams_total": n_total, "parallelism": f"dp{world}",
-                      "max_length": args.max_length},
-           "streams_total": n_total, "streams_per_gpu": args.streams, "block_ms": args.block_ms,
-           "blocks": n_blocks, "phrases": int(counts[0]),
-           "asynchronous": bool(args.stream_async), "duplex": bool(args.duplex),
-           # per-block push latency (gate + segmentation of every channel's 320 ms block)
-           "p50_ms": round(p50, 2), "p99_ms": round(p99, 2), "max_ms": round(float(lat.max()), 2),
-           # per-phrase duplex latency (phrase complete -> packet + rendered audio)
-           "phrase_p50_ms": round(pp50, 2), "phrase_p99_ms": round(pp99, 2),
-           "phrase_max_ms": round(float(plat.max()), 2),
-           "worker_max_queue": int(counts[1]), "wall_s": round(t_total, 2),
-           "audio_s": round(n_blocks * args.block_ms / 1000.0, 2),
-           "realtime": bool(p99 < args.block_ms and pp99 < args.block_ms),
-           "fallback": not args.stream_t0, "temperatures": list(temps),
-           "extra_seek_windows": int(counts[2]),
-           "roofline": None,
-           "roofline_note": "real-time arrival: per-phrase batches of a few 1.5-6 s phrases, "
-                            "latency-bound; the kernels' rooflines are the config-4 line's",
-           "cpu_baseline": None}
-    print(json.dumps(out), flush=True)
+    return {"temperatures": list(temps), "fallback": len(temps) > 1, "blocks": n_blocks,
+            "phrases": int(counts[0]),
+            # per-block push latency (gate + segmentation of every channel's 320 ms block)
+            "p50_ms": round(p50, 2), "p99_ms": round(p99, 2), "max_ms": round(float(lat.max()), 2),
+            # per-phrase duplex latency (phrase complete -> packet + rendered audio)
+            "phrase_p50_ms": round(pp50, 2), "phrase_p99_ms": round(pp99, 2),
+            "phrase_max_ms": round(float(plat.max()), 2),
+            "worker_max_queue": int(counts[1]), "wall_s": round(t_total, 2),
+            "audio_s": round(n_blocks * args.block_ms / 1000.0, 2),
+            "realtime": bool(p99 < args.block_ms and pp99 < args.block_ms),
+            # the worker kept up: every phrase encoded + rendered before the stream ended plus
+            # one block, queue bounded
+            "kept_up": bool(t_total < n_blocks * args.block_ms / 1000.0 + args.block_ms / 1000.0 * 2),
+            "extra_seek_windows": int(counts[2])}
 
 
 def run_launch_check(args, rank, world):
