@@ -624,12 +624,12 @@ def _stream_leg(args, rank, world, use_dist, dev, temps):
     enc.close()
     warm.close()
     lat, plat = list(enc.latencies), list(enc.phrase_latencies)
-    counts = [phrases, enc.max_queue, enc.extra_windows]
+    counts = [phrases, enc.max_queue, enc.extra_windows, getattr(enc, "worker_batches", 0)]
     if use_dist:
         from janus_amd.dist import gather_values
         lat, plat = gather_values(lat, dev), gather_values(plat, dev)
         per_rank = gather_values(counts, dev)
-        counts = [sum(per_rank[0::3]), max(per_rank[1::3]), sum(per_rank[2::3])]
+        counts = [sum(per_rank[0::4]), max(per_rank[1::4]), sum(per_rank[2::4]), sum(per_rank[3::4])]
         wall = torch.tensor([t_total], dtype=torch.float64, device=dev)
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
         t_total = float(wall.item())
@@ -646,7 +646,9 @@ def _stream_leg(args, rank, world, use_dist, dev, temps):
             # per-phrase duplex latency (phrase complete -> packet + rendered audio)
             "phrase_p50_ms": round(pp50, 2), "phrase_p99_ms": round(pp99, 2),
             "phrase_max_ms": round(float(plat.max()), 2),
-            "worker_max_queue": int(counts[1]), "wall_s": round(t_total, 2),
+            "worker_max_queue": int(counts[1]),
+            # worker batches (jobs queued while one ran are merged into the next batch)
+            "worker_batches": int(counts[3]), "wall_s": round(t_total, 2),
             "audio_s": round(n_blocks * args.block_ms / 1000.0, 2),
             "realtime": bool(p99 < args.block_ms and pp99 < args.block_ms),
             # the worker kept up: every phrase encoded + rendered before the stream ended plus

@@ -19,6 +19,9 @@
 //
 // Accumulation order: one fp32 accumulator per output, k-steps of 32 in order — the same
 // MFMA sequence per output as gemm_nt_kernel (gemm.hip), so the two are bit-identical.
+#include <cstring>
+
+#include "common.h"
 #include "mfma.h"
 #include "kernels.h"
 
@@ -32,6 +35,7 @@ constexpr int kStageHalves = (kBM + kBN) * kBK; // one buffer: A tile then B til
 constexpr int kEP = 68;                         // epilogue fp32 pitch (64 + 4)
 constexpr int kEpWave = 64 * kEP;               // floats per wave in the epilogue image
 constexpr int kSmemBytes = 8 * kEpWave * 4 > 2 * kStageHalves * 2 ? 8 * kEpWave * 4 : 2 * kStageHalves * 2;
+constexpr bool kGemmBigPhased = false;          // the default schedule (A/B: JANUS_GEMM_BIG)
 }  // namespace
 
 // DMA one 8-row x 128-B piece per wave-instruction: lane l -> row (l >> 3) of the piece,
@@ -171,6 +175,190 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Phased schedule (r06): the same 256 x 256 x 64 tiles, MFMA sequence per output and
+// epilogue, but the 128 KB of LDS is eight 16-KB HALF-TILE slots (A rows 0-127 / 128-255,
+// W rows 0-127 / 128-255 of one k-tile; k-tile t in slots 4 (t & 1) + h) and each k-tile is
+// three phases, so a slot is restaged for k-tile t + 2 as soon as its last fragment read
+// of k-tile t has retired — not after the whole k-tile. Wave (wr, wc) owns rows
+// mh·128 + wr·64 + [0, 64) and columns nh·128 + wc·32 + [0, 32) (mh, nh in {0, 1}), so
+// output quadrant (mh, nh) of every wave reads A half mh and W half nh only:
+//   phase 0: read A0, W0 -> quadrant (0, 0);  issue A1(t + 1)
+//   phase 1: read W1      -> quadrant (0, 1);  issue A0(t + 2), W0(t + 2)
+//   phase 2: read A1      -> quadrants (1, 1), (1, 0) (W0 still in registers);  issue W1(t + 2)
+// Every half-tile is DMA'd 4-7 phases ahead of its first read (≈ 80-112 KB in flight per
+// CU instead of one 64 KB k-tile drained to zero at every k-tile), retired by a counted
+// vmcnt before the raw s_barrier that ends the phase ahead of its first read. A slot's
+// restage is issued after the barrier that follows its last read (every fragment read of a
+// phase is consumed by that phase's MFMAs, so the reads have retired at the barrier).
+// The per-output k order is unchanged: bit-identical to gemm_big_kernel / gemm_nt_kernel.
+namespace {
+constexpr int kHalf = 128 * kBK;   // halves per slot
+}
+
+template <int N_>
+__device__ __forceinline__ void vm_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N_) : "memory");   // + this wave's reads
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_big_phased_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
+  _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / kBN, nbm = (M + kBM - 1) / kBM;
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int row0 = bm * kBM, col0 = bn * kBN;
+  const int lane = threadIdx.x & 63, wid = wave_id();
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // DMA half h of k-tile t into its slot: wave w takes rows [16w, 16w + 16) of the half
+  auto stage = [&](int t, int h) {
+    _Float16* dst = smem + ((t & 1) * 4 + h) * kHalf;
+    const bool a = h < 2;
+    const int base = (a ? row0 : col0) + (h & 1) * 128, lim = (a ? M : N) - 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rl = wid * 16 + i * 8;
+      glds_rows8(a ? p.A : p.W, a ? p.lda : p.ldw, base + rl, rl, lim, t * kBK, dst + rl * kBK, lane);
+    }
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[i][j][m][n] = zero_f32x4();
+
+  const int fr = lane & 15, sw = fr >> 1;
+  const int a_off = (wr * 64 + fr) * kBK, b_off = (wc * 32 + fr) * kBK;
+  half8 fa[4][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](const _Float16* slot) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) fa[m][s] = *reinterpret_cast<const half8*>(slot + a_off + m * 16 * kBK + ch);
+    }
+  };
+  auto read_b = [&](const _Float16* slot, half8 (&fb)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = ((4 * s + (lane >> 4)) ^ sw) * 8;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) fb[n][s] = *reinterpret_cast<const half8*>(slot + b_off + n * 16 * kBK + ch);
+    }
+  };
+  auto quad = [&](f32x4 (&c)[4][2], half8 (&fb)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) c[m][n] = mfma16(fa[m][s], fb[n][s], c[m][n]);
+  };
+
+  const int nk = K / kBK;
+  // prologue: k-tile 0 whole, then A0 W0 W1 of k-tile 1 (its A1 goes out in k-tile 0's
+  // phase 0); wait for A0(0), W0(0)
+  stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+  if (nk > 1) {
+    stage(1, 0); stage(1, 2); stage(1, 3);
+    vm_wait_barrier<10>();
+  } else {
+    vm_wait_barrier<4>();
+  }
+  for (int t = 0; t < nk; ++t) {
+    const _Float16* sl = smem + (t & 1) * 4 * kHalf;
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    // phase 0
+    if (more1) stage(t + 1, 1);
+    read_a(sl);
+    read_b(sl + 2 * kHalf, fb0);
+    quad(acc[0][0], fb0);
+    if (more1) vm_wait_barrier<10>(); else vm_wait_barrier<2>();   // W1(t)
+    // phase 1
+    if (more2) { stage(t + 2, 0); stage(t + 2, 2); }
+    read_b(sl + 3 * kHalf, fb1);
+    quad(acc[0][1], fb1);
+    if (more2) vm_wait_barrier<12>(); else if (more1) vm_wait_barrier<8>(); else vm_wait_barrier<0>();  // A1(t)
+    // phase 2
+    if (more2) stage(t + 2, 3);
+    read_a(sl + kHalf);
+    quad(acc[1][1], fb1);
+    quad(acc[1][0], fb0);
+    if (more2) vm_wait_barrier<10>(); else if (more1) vm_wait_barrier<4>(); else vm_wait_barrier<0>();  // A0, W0(t + 1)
+  }
+
+  // epilogue (the staging image is free: every DMA retired, every read consumed), two
+  // passes (mh) of 64 rows per wave; image column v < 32 is the wave's nh = 0 group,
+  // v >= 32 its nh = 1 group
+  float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
+  const int er = lane >> 3, ec = (lane & 7) * 8;
+  const int gcol = col0 + (ec >> 5) * 128 + wc * 32 + (ec & 31);
+  float bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = p.bias ? p.bias[gcol + j] : 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sC[(m * 16 + (lane >> 4) * 4 + r) * kEP + nh * 32 + n * 16 + fr] = acc[h][nh][m][n][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    float4 res[8][2];
+    if constexpr (EPI == EPI_RESID_F32) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = min(row0 + h * 128 + wr * 64 + it * 8 + er, M - 1);
+        res[it][0] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol);
+        res[it][1] = *reinterpret_cast<const float4*>(p.R + (int64_t)row * p.ldr + gcol + 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + er;
+      const int row = row0 + h * 128 + wr * 64 + lr;
+      const float4 lo = *reinterpret_cast<const float4*>(sC + lr * kEP + ec);
+      const float4 hi = *reinterpret_cast<const float4*>(sC + lr * kEP + ec + 4);
+      float v[8] = {lo.x + bias[0], lo.y + bias[1], lo.z + bias[2], lo.w + bias[3],
+                    hi.x + bias[4], hi.y + bias[5], hi.z + bias[6], hi.w + bias[7]};
+      if (row < M) {
+        if constexpr (EPI == EPI_F16 || EPI == EPI_GELU_F16) {
+          half8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (_Float16)(EPI == EPI_GELU_F16 ? gelu_erf(v[j]) : v[j]);
+          *reinterpret_cast<half8*>(static_cast<_Float16*>(p.C) + (int64_t)row * p.ldc + gcol) = o;
+        } else {
+          float* c = static_cast<float*>(p.C) + (int64_t)row * p.ldc + gcol;
+          if constexpr (EPI == EPI_RESID_F32) {
+            v[0] += res[it][0].x; v[1] += res[it][0].y; v[2] += res[it][0].z; v[3] += res[it][0].w;
+            v[4] += res[it][1].x; v[5] += res[it][1].y; v[6] += res[it][1].z; v[7] += res[it][1].w;
+          }
+          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 bool gemm_big_supported(int epi, const GemmArgs& p) {
   if (!(epi == EPI_F16 || epi == EPI_GELU_F16 || epi == EPI_RESID_F32 || epi == EPI_F32)) return false;
   if (p.M < kBM || p.N % kBN != 0 || p.K % kBK != 0 || p.K < kBK) return false;
@@ -184,6 +372,18 @@ bool gemm_big_supported(int epi, const GemmArgs& p) {
 void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
   const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
+  const char* v = ab_env("JANUS_GEMM_BIG");   // A/B builds only: "dbuf" | "phased"
+  const bool phased = v ? std::strcmp(v, "phased") == 0 : kGemmBigPhased;
+  if (phased) {
+    switch (epi) {
+      case EPI_F16: gemm_big_phased_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_GELU_F16: gemm_big_phased_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_RESID_F32: gemm_big_phased_kernel<EPI_RESID_F32><<<blocks, kThreads, 0, s>>>(p); break;
+      default: gemm_big_phased_kernel<EPI_F32><<<blocks, kThreads, 0, s>>>(p); break;
+    }
+    JANUS_LAUNCH_CHECK();
+    return;
+  }
   switch (epi) {
     case EPI_F16: gemm_big_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
     case EPI_GELU_F16: gemm_big_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;

@@ -373,12 +373,14 @@ def gather_windows(items, n_frames: int = N_FRAMES, device=None):
 
 
 def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448,
-                      temperatures=TEMPERATURES, best_of: int = BEST_OF):
+                      temperatures=TEMPERATURES, best_of: int = BEST_OF, utt_keys=None):
     """faster-whisper's seek loop for several 16 kHz utterances at once: every round
     decodes the current window of each unfinished utterance as one GPU batch (per-row
     prompts), then the temperature fallback of the windows whose gates failed
-    (``temperatures`` = (0.0,) disables it). Returns one _Stream (segments + gate counters)
-    per utterance."""
+    (``temperatures`` = (0.0,) disables it). ``utt_keys``: the utterance numbers the
+    fallback seeds are keyed on (default: the index in ``audios``; a caller that batches
+    the same utterances differently passes stable numbers to draw the same noise).
+    Returns one _Stream (segments + gate counters) per utterance."""
     temperatures = tuple(float(t) for t in temperatures)
     if not temperatures or temperatures[0] != 0.0:
         raise NotImplementedError("the first temperature must be 0 (faster-whisper's default)")
@@ -406,7 +408,7 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
             enc = engine.encode(mel)
             prompts = [s.prompt(tk, max_length) for s in grp]
             out = engine.decode_ex(enc, prompts=prompts, max_length=max_length)
-            keys = [(i, s.windows) for i, s in zip(idx, grp)]
+            keys = [(i if utt_keys is None else int(utt_keys[i]), s.windows) for i, s in zip(idx, grp)]
             first, final, ndec = settle_round(engine, tk, out.rows(), prompts, keys, enc, max_length,
                                               temperatures, best_of)
             n_tok = out.n_tokens.cpu().numpy()

@@ -38,6 +38,7 @@ SILENCE_THRESHOLD_CHUNKS = 15  # engine.py:441
 MIN_PHRASE_SAMPLES = CHUNK * 6  # engine.py:504
 CAPTURE_RATE = 48000
 WINDOW_16K = 480000           # one 30 s Whisper window at 16 kHz
+MERGE_PHRASES = 256           # asynchronous worker: most phrases merged into one batch
 
 class PhraseSegmenter:
     """engine.py:438-506 for one channel: feed every chunk with its gate decision; returns
@@ -132,6 +133,8 @@ class StreamingEncoder:
         self.receiver = receiver    # JanusPipeline-like .decode(packets, frames), or None
         self.asynchronous = asynchronous
         self.max_queue = 0
+        self._serial = 0      # phrases completed so far (all channels)
+        self.worker_batches = 0     # asynchronous worker: batches run (merged jobs count once)
         self.long_phrases = 0       # phrases over one 30 s window
         self.extra_windows = 0      # seek-loop windows beyond each phrase's first
         if asynchronous:
@@ -160,7 +163,8 @@ class StreamingEncoder:
                 ph = self.segmenters[s].push(host[s, j * CHUNK:(j + 1) * CHUNK], bool(speech[s, j]),
                                              non_vad_mode=non_vad)
                 if ph is not None:
-                    done.append((s, ph))
+                    done.append((s, ph, self._serial))
+                    self._serial += 1
         if self.asynchronous:
             if self._error is not None:
                 raise RuntimeError("streaming worker failed") from self._error
@@ -175,14 +179,17 @@ class StreamingEncoder:
         return out
 
     def _job(self, done, timestamp, t_submit):
+        """Encode (+ render) one batch of completed phrases; t_submit: the push time of the
+        phrases' block, one value or one per phrase (merged jobs)."""
         res = self._encode(done, timestamp)
         if self.receiver is not None:
             self._render(res, done)
         torch.cuda.current_stream(self.device).synchronize()
         t = time.perf_counter()
-        for r in res:
-            r["latency_s"] = t - t_submit
-            self.phrase_latencies.append(t - t_submit)
+        subs = t_submit if isinstance(t_submit, list) else [t_submit] * len(res)
+        for r, t0 in zip(res, subs):
+            r["latency_s"] = t - t0
+            self.phrase_latencies.append(t - t0)
         return res
 
     def _render(self, res, done):
@@ -191,7 +198,7 @@ class StreamingEncoder:
         pk = [r["packet"] for r in res]
         if not any(p is not None for p in pk):
             return
-        secs = max(len(ph) for _, ph in done) / CAPTURE_RATE
+        secs = max(len(d[1]) for d in done) / CAPTURE_RATE
         frames = max(1, int(np.ceil(secs * 44100 / 512)))
         wav, pcm, _ = self.receiver.decode(pk, frames)
         k = 0
@@ -201,18 +208,51 @@ class StreamingEncoder:
                 k += 1
 
     def _run(self):
+        """The worker: every job queued while the previous one ran is merged into ONE batch
+        (one batched generate_segments for all of them: a worker that fell behind catches up
+        with bigger batches instead of a growing queue), in queue order, up to MERGE_PHRASES
+        phrases; a channel with several phrases in the batch runs them through its YIN
+        state in order (_encode's prosody rounds), and every packet keeps its own block's
+        timestamp and every latency its own push time."""
         torch.cuda.set_device(self.device)
-        while True:
-            job = self._jobs.get()
-            try:
+        pending = deque()
+        stop = False
+        while not (stop and not pending):
+            if not pending:
+                job = self._jobs.get()
                 if job is None:
+                    self._jobs.task_done()
                     return
+                pending.append(job)
+            while True:   # everything queued meanwhile
+                try:
+                    job = self._jobs.get_nowait()
+                except queue.Empty:
+                    break
+                if job is None:
+                    self._jobs.task_done()
+                    stop = True
+                    break
+                pending.append(job)
+            done, stamps, subs, taken = [], [], [], 0
+            for jd, ts, t0 in pending:
+                if taken and len(done) + len(jd) > MERGE_PHRASES:
+                    break
+                done += jd
+                stamps += [ts] * len(jd)
+                subs += [t0] * len(jd)
+                taken += 1
+            ts = stamps[0] if taken == 1 else stamps
+            self.worker_batches += 1
+            try:
                 with torch.cuda.stream(self._side):
-                    self._results.put(self._job(*job))
+                    self._results.put(self._job(done, ts, subs))
             except BaseException as e:  # surfaced by the next push
                 self._error = e
             finally:
-                self._jobs.task_done()
+                for _ in range(taken):
+                    pending.popleft()
+                    self._jobs.task_done()
 
     def _drain(self):
         out = []
@@ -237,9 +277,10 @@ class StreamingEncoder:
             self._worker.join()
 
     def _encode(self, done, timestamp):
-        streams = [s for s, _ in done]
-        lengths = [len(p) for _, p in done]
-        pcm_np = np.concatenate([p for _, p in done] + [np.zeros(1, np.float32)]).astype(np.float32)
+        streams = [d[0] for d in done]
+        lengths = [len(d[1]) for d in done]
+        serials = [d[2] for d in done]   # stable phrase numbers: the fallback's seed keys
+        pcm_np = np.concatenate([d[1] for d in done] + [np.zeros(1, np.float32)]).astype(np.float32)
         pcm = torch.from_numpy(pcm_np).to(self.device)
         offs_np = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
         offs = torch.from_numpy(offs_np).to(self.device)
@@ -254,7 +295,7 @@ class StreamingEncoder:
         from .services.transcriber import generate_segments
         auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in range(B)]
         streams_st = generate_segments(w, auds, max_length=self.max_length,
-                                       temperatures=self.temperatures)
+                                       temperatures=self.temperatures, utt_keys=serials)
         texts = [' '.join(sg.text.strip() for sg in st.segments).strip() for st in streams_st]
         self.long_phrases += sum(1 for n in lengths if (n + 2) // 3 > WINDOW_16K)
         self.extra_windows += sum(st.windows - 1 for st in streams_st)
@@ -289,9 +330,11 @@ class StreamingEncoder:
                     tags[i] = t
         except Exception:                               # engine.py:520-525
             tags = [{"energy": "Normal", "pitch": "Normal"} for _ in range(B)]
-        ts = time.time() if timestamp is None else timestamp
+        stamps = timestamp if isinstance(timestamp, list) else [timestamp] * B
+        now = time.time()
         res = []
-        for s, t, g in zip(streams, texts, tags):
+        for s, t, g, ts in zip(streams, texts, tags, stamps):
+            ts = now if ts is None else ts
             pkt = JanusPacket(t, self.mode, g, self.override, ts).serialize() if t.strip() else None
             res.append({"stream": s, "text": t, "tags": g, "packet": pkt})
         return res
