@@ -377,6 +377,22 @@ int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* enc, int ba
                                    void* stream);
 
 /*
+ * janus_whisper_decode_sample_ex with a temperature per row: temperatures [host] f32 [B],
+ * each >= 0 (0: a greedy row, as janus_whisper_decode_greedy_ex; its seed is ignored).
+ * Row b's tokens equal those of a greedy / decode_sample_ex call at temperatures[b] with
+ * the same seed (rows are independent of their batch neighbours), so a window's T = 0 row
+ * and the hypotheses of every fallback temperature can run in ONE call and the caller keeps
+ * exactly what the sequential generate_with_fallback walk (transcriber.py:53-57,
+ * faster-whisper's temperature loop) keeps: janus_amd/services/transcriber.py
+ * generate_segments(speculative=True), the streaming encoder's setting.
+ */
+int janus_whisper_decode_sample_rows_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                        const janus_decode_options* opt, const janus_decode_rows* rows,
+                                        const float* temperatures, const uint32_t* seeds,
+                                        int32_t* tokens, int32_t* n_tokens, float* sum_logprob,
+                                        float* no_speech_prob, void* stream);
+
+/*
  * Shape of the last decode call on this context (lane 0): positions the decoder stepped
  * (every row together; the early-exit poll stops at a 16-position boundary) and the
  * kernel launches those positions issued (nodes of the captured decode graphs; 0 when

@@ -89,9 +89,11 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                            LogitPart* parts, hipStream_t s,
                            const float* lnx = nullptr, int ldx = 0, const float* ln_g = nullptr,
                            const float* ln_b = nullptr, int max_blocks = 256,
-                           const uint32_t* seeds = nullptr, int pos = 0);
+                           const uint32_t* seeds = nullptr, int pos = 0,
+                           const float* row_inv_temp = nullptr);
 // R.inv_temp > 0: seeds [B] (device) per-row noise seeds, pos = the position whose logits
-// these are (the sampled token goes to pos + 1)
+// these are (the sampled token goes to pos + 1); row_inv_temp [B] (device, nullable): row
+// b samples at 1 / row_inv_temp[b] instead of R.inv_temp (several temperatures in one call)
 // plen [B] (device, nullable = all rows sample from pos + 1 >= 1): rows with pos + 1 <
 // plen[b] are still inside their own prompt and keep the forced token. At a row's first
 // sampled step (pos + 1 == plen[b]) nsp[b] (nullable) gets the raw softmax probability of

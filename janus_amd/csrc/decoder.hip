@@ -407,7 +407,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     DecodeRules R, const uint8_t* __restrict__ smask, const RowRules* __restrict__ rules,
     LogitPart* __restrict__ parts, int ntiles, const float* __restrict__ lnx, int ldx,
     const float* __restrict__ ln_g, const float* __restrict__ ln_b, int rot,
-    const uint32_t* __restrict__ seeds, int pos) {
+    const uint32_t* __restrict__ seeds, int pos, const float* __restrict__ rinv) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lg_smem[];
   JANUS_DEC_WAVE_PRIO();
   // row group blockIdx.y: rows [64 y, 64 y + 64) of the call (one launch for every group:
@@ -419,6 +419,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
     parts += (int64_t)r0 * gridDim.x;
     if (lnx) lnx += (int64_t)r0 * ldx;
     if (seeds) seeds += r0;
+    if (rinv) rinv += r0;
     B = min(64, B - r0);
   }
   constexpr int K = NKS * 32;
@@ -477,6 +478,9 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
   RowRules rr;  // lane = row in the statistics pass (fields copied: no scratch for pad[])
   rr.sample_begin = sR[lane].sample_begin; rr.suppress_all_ts = sR[lane].suppress_all_ts;
   rr.suppress_text = sR[lane].suppress_text; rr.ts_floor = sR[lane].ts_floor;
+  // this row's 1 / T (sampling): per row when the call mixes temperatures; 0 = a greedy
+  // row (key = logit, as the greedy kernel)
+  const float inv_t = SAMPLE && rinv ? rinv[min(lane, B - 1)] : R.inv_temp;
   // running statistics of this wave's tiles for row = lane
   float m_all = -INFINITY, s_all = 0.f, m_text = -INFINITY, m_ts = -INFINITY, s_ts = 0.f;
   float ba_v = -INFINITY, bt_v = -INFINITY;
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
       if constexpr (SAMPLE) {
         for (int c = 0; c < 16; ++c) {
           if (!((okm >> c) & 1u)) continue;
-          const float key = vals[c] * R.inv_temp + sample_gumbel(nb, col0 + c);
+          const float key = inv_t > 0.f ? vals[c] * inv_t + sample_gumbel(nb, col0 + c) : vals[c];
           if (better(key, col0 + c, ba_v, ba_i)) { ba_v = key; ba_i = col0 + c; ba_r = vals[c]; }
         }
       } else {
@@ -597,7 +601,7 @@ __global__ __launch_bounds__(lg_waves(NKS * 32) * 64) void logits_partial_kernel
         const float v = vals[c];
         u_all += __expf(v - t_all);
         // sampling: the key (perturbed logit) is compared, the logit kept beside it
-        const float key = SAMPLE ? v * R.inv_temp + sample_gumbel(nb, t) : v;
+        const float key = SAMPLE && inv_t > 0.f ? v * inv_t + sample_gumbel(nb, t) : v;
         if (better(key, t, ba_v, ba_i)) { ba_v = key; ba_i = t; ba_r = v; }
         if (R.ts_begin >= 0 && t >= R.ts_begin) {
           u_ts += __expf(v - t_ts);
@@ -647,7 +651,7 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
                            const DecodeRules& R, const uint8_t* smask, const RowRules* rules,
                            LogitPart* parts, hipStream_t s, const float* lnx, int ldx,
                            const float* ln_g, const float* ln_b, int max_blocks,
-                           const uint32_t* seeds, int pos) {
+                           const uint32_t* seeds, int pos, const float* row_inv_temp) {
   JANUS_CHECK(K == 384 || K == 512 || K == 768, "logits: K (d_model) must be 384, 512 or 768");
   const bool sample = R.inv_temp > 0.f;
   JANUS_CHECK(!sample || seeds, "logits: sampling needs per-row seeds");
@@ -689,7 +693,8 @@ void logits_partial_launch(const _Float16* A, int lda, const _Float16* W, int K,
   }
   // 64 rows per row group (blockIdx.y), every group in one launch
   kern<<<dim3(grid, (B + 63) / 64), nw * 64, lds, s>>>(A, lda, W, V, B, R, smask, rules, parts, ntiles, lnx, ldx,
-                                                      ln_g, ln_b, rot, seeds, pos);
+                                                      ln_g, ln_b, rot, seeds, pos,
+                                                      sample ? row_inv_temp : nullptr);
   JANUS_LAUNCH_CHECK();
 }
 

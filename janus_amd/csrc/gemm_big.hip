@@ -36,6 +36,7 @@ constexpr int kEP = 68;                         // epilogue fp32 pitch (64 + 4)
 constexpr int kEpWave = 64 * kEP;               // floats per wave in the epilogue image
 constexpr int kSmemBytes = 8 * kEpWave * 4 > 2 * kStageHalves * 2 ? 8 * kEpWave * 4 : 2 * kStageHalves * 2;
 constexpr bool kGemmBigPhased = false;          // the default schedule (A/B: JANUS_GEMM_BIG)
+constexpr int kEpiNone = 99;                    // A/B timing builds: no epilogue (wrong output)
 }  // namespace
 
 // DMA one 8-row x 128-B piece per wave-instruction: lane l -> row (l >> 3) of the piece,
@@ -116,6 +117,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_kernel(GemmArgs p) {
     __syncthreads();
   }
 
+  if constexpr (EPI == kEpiNone) {   // timing ablation: keep the accumulators alive only
+    float t = 0.0f;
+#pragma unroll
+    for (int m = 0; m < kWMT; ++m)
+#pragma unroll
+      for (int n = 0; n < kWNT; ++n) t += acc[m][n][0] + acc[m][n][3];
+    if (t == 1234.5f) static_cast<float*>(p.C)[threadIdx.x] = t;
+    return;
+  }
   // epilogue, two passes of 64 rows per wave through the wave's own LDS image
   float* sC = reinterpret_cast<float*>(smem_raw) + wid * kEpWave;
   const int er = lane >> 3, ec = (lane & 7) * 8;           // 8 rows x 8 lanes per pass step
@@ -203,7 +213,7 @@ __device__ __forceinline__ void vm_wait_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int EPI>
+template <int EPI, bool PRIO>
 __global__ __launch_bounds__(kThreads, 1) void gemm_big_phased_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem_raw[kSmemBytes];
   _Float16* smem = reinterpret_cast<_Float16*>(smem_raw);
@@ -258,12 +268,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_phased_kernel(GemmArgs p
     }
   };
   auto quad = [&](f32x4 (&c)[4][2], half8 (&fb)[2][2]) {
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n) c[m][n] = mfma16(fa[m][s], fb[n][s], c[m][n]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   const int nk = K / kBK;
@@ -298,6 +310,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_big_phased_kernel(GemmArgs p
     if (more2) vm_wait_barrier<10>(); else if (more1) vm_wait_barrier<4>(); else vm_wait_barrier<0>();  // A0, W0(t + 1)
   }
 
+  if constexpr (EPI == kEpiNone) {
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) t += acc[i][j][m][n][0] + acc[i][j][m][n][3];
+    if (t == 1234.5f) static_cast<float*>(p.C)[threadIdx.x] = t;
+    return;
+  }
   // epilogue (the staging image is free: every DMA retired, every read consumed), two
   // passes (mh) of 64 rows per wave; image column v < 32 is the wave's nh = 0 group,
   // v >= 32 its nh = 1 group
@@ -372,14 +397,33 @@ bool gemm_big_supported(int epi, const GemmArgs& p) {
 void gemm_big_launch(int epi, const GemmArgs& p, hipStream_t s) {
   JANUS_CHECK(gemm_big_supported(epi, p), "gemm_big: unsupported shape / layout");
   const unsigned blocks = (unsigned)(cdiv(p.M, kBM) * (p.N / kBN));
-  const char* v = ab_env("JANUS_GEMM_BIG");   // A/B builds only: "dbuf" | "phased"
-  const bool phased = v ? std::strcmp(v, "phased") == 0 : kGemmBigPhased;
+  const char* v = ab_env("JANUS_GEMM_BIG");   // A/B builds: dbuf | phased | phased_prio [_noepi]
+  const bool phased = v ? std::strncmp(v, "phased", 6) == 0 : kGemmBigPhased;
+  if (v && std::strstr(v, "_noepi")) {
+    if (!phased) gemm_big_kernel<kEpiNone><<<blocks, kThreads, 0, s>>>(p);
+    else gemm_big_phased_kernel<kEpiNone, false><<<blocks, kThreads, 0, s>>>(p);
+    JANUS_LAUNCH_CHECK();
+    return;
+  }
   if (phased) {
+    const bool prio = v && std::strcmp(v, "phased_prio") == 0;
     switch (epi) {
-      case EPI_F16: gemm_big_phased_kernel<EPI_F16><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_GELU_F16: gemm_big_phased_kernel<EPI_GELU_F16><<<blocks, kThreads, 0, s>>>(p); break;
-      case EPI_RESID_F32: gemm_big_phased_kernel<EPI_RESID_F32><<<blocks, kThreads, 0, s>>>(p); break;
-      default: gemm_big_phased_kernel<EPI_F32><<<blocks, kThreads, 0, s>>>(p); break;
+      case EPI_F16:
+        if (prio) gemm_big_phased_kernel<EPI_F16, true><<<blocks, kThreads, 0, s>>>(p);
+        else gemm_big_phased_kernel<EPI_F16, false><<<blocks, kThreads, 0, s>>>(p);
+        break;
+      case EPI_GELU_F16:
+        if (prio) gemm_big_phased_kernel<EPI_GELU_F16, true><<<blocks, kThreads, 0, s>>>(p);
+        else gemm_big_phased_kernel<EPI_GELU_F16, false><<<blocks, kThreads, 0, s>>>(p);
+        break;
+      case EPI_RESID_F32:
+        if (prio) gemm_big_phased_kernel<EPI_RESID_F32, true><<<blocks, kThreads, 0, s>>>(p);
+        else gemm_big_phased_kernel<EPI_RESID_F32, false><<<blocks, kThreads, 0, s>>>(p);
+        break;
+      default:
+        if (prio) gemm_big_phased_kernel<EPI_F32, true><<<blocks, kThreads, 0, s>>>(p);
+        else gemm_big_phased_kernel<EPI_F32, false><<<blocks, kThreads, 0, s>>>(p);
+        break;
     }
     JANUS_LAUNCH_CHECK();
     return;

@@ -65,7 +65,9 @@ struct LaneArrival {
 struct DecLane {
   DevMem d_x, d_a, d_qkv, d_o, d_q2, d_f, d_kc, d_vc, d_ck, d_cv, d_smask, d_done, d_prompt, d_nsp,
       d_supp, d_part_o, d_part_ml, d_parts, d_rules, d_tok, d_ntok, d_slp, d_lnp, d_lncnt, d_xqk,
-      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups, d_roff, d_omid, d_segbar, d_segerr;
+      d_xc, d_xpc, d_xpml, d_enc, d_seed, d_xpairs, d_xgroups, d_roff, d_omid, d_segbar, d_segerr,
+      d_itemp;
+  std::vector<float> h_itemp;    // per-row 1 / T of the last call (source of an async copy)
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
   std::map<std::vector<int64_t>, size_t> graph_nodes;  // kernel nodes per captured graph
   int last_positions = 0;        // positions the last decode stepped
@@ -299,6 +301,7 @@ static uint32_t float_bits(float f) {
 struct DecodeSampling {
   float temperature;
   const uint32_t* seeds;
+  const float* temps = nullptr;   // host [B], per-row temperatures (overrides temperature)
 };
 
 static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, int B, const janus_decode_options* opt,
@@ -506,6 +509,16 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     JANUS_CHECK(smp->seeds, "decode: sampling needs per-row seeds");
     JANUS_HIP(hipMemcpyAsync(Z.d_seed.p, smp->seeds, sizeof(uint32_t) * B, hipMemcpyHostToDevice, s));
   }
+  const bool row_temps = sampling && smp->temps;
+  if (row_temps) {
+    Z.h_itemp.resize(B);
+    for (int b = 0; b < B; ++b) {
+      JANUS_CHECK(smp->temps[b] >= 0.f, "decode: per-row temperatures must be >= 0");
+      Z.h_itemp[b] = smp->temps[b] > 0.f ? 1.0f / smp->temps[b] : 0.f;   // 0: a greedy row
+    }
+    Z.d_itemp.ensure(sizeof(float) * B);
+    JANUS_HIP(hipMemcpyAsync(Z.d_itemp.p, Z.h_itemp.data(), sizeof(float) * B, hipMemcpyHostToDevice, s));
+  }
   if (opt->n_suppress > 0)
     JANUS_HIP(hipMemcpyAsync(Z.d_supp.p, opt->suppress, sizeof(int32_t) * opt->n_suppress,
                              hipMemcpyHostToDevice, s));
@@ -546,7 +559,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
   R.no_timestamps = opt->no_timestamps;
   R.max_initial_ts = opt->max_initial_timestamp_index;
   R.target = rows ? rows->no_speech_token : -1;
-  R.inv_temp = sampling ? 1.0f / smp->temperature : 0.f;
+  // per-row temperatures: R.inv_temp only selects the sampling kernel (rows read their own)
+  R.inv_temp = !sampling ? 0.f : smp->temps ? 1.0f : 1.0f / smp->temperature;
   const float scale = 0.125f;
   const float* pos_emb = w->params.get("decoder.embed_positions.weight", (int64_t)NC * d);
   std::vector<int32_t> h_done(B);
@@ -832,7 +846,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
     logits_partial_launch(a, d, w->tok16.as<_Float16>(), d, V, B, R, Z.d_smask.as<uint8_t>(),
                           Z.d_rules.as<RowRules>(), Z.d_parts.as<LogitPart>(), s,
                           lnp_fin ? x : nullptr, d, fin_g, fin_b, lg_cap,
-                          sampling ? Z.d_seed.as<uint32_t>() : nullptr, pos);
+                          sampling ? Z.d_seed.as<uint32_t>() : nullptr, pos,
+                          row_temps ? Z.d_itemp.as<float>() : nullptr);
     if (fuse_se && pos + 1 < maxlen - 1)
       select_embed_launch(Z.d_parts.as<LogitPart>(), nblk, R, Z.d_rules.as<RowRules>(), tokens,
                           maxlen, pos, done, sum_lp, n_tokens, B, s, Z.d_prompt.as<int32_t>(),
@@ -855,7 +870,8 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       (int64_t)Z.d_xc.p, (int64_t)Z.d_xpc.p, (int64_t)Z.d_xpml.p, (int64_t)enc, (int64_t)tokens, (int64_t)done, (int64_t)sum_lp,
       (int64_t)n_tokens, (int64_t)Z.d_smask.p, R.eot, R.ts_begin, R.suppress_blank, R.blank,
       R.no_timestamps, R.max_initial_ts, R.target, (int64_t)Z.d_prompt.p, (int64_t)Z.d_nsp.p,
-      (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)xpairs,
+      (int64_t)sampling, (int64_t)float_bits(R.inv_temp), (int64_t)Z.d_seed.p, (int64_t)row_temps,
+      (int64_t)Z.d_itemp.p, (int64_t)xpairs,
       (int64_t)npairs, (int64_t)xgroups, (int64_t)ngroups, (int64_t)grp_rows, (int64_t)roff,
       (int64_t)max_roff, (int64_t)persist + (int64_t)layerk + (int64_t)xfuse, (int64_t)seg_grid, (int64_t)Z.d_omid.p, (int64_t)Z.d_segbar.p,
       (int64_t)Z.d_segerr.p};
@@ -1051,6 +1067,26 @@ extern "C" int janus_whisper_decode_sample_ex(janus_whisper* w, const uint16_t* 
                       &smp);
 }
 
+extern "C" int janus_whisper_decode_sample_rows_ex(janus_whisper* w, const uint16_t* enc, int batch,
+                                                   const janus_decode_options* opt,
+                                                   const janus_decode_rows* rows, const float* temperatures,
+                                                   const uint32_t* seeds, int32_t* tokens,
+                                                   int32_t* n_tokens, float* sum_logprob,
+                                                   float* no_speech_prob, void* stream) {
+  if (!temperatures || !seeds || batch <= 0) {
+    set_error("decode_sample_rows: temperatures and seeds must be non-null");
+    return -1;
+  }
+  for (int b = 0; b < batch; ++b)
+    if (!(temperatures[b] >= 0.f)) {
+      set_error("decode_sample_rows: every temperature must be >= 0");
+      return -1;
+    }
+  const DecodeSampling smp{1.0f, seeds, temperatures};
+  return decode_entry(w, enc, batch, opt, rows, tokens, n_tokens, sum_logprob, no_speech_prob, stream,
+                      &smp);
+}
+
 extern "C" int janus_whisper_decode_stand_slot(janus_whisper* w, int slot, int32_t* stand, int batch) {
   return guarded([&] {
     JANUS_CHECK(w && stand, "null argument");
@@ -1167,7 +1203,7 @@ static int decode_entry(janus_whisper* w, const uint16_t* enc, int batch,
           }
         }
         DecodeSampling ssub{};
-        if (smp) ssub = DecodeSampling{smp->temperature, smp->seeds + b0};
+        if (smp) ssub = DecodeSampling{smp->temperature, smp->seeds + b0, smp->temps ? smp->temps + b0 : nullptr};
         decode_greedy(w, Z, e + (int64_t)b0 * w->cfg.n_audio_ctx * w->cfg.d_model, b1 - b0, opt,
                       rows ? &sub : nullptr, tokens + (int64_t)b0 * maxlen, n_tokens + b0,
                       sum_logprob + b0, no_speech_prob ? no_speech_prob + b0 : nullptr, Z.stream,

@@ -254,15 +254,28 @@ class _Stream:
 
 
 def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, best_of,
-              enc_rows=None, **dec_kw):
+              enc_rows=None, presampled=None, **dec_kw):
     """Run the temperature fallback for the windows of one round: first [Candidate] (T = 0
     results), keys [(utt, window)]; returns each window's settled Candidate. The
     hypotheses of every window still failing at a temperature go out as one sampled batch
     (chunks of FALLBACK_ROWS rows). ``enc_rows``: window j's encoder output is enc[enc_rows[j]]
-    (default enc[j])."""
+    (default enc[j]). ``presampled[j][ti - 1]``: window j's best_of hypothesis rows at
+    temperatures[ti], already decoded (generate_segments(speculative=True)): the walk keeps
+    the same candidates the sequential decodes would give (rows are independent of their
+    batch neighbours and every draw is keyed by (utt, window, ti, h))."""
     er = list(range(len(first))) if enc_rows is None else list(enc_rows)
     results = [[c] for c in first]
     final = [settle(r, temperatures) if not r[0].needs_fallback else None for r in results]
+    if presampled is not None:
+        for j in range(len(first)):
+            for ti in range(1, len(temperatures)):
+                if final[j] is not None:
+                    break
+                toks, avg_lp, nsp = best_hypothesis(presampled[j][ti - 1])
+                results[j].append(candidate(tk, toks, avg_lp, nsp, float(temperatures[ti])))
+                if not results[j][-1].needs_fallback or ti == len(temperatures) - 1:
+                    final[j] = settle(results[j], temperatures)
+        return final, [len(r) - 1 for r in results]
     # the shared-encoder PAIR path (H <= 8, d <= 512) reads each window's output in place;
     # wider models gather one encoder copy per hypothesis row (0.74 GB per 320 rows at
     # d = 768), so their sampled decodes stay at FALLBACK_ROWS_GATHER rows
@@ -293,7 +306,7 @@ def _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures, b
 
 
 def settle_round(engine, tk, rows, prompts, keys, enc, max_length, temperatures=(0.0,),
-                 best_of: int = BEST_OF, enc_rows=None, **dec_kw):
+                 best_of: int = BEST_OF, enc_rows=None, presampled=None, **dec_kw):
     """One round of generate_with_fallback: ``rows`` the T = 0 decode of the round's windows
     ([(tokens, avg_logprob, no_speech_prob)], DecodeOut.rows()), ``prompts`` / ``keys`` [(utt, window)] per window,
     ``enc`` the windows' encoder output (enc[enc_rows[j]] for window j). Returns (first,
@@ -302,7 +315,7 @@ def settle_round(engine, tk, rows, prompts, keys, enc, max_length, temperatures=
     first = [candidate(tk, toks, avg_lp, nsp, 0.0) for (toks, avg_lp, nsp) in rows]
     if len(temperatures) > 1:
         final, ndec = _fallback(engine, tk, enc, prompts, first, keys, max_length, temperatures,
-                                best_of, enc_rows=enc_rows, **dec_kw)
+                                best_of, enc_rows=enc_rows, presampled=presampled, **dec_kw)
     else:
         final, ndec = first, [0] * len(first)
     return first, final, ndec
@@ -373,13 +386,19 @@ def gather_windows(items, n_frames: int = N_FRAMES, device=None):
 
 
 def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_length: int = 448,
-                      temperatures=TEMPERATURES, best_of: int = BEST_OF, utt_keys=None):
+                      temperatures=TEMPERATURES, best_of: int = BEST_OF, utt_keys=None,
+                      speculative: bool = False):
     """faster-whisper's seek loop for several 16 kHz utterances at once: every round
     decodes the current window of each unfinished utterance as one GPU batch (per-row
     prompts), then the temperature fallback of the windows whose gates failed
     (``temperatures`` = (0.0,) disables it). ``utt_keys``: the utterance numbers the
     fallback seeds are keyed on (default: the index in ``audios``; a caller that batches
     the same utterances differently passes stable numbers to draw the same noise).
+    ``speculative``: each round decodes every window's T = 0 row AND the best_of hypotheses
+    of every fallback temperature in ONE call (per-row temperatures), then walks the
+    temperatures exactly as the sequential fallback does — the same results for one decode
+    call's latency instead of up to len(temperatures) in a row, at (1 + 5 x 5) rows per
+    window (the streaming encoder's setting: a few phrases at a time, latency-bound).
     Returns one _Stream (segments + gate counters) per utterance."""
     temperatures = tuple(float(t) for t in temperatures)
     if not temperatures or temperatures[0] != 0.0:
@@ -396,6 +415,10 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
         pcm = torch.from_numpy(np.concatenate([st.audio, np.zeros(1, np.float32)])).to(dev)
         offs = torch.tensor([0, len(st.audio)], dtype=torch.int64, device=dev)
         feats.append(engine.logmel_frames(pcm, offs, 1, 1, st.content_frames))
+    spec = speculative and len(temperatures) > 1
+    per_row = 1 + (len(temperatures) - 1) * best_of          # rows per window, speculative
+    if spec:
+        max_batch = max(1, min(max_batch, FALLBACK_ROWS // per_row))
     while True:
         act = [i for i, s in enumerate(streams) if s.active]
         if not act:
@@ -407,11 +430,31 @@ def generate_segments(engine: WhisperEngine, audios, max_batch: int = 64, max_le
             mel = gather_windows([(feats[i], 0, s.seek, size) for i, s, size in zip(idx, grp, sizes)])
             enc = engine.encode(mel)
             prompts = [s.prompt(tk, max_length) for s in grp]
-            out = engine.decode_ex(enc, prompts=prompts, max_length=max_length)
             keys = [(i if utt_keys is None else int(utt_keys[i]), s.windows) for i, s in zip(idx, grp)]
-            first, final, ndec = settle_round(engine, tk, out.rows(), prompts, keys, enc, max_length,
-                                              temperatures, best_of)
-            n_tok = out.n_tokens.cpu().numpy()
+            pres = None
+            if spec:
+                temps, seeds, eidx, rprom = [], [], [], []
+                for j, key in enumerate(keys):
+                    temps.append(0.0)
+                    seeds.append(0)
+                    for ti in range(1, len(temperatures)):
+                        temps += [float(temperatures[ti])] * best_of
+                        seeds += [fallback_seed(key[0], key[1], ti, h) for h in range(best_of)]
+                    eidx += [j] * per_row
+                    rprom += [prompts[j]] * per_row
+                out = engine.decode_ex(enc, prompts=rprom, max_length=max_length, temperature=temps,
+                                       seeds=seeds, enc_index=eidx)
+                allr = out.rows()
+                t0 = [allr[j * per_row] for j in range(len(grp))]
+                pres = [[allr[j * per_row + 1 + (ti - 1) * best_of: j * per_row + 1 + ti * best_of]
+                         for ti in range(1, len(temperatures))] for j in range(len(grp))]
+                n_tok = out.n_tokens.cpu().numpy()[0::per_row]
+            else:
+                out = engine.decode_ex(enc, prompts=prompts, max_length=max_length)
+                t0 = out.rows()
+                n_tok = out.n_tokens.cpu().numpy()
+            first, final, ndec = settle_round(engine, tk, t0, prompts, keys, enc, max_length,
+                                              temperatures, best_of, presampled=pres)
             for s, size, c0r, r, nd, nt in zip(grp, sizes, first, final, ndec, n_tok):
                 advance(tk, s, size, c0r, r, nd, nt)
     return streams

@@ -294,8 +294,12 @@ class StreamingEncoder:
         # in the following round of the same batched loop
         from .services.transcriber import generate_segments
         auds = [np.ascontiguousarray(pcm_np[offs_np[i]:offs_np[i] + lengths[i]][::3]) for i in range(B)]
+        # speculative: every phrase window's T = 0 row and all its fallback hypotheses in one
+        # decode call (the same results as the sequential temperature walk, one decode's
+        # latency: a phrase waits for one call, not up to six in a row)
         streams_st = generate_segments(w, auds, max_length=self.max_length,
-                                       temperatures=self.temperatures, utt_keys=serials)
+                                       temperatures=self.temperatures, utt_keys=serials,
+                                       speculative=True)
         texts = [' '.join(sg.text.strip() for sg in st.segments).strip() for st in streams_st]
         self.long_phrases += sum(1 for n in lengths if (n + 2) // 3 > WINDOW_16K)
         self.extra_windows += sum(st.windows - 1 for st in streams_st)

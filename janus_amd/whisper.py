@@ -353,7 +353,9 @@ class WhisperEngine:
         """janus_whisper_decode_greedy_ex: per-row prompts (lists of token ids; None = the
         SOT sequence for every row) and the no-speech probability. Returns a DecodeOut.
         temperature > 0 samples instead (janus_whisper_decode_sample_ex: Gumbel-max over the
-        rule-filtered logits / T with per-row uint32 ``seeds``). ``enc_index`` (one int per
+        rule-filtered logits / T with per-row uint32 ``seeds``); a sequence of temperatures
+        (one per row, each >= 0; 0 = a greedy row) samples row b at temperature[b] in the
+        same call (janus_whisper_decode_sample_rows_ex). ``enc_index`` (one int per
         decoder row): row b attends to enc[enc_index[b]] — the best_of hypotheses of a
         window share its encoder output, read once per pair of rows. ``pos_offset`` /
         ``steps`` (greedy): a staggered call — row b runs ``steps`` positions from
@@ -370,6 +372,12 @@ class WhisperEngine:
             raise ValueError("steps must be >= 0")
         if steps and pos_offset is None:
             raise ValueError("steps applies to a staggered call (pos_offset) only")
+        row_t = None
+        if not np.isscalar(temperature):
+            row_t = np.ascontiguousarray(np.asarray(temperature, np.float32))
+            if row_t.shape != (B,) or not (row_t >= 0).all():
+                raise ValueError("per-row temperatures: one value >= 0 per row")
+            temperature = 1.0
         if temperature > 0:
             if seeds is None or len(seeds) != B:
                 raise ValueError("sampling needs one uint32 seed per row")
@@ -409,7 +417,12 @@ class WhisperEngine:
         ntok = torch.empty(B, dtype=torch.int32, device=self.device)
         slp = torch.empty(B, dtype=torch.float32, device=self.device)
         nsp = torch.empty(B, dtype=torch.float32, device=self.device)
-        if temperature > 0:
+        if row_t is not None:
+            nat.call("janus_whisper_decode_sample_rows_ex", self._h, enc.data_ptr(), B,
+                     ctypes.addressof(opt), ctypes.addressof(rows), row_t.ctypes.data,
+                     sd.ctypes.data, tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
+                     nsp.data_ptr(), nat.stream_ptr())
+        elif temperature > 0:
             nat.call("janus_whisper_decode_sample_ex", self._h, enc.data_ptr(), B,
                      ctypes.addressof(opt), ctypes.addressof(rows), ctypes.c_float(temperature),
                      sd.ctypes.data, tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
@@ -418,7 +431,7 @@ class WhisperEngine:
             nat.call("janus_whisper_decode_greedy_ex", self._h, enc.data_ptr(), B, ctypes.addressof(opt),
                      ctypes.addressof(rows), tokens.data_ptr(), ntok.data_ptr(), slp.data_ptr(),
                      nsp.data_ptr(), nat.stream_ptr())
-        del keep, pr, ei, po
+        del keep, pr, ei, po, row_t
         return DecodeOut(tokens, ntok, slp, nsp, plens)
 
     def decode_stand(self, batch: int, state_slot: int = 0):

@@ -370,6 +370,50 @@ def test_seek_loop_matches_oracle(engine, gpu, temps):
               f"{st.fallbacks} failed at T=0, {st.fallback_decodes} sampled decodes")
 
 
+def test_seek_loop_speculative_matches_sequential(engine, gpu):
+    """generate_segments(speculative=True) — each round's T = 0 rows and every fallback
+    temperature's best_of hypotheses in ONE decode call (per-row temperatures) — gives
+    exactly the sequential temperature walk's result: segments, tokens, windows, gate and
+    fallback counters (the streaming encoder's setting)."""
+    from janus_amd.services.transcriber import TEMPERATURES, generate_segments
+    eng, _ = engine
+    auds = [synth_speech(160, 40.0, sr=16000), synth_speech(161, 7.0, sr=16000),
+            synth_speech(162, 3.0, sr=16000)]
+    res = {}
+    for spec in (False, True):
+        res[spec] = generate_segments(eng, auds, max_length=64, temperatures=TEMPERATURES,
+                                      speculative=spec, utt_keys=[11, 12, 13])
+    for a, b in zip(res[False], res[True]):
+        assert [(s.start, s.end, s.text, list(s.tokens), s.temperature) for s in a.segments] == \
+            [(s.start, s.end, s.text, list(s.tokens), s.temperature) for s in b.segments]
+        assert (a.windows, a.fallbacks, a.skips, a.fallback_decodes, a.sampled) == \
+            (b.windows, b.fallbacks, b.skips, b.fallback_decodes, b.sampled)
+        assert a.window_tokens == b.window_tokens and a.window_rows == b.window_rows
+    assert sum(s.fallback_decodes for s in res[True]) > 0
+
+
+def test_per_row_temperatures_match_scalar(engine, gpu):
+    """janus_whisper_decode_sample_rows_ex: rows at different temperatures (0 = greedy) in
+    one call decode bit-identically to the greedy call and to one scalar-temperature call
+    per temperature with the same seeds and shared encoder rows."""
+    eng, _ = engine
+    utts = [synth_speech(330 + k, 3.0 + 2 * k) for k in range(3)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    ei = [0, 0, 0, 1, 1, 2, 2, 2]
+    temps = [0.0, 0.2, 1.0, 0.0, 0.6, 0.2, 0.0, 1.0]
+    seeds = [500 + 7 * b for b in range(len(ei))]
+    mix = eng.decode_ex(enc, max_length=40, temperature=temps, seeds=seeds, enc_index=ei)
+    got = [t.cpu() for t in (mix.tokens, mix.n_tokens, mix.sum_logprob, mix.no_speech_prob)]
+    for T in sorted(set(temps)):
+        rows = [b for b in range(len(ei)) if temps[b] == T]
+        kw = dict(temperature=T, seeds=[seeds[b] for b in rows]) if T > 0 else {}
+        ref = eng.decode_ex(enc, max_length=40, enc_index=[ei[b] for b in rows], **kw)
+        want = [t.cpu() for t in (ref.tokens, ref.n_tokens, ref.sum_logprob, ref.no_speech_prob)]
+        for g, w_ in zip(got, want):
+            assert torch.equal(g[rows], w_), T
+
+
 def test_sample_noise_matches_oracle(gpu):
     """The decoder's Gumbel noise (janus_sample_gumbel_f32: the hash and -log(-log u) the
     sampling logits kernel adds) equals the oracle's restatement (float64 logs) to f32
