@@ -966,14 +966,17 @@ class JanusPipeline(PacketRenderer):
     def _yin_split(self, st, B):
         """Utterances whose YIN runs on the decoder side in the staggered step. Fixed by
         tuning.yin_dec_utts; otherwise self-balancing: starts at 7B/8 (where it settled on
-        the r04 boxes: 52-59 of 64) and moves by the previous full step's side-time gap
+        the r04 boxes: 52-59 of 64) when the decoder call leaves room for YIN beside it (at
+        most 128 rows), at 0 when it does not (every window decoded: 256 rows, the decoder
+        side binds and YIN after its call would lengthen it — r06 traces showed the 7B/8
+        start needing four steps to walk down), and moves by the previous full step's side-time gap
         (vocoder side minus decoder side, HIP events on the two CU-masked streams) over
         twice the per-utterance YIN time, at most 16 per step,
         so the two partitions finish together whatever the box's vocoder / decoder speed
         ratio (measured from box to box: vocoder side 253-265 ms at the same split)."""
         if self.tuning.yin_dec_utts is not None:
             return max(0, min(B - 1, self.tuning.yin_dec_utts))
-        n = st.get("n_dec", 7 * B // 8)
+        n = st.get("n_dec", 7 * B // 8 if st["n"] * st["R"] <= 128 else 0)
         prev = st.get("prev_ev")
         if prev is not None and prev[1].query() and prev[3].query():
             gap = prev[0].elapsed_time(prev[1]) - prev[2].elapsed_time(prev[3])
