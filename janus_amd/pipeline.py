@@ -65,6 +65,12 @@ class ServingTuning:
     yin_beside_blocks: int = 128    # overlapped step, yin_side "beside": its grid cap
     xattn_splits: Optional[int] = None  # cross-attention key splits (None: 1 staggered, 4 else)
     dec_path_flags: int = 0         # staggered decoder: janus_decode_options.path_flags (A/Bs)
+    logits_blocks: int = 0          # staggered decoder: vocabulary-projection blocks per row
+                                    # group of 64 (janus_decode_options.logits_blocks; 0: the
+                                    # decoder's CUs / row groups, so every group runs in ONE
+                                    # round and its blocks of a vocabulary slice share an L2:
+                                    # 32 at 256 rows, +1.6 % xRT against one block per CU,
+                                    # DESIGN.md §5h)
     fallback_full: bool = True      # overlapped step: seek rounds / fallback on the whole GPU
     fallback_xattn_splits: int = 4
     host_prefetch: bool = True      # staggered: D2H of the completed windows behind their call
@@ -938,9 +944,13 @@ class JanusPipeline(PacketRenderer):
         if g is not None:
             for j, it in enumerate(g):
                 prompts[f * B + j] = it.prompt
+        lgb = self.tuning.logits_blocks
+        if lgb <= 0:   # one round: the decoder's CUs over the call's 64-row groups
+            lgb = max(8, (self._dec_s.n_cus // ((n * B + 63) // 64)) // 8 * 8)
         dec = w.decode_ex(st["enc"], prompts=prompts, max_length=L, pos_offset=offs, steps=S,
                           xattn_splits=self._xsplits(1), cu_count=self._dec_s.n_cus,
-                          persistent=self.tuning.persistent, path_flags=self.tuning.dec_path_flags)
+                          persistent=self.tuning.persistent, path_flags=self.tuning.dec_path_flags,
+                          logits_blocks=lgb)
         st["started"] = True
         # where each set's rows stand now (offset + S, or fewer when every row finished and
         # the call stopped early), as the context recorded it
