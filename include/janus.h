@@ -411,6 +411,15 @@ int janus_whisper_decode_info(janus_whisper* w, int32_t* positions, int64_t* lau
  */
 int janus_whisper_decode_stand(janus_whisper* w, int32_t* stand, int batch);
 /* The same for decoder state slot `slot` (janus_decode_options.state_slot). */
+/*
+ * A call with janus_decode_options.check_every = 0 (no early-exit polling) returns as soon
+ * as its work is enqueued, without waiting for the stream; the persistent segments' grid
+ * barrier timeout (a resident grid that never became co-resident) is then reported here:
+ * waits for the last such call of state slot `slot` and returns non-zero (janus_last_error)
+ * if it timed out — call it before using that call's outputs. The lane's next decode call
+ * checks it too. Returns 0 when nothing is pending.
+ */
+int janus_whisper_decode_check(janus_whisper* w, int slot);
 int janus_whisper_decode_stand_slot(janus_whisper* w, int slot, int32_t* stand, int batch);
 
 /* ------------------------------------------------------------ vocoder --- */

@@ -79,6 +79,7 @@ SIGNATURES = {
     "janus_whisper_decode_greedy_ex": [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P],
     "janus_whisper_decode_sample_ex": [_P, _P, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P],
     "janus_whisper_decode_sample_rows_ex": [_P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "janus_whisper_decode_check": [_P, _I32],
     "janus_whisper_decode_info": [_P, _P, _P],
     "janus_whisper_decode_stand": [_P, _P, _I32],
     "janus_whisper_decode_stand_slot": [_P, _I32, _P, _I32],

@@ -81,6 +81,12 @@ struct DecLane {
   hipStream_t stream = nullptr;  // graph capture needs a non-null stream
   std::vector<uint32_t> stream_mask;  // CU mask the lane stream was created with (empty: none)
   hipEvent_t ev_done = nullptr;
+  // a call without early-exit polling (check_every 0) returns without waiting for its
+  // stream: its persistent segments' barrier-timeout flag is copied to pinned h_segerr
+  // behind it and checked by janus_whisper_decode_check (or at this lane's next call)
+  uint32_t* h_segerr = nullptr;
+  hipEvent_t ev_segerr = nullptr;
+  bool segerr_pending = false;
   DecLane() = default;
   DecLane(const DecLane&) = delete;
   DecLane& operator=(const DecLane&) = delete;
@@ -88,6 +94,8 @@ struct DecLane {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     if (stream) (void)hipStreamDestroy(stream);
     if (ev_done) (void)hipEventDestroy(ev_done);
+    if (ev_segerr) (void)hipEventDestroy(ev_segerr);
+    if (h_segerr) (void)hipHostFree(h_segerr);
   }
 };
 
@@ -304,10 +312,25 @@ struct DecodeSampling {
   const float* temps = nullptr;   // host [B], per-row temperatures (overrides temperature)
 };
 
+// The deferred barrier-timeout check of the lane's last non-polling call (check_every 0):
+// waits for that call's flag copy and throws if a persistent segment gave up at a barrier.
+static void lane_check(DecLane& Z) {
+  if (!Z.segerr_pending) return;
+  Z.segerr_pending = false;
+  JANUS_HIP(hipEventSynchronize(Z.ev_segerr));
+  if (*Z.h_segerr) {
+    *Z.h_segerr = 0;
+    JANUS_HIP(hipMemset(Z.d_segbar.p, 0, sizeof(unsigned) * 256));
+    JANUS_HIP(hipMemset(Z.d_segerr.p, 0, 256));
+    throw Error("decode: a persistent decoder segment timed out at a grid barrier (grid not co-resident)");
+  }
+}
+
 static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, int B, const janus_decode_options* opt,
                           const janus_decode_rows* rows, int32_t* tokens_out, int32_t* n_tokens_out,
                           float* sum_lp_out, float* nsp_out, hipStream_t s, LaneLatch* latch,
                           const DecodeSampling* smp = nullptr) {
+  lane_check(Z);   // the previous non-polling call's flag first
   LaneArrival arrival(latch);
   const auto& c = w->cfg;
   const int d = c.d_model, H = c.n_heads, Te = c.n_audio_ctx, V = c.n_vocab, NC = c.n_text_ctx;
@@ -924,7 +947,13 @@ static void decode_greedy(janus_whisper* w, DecLane& Z, const _Float16* enc_in, 
       if (all) break;  // remaining positions keep -1; callers stop at the first eot
     }
   }
-  if (persist) {  // a segment whose grid never became co-resident gave up at a barrier
+  if (persist && opt->check_every <= 0) {   // the check deferred: the call does not wait
+    if (!Z.h_segerr) JANUS_HIP(hipHostMalloc((void**)&Z.h_segerr, sizeof(uint32_t), hipHostMallocDefault));
+    if (!Z.ev_segerr) JANUS_HIP(hipEventCreateWithFlags(&Z.ev_segerr, hipEventDisableTiming));
+    JANUS_HIP(hipMemcpyAsync(Z.h_segerr, Z.d_segerr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    JANUS_HIP(hipEventRecord(Z.ev_segerr, s));
+    Z.segerr_pending = true;
+  } else if (persist) {  // a segment whose grid never became co-resident gave up at a barrier
     uint32_t herr = 0;
     JANUS_HIP(hipMemcpyAsync(&herr, Z.d_segerr.p, sizeof(herr), hipMemcpyDeviceToHost, s));
     JANUS_HIP(hipStreamSynchronize(s));
@@ -1094,6 +1123,15 @@ extern "C" int janus_whisper_decode_stand_slot(janus_whisper* w, int slot, int32
     JANUS_CHECK(slot >= 0 && slot < (int)w->lanes.size() && (int)w->lanes[slot]->stand.size() == batch,
                 "decode_stand: no completed decode of this batch size in this slot");
     std::copy(w->lanes[slot]->stand.begin(), w->lanes[slot]->stand.end(), stand);
+  });
+}
+
+extern "C" int janus_whisper_decode_check(janus_whisper* w, int slot) {
+  return guarded([&] {
+    JANUS_CHECK(w, "null argument");
+    std::lock_guard<std::mutex> lk(w->mu);
+    JANUS_CHECK(slot >= 0 && slot < 8, "decode_check: slot must be 0 .. 7");
+    if (slot < (int)w->lanes.size()) lane_check(*w->lanes[slot]);
   });
 }
 

@@ -443,6 +443,12 @@ class WhisperEngine:
                  int(batch))
         return [int(v) for v in out]
 
+    def decode_check(self, state_slot: int = 0):
+        """janus_whisper_decode_check: raise if the last non-polling call (check_every 0) of
+        decoder state slot ``state_slot`` hit a persistent-segment barrier timeout (waits for
+        that call's flag; nothing pending: returns at once). Call before using its outputs."""
+        nat.call("janus_whisper_decode_check", self._h, int(state_slot))
+
     def decode_info(self):
         """(positions stepped, kernel launches issued) by the last decode call
         (janus_whisper_decode_info: captured graph nodes; measurement only)."""

@@ -414,6 +414,27 @@ def test_per_row_temperatures_match_scalar(engine, gpu):
             assert torch.equal(g[rows], w_), T
 
 
+def test_non_polling_call_matches_polling(base_engine, gpu):
+    """A decode call without early-exit polling (check_every 0: the staggered serving
+    step's calls, which return without waiting for their stream) gives the polling call's
+    rows — tokens up to each row's end, counts, log-prob sums — on the persistent segments,
+    and janus_whisper_decode_check then reports no barrier timeout."""
+    eng, _ = base_engine
+    utts = [synth_speech(340 + k, 2.0 + k) for k in range(4)]
+    pcm, offs = pack(utts, gpu)
+    enc = eng.encode(eng.logmel(pcm, offs, len(utts), 3))
+    a = eng.decode_ex(enc, max_length=48, persistent=2, check_every=16)
+    b = eng.decode_ex(enc, max_length=48, persistent=2, check_every=0)
+    eng.decode_check()
+    torch.cuda.synchronize()
+    plen = len(eng.tokenizer.sot_sequence)
+    assert torch.equal(a.n_tokens.cpu(), b.n_tokens.cpu())
+    assert torch.equal(a.sum_logprob.cpu(), b.sum_logprob.cpu())
+    for r in range(len(utts)):
+        n = plen + int(a.n_tokens[r])
+        assert torch.equal(a.tokens[r, :n].cpu(), b.tokens[r, :n].cpu())
+
+
 def test_sample_noise_matches_oracle(gpu):
     """The decoder's Gumbel noise (janus_sample_gumbel_f32: the hash and -log(-log u) the
     sampling logits kernel adds) equals the oracle's restatement (float64 logs) to f32
