@@ -677,9 +677,10 @@ class JanusPipeline(PacketRenderer):
             items, plens = rec["items"], rec["plens"]
             tok, nt, lp, ns = tok.numpy(), nt.numpy(), lp.numpy(), ns.numpy()
             rows = []
+            eot = w.tokenizer.eot
             for j in range(len(items)):
                 s = tok[j][int(plens[j]):int(plens[j]) + int(nt[j])]
-                s = [int(x) for x in s if x != w.tokenizer.eot]
+                s = s[s != eot].tolist()
                 rows.append((s, float(lp[j]) / (len(s) + 1), float(ns[j])))
             prompts = [it.prompt for it in items]
             keys = [it.key for it in items]

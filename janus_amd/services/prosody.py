@@ -71,7 +71,7 @@ def prosody_launch(pcm: torch.Tensor, sample_offsets: torch.Tensor, lengths, sam
     assert pcm.dtype == torch.float32 and pcm.is_contiguous() and pcm.is_cuda
     ho_np = hop_offsets(lengths, hop)
     total = int(ho_np[-1])
-    hop_off = torch.from_numpy(ho_np).to(dev, non_blocking=True)
+    hop_off = torch.from_numpy(ho_np).pin_memory().to(dev, non_blocking=True)   # no host wait
     f0 = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
     rms = torch.empty(max(B, 1), dtype=torch.float32, device=dev)
     mean_f0 = torch.empty(max(B, 1), dtype=torch.float32, device=dev)

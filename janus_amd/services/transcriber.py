@@ -374,13 +374,15 @@ def gather_windows(items, n_frames: int = N_FRAMES, device=None):
             if n > 0:
                 out[j, :n] = f[row, seek:seek + n]
             continue
-        rows = torch.tensor([r for _, r, _, _ in lst], dtype=torch.int64, device=dev)
-        seeks = torch.tensor([s for _, _, s, _ in lst], dtype=torch.int64, device=dev)
-        sizes = torch.tensor([z for _, _, _, z in lst], dtype=torch.int64, device=dev)
+        # the four index vectors in one pinned host tensor, copied without blocking the host
+        # (a pageable copy would wait for the stream: the serving step's encoder ahead of it)
+        idx = torch.tensor([[r, sk, z, j] for j, r, sk, z in lst], dtype=torch.int64)
+        if dev.type == "cuda":
+            idx = idx.pin_memory().to(dev, non_blocking=True)
+        rows, seeks, sizes, js = idx[:, 0], idx[:, 1], idx[:, 2], idx[:, 3]
         src = seeks[:, None] + t[None, :]
         valid = (t[None, :] < sizes[:, None]) & (src < F)
         g = f[rows[:, None], torch.where(valid, src, 0)]          # [n][n_frames][80]
-        js = torch.tensor([j for j, _, _, _ in lst], dtype=torch.int64, device=dev)
         out[js] = torch.where(valid[..., None], g, torch.zeros((), dtype=g.dtype, device=dev))
     return out
 

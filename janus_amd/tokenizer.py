@@ -92,10 +92,11 @@ class WhisperTokenizer:
         return [inv[b] for b in text.encode("utf-8")]
 
     def decode(self, tokens) -> str:
-        toks = [int(t) for t in tokens if 0 <= int(t) < self.eot]
+        a = np.asarray(tokens, dtype=np.int64).reshape(-1)
+        toks = a[(a >= 0) & (a < self.eot)].tolist()   # text tokens only (vectorised filter)
         if self._hf is not None:
             return self._hf.decode(toks)
-        return b"".join(self._table[t] for t in toks).decode("utf-8", errors="replace")
+        return b"".join(map(self._table.__getitem__, toks)).decode("utf-8", errors="replace")
 
     def non_speech_tokens(self):
         if self._hf is None:

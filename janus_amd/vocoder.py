@@ -185,9 +185,12 @@ class VocoderEngine:
         B = len(prompts)
         offs = np.concatenate([[0], np.cumsum([len(p) for p in prompts])]).astype(np.int64)
         allb = np.frombuffer(b"".join(prompts) + b"\0", np.uint8).copy()
-        d_bytes = torch.from_numpy(allb).to(self.device)
-        d_offs = torch.from_numpy(offs).to(self.device)
-        d_emo = torch.tensor(list(emotions), dtype=torch.int32, device=self.device)
+        # pinned, non-blocking uploads: a pageable copy would hold the host until the stream
+        # reaches it (the serving step issues this behind its encoders)
+        up = lambda a: torch.from_numpy(a).pin_memory().to(self.device, non_blocking=True)  # noqa: E731
+        d_bytes = up(allb)
+        d_offs = up(offs)
+        d_emo = up(np.asarray(list(emotions), np.int32))
         lat = torch.empty(B, frames, self.cfg.latent_dim, dtype=torch.float16, device=self.device)
         spk_ptr = None
         if speaker is not None:
