@@ -65,10 +65,9 @@ class ServingTuning:
     yin_beside_blocks: int = 128    # overlapped step, yin_side "beside": its grid cap
     xattn_splits: Optional[int] = None  # cross-attention key splits (None: 1 staggered, 4 else)
     dec_path_flags: int = 0         # staggered decoder: janus_decode_options.path_flags (A/Bs)
-    dec_first: bool = False         # staggered: the decoder calls issued before the vocoder side
-                                    # (needs dec_poll 0, or the host waits for the decoder first)
     dec_poll: int = 16              # staggered decoder: janus_decode_options.check_every (0: the
-                                    # calls do not wait for their stream)
+                                    # calls do not wait for their stream — measured 50 % slower,
+                                    # DESIGN.md §5h)
     logits_blocks: int = 0          # staggered decoder: vocabulary-projection blocks per row
                                     # group of 64 (janus_decode_options.logits_blocks; 0: the
                                     # decoder's CUs / row groups, so every group runs in ONE
@@ -92,7 +91,7 @@ class ServingTuning:
                 continue
             if f.name in ("yin_side", "cont_encode"):
                 kw[f.name] = v
-            elif f.name in ("fallback_full", "host_prefetch", "side_timing", "all_windows", "dec_first"):
+            elif f.name in ("fallback_full", "host_prefetch", "side_timing", "all_windows"):
                 kw[f.name] = v not in ("", "0")
             else:
                 kw[f.name] = int(v)
@@ -842,79 +841,59 @@ class JanusPipeline(PacketRenderer):
         kv = 0
         pk_dec = []
         wav_b = pcm_b = None
-        # issue order of the two sides (tuning.dec_first) and whether the decoder calls wait
-        # for their stream (tuning.dec_poll, janus_decode_options.check_every)
-        box = {"pres_dec": None, "dec_yin": False, "pres": pres, "busy": False}
-
-        def dec_side():
-            busy = any(g is not None for g in groups) or any(x is not None for x in st["sets"])
-            if busy:
-                with torch.cuda.stream(ds):
-                    # the decoder side's YIN runs concurrently with the decode calls, on a second
-                    # stream over the decoder's CUs with its grid capped at tuning.yin_beside blocks
-                    # (default 128; 0: after the calls): the latency-bound decoder leaves issue
-                    # slots free (profiles/r04_yin_beside_ab.json)
-                    # (not beside a 256-row call: its resident grid holds two blocks on every
-                    # CU of the partition, the YIN blocks would keep them from co-residing)
-                    yb = self.tuning.yin_beside
-                    beside = yb > 0 and n_dec > 0 and st["n"] * st["R"] <= 128
-                    if beside:
-                        ys = self._yin_s.stream
-                        ys.wait_stream(ds)
-                        with torch.cuda.stream(ys):
-                            try:
-                                pd = prosody_launch(pcm, offsets[0:n_dec + 1], lengths[0:n_dec], CAPTURE_RATE,
-                                                    512, max_blocks=yb)
-                            except Exception:  # engine.py:520-525
-                                pd = None
-                    for c in range(C):
-                        g = groups[c]
-                        if g is None and not any(x is not None for x in st["sets"]):
-                            continue
-                        self._stag_call(st, g, gencs[c], S, c)
-                    if beside:
-                        ds.wait_stream(ys)
-                        box["pres_dec"], box["dec_yin"] = pd, True
-                    elif n_dec > 0:
-                        box["pres_dec"], box["dec_yin"] = yin(0, n_dec), True
-            elif pcm is not None and n_dec > 0:
-                with torch.cuda.stream(ds):
-                    box["pres_dec"], box["dec_yin"] = yin(0, n_dec), True
-
-            box["busy"] = busy
-
-        def voc_side():
-            nonlocal wav, pcm16, kv, pk_dec
-            with torch.cuda.stream(vs):
-                if late and st["queue"]:
-                    # the continuation windows queued by this step's host part, encoded on the
-                    # vocoder's CUs (its side has the slack): they enter the next step's call
-                    todo = list(st["queue"])
-                    st["queue"].clear()
-                    mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in todo])
-                    enc2 = w.encode(mel2)
-                    for i, it in enumerate(todo):
-                        it.enc, it.erow = enc2, i
-                    st["ready"].extend(todo)
-                if res_prev is not None:
-                    pk = res_prev.packets
-                    kv = min(len(pk), max(0, self.tuning.voc_dec_utts))
-                    self.voc_dec_utts = kv   # the main vocoder context renders the other len(pk) - kv
-                    pk_dec = pk[len(pk) - kv:] if kv else []
-                    wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
-                if pcm is not None:
-                    box["pres"] = yin(n_dec, B)
-                ev[1].record(vs)
-
-        if self.tuning.dec_first:
-            dec_side()
-            voc_side()
-        else:
-            voc_side()
-            dec_side()
-        pres, busy, pres_dec, dec_yin = box["pres"], box["busy"], box["pres_dec"], box["dec_yin"]
-        if dec_yin:   # the decoder side's utterances first, as the batch's YIN order
-            pres = (pres_dec, pres)
+        with torch.cuda.stream(vs):
+            if late and st["queue"]:
+                # the continuation windows queued by this step's host part, encoded on the
+                # vocoder's CUs (its side has the slack): they enter the next step's call
+                todo = list(st["queue"])
+                st["queue"].clear()
+                mel2 = gather_windows([(it.batch.feats, it.u, it.seek, it.size) for it in todo])
+                enc2 = w.encode(mel2)
+                for i, it in enumerate(todo):
+                    it.enc, it.erow = enc2, i
+                st["ready"].extend(todo)
+            if res_prev is not None:
+                pk = res_prev.packets
+                kv = min(len(pk), max(0, self.tuning.voc_dec_utts))
+                self.voc_dec_utts = kv   # the main vocoder context renders the other len(pk) - kv
+                pk_dec = pk[len(pk) - kv:] if kv else []
+                wav, pcm16, _ = self.decode(pk[:len(pk) - kv], frames)
+            if pcm is not None:
+                pres = yin(n_dec, B)
+            ev[1].record(vs)
+        busy = any(g is not None for g in groups) or any(x is not None for x in st["sets"])
+        if busy:
+            with torch.cuda.stream(ds):
+                # the decoder side's YIN runs concurrently with the decode calls, on a second
+                # stream over the decoder's CUs with its grid capped at tuning.yin_beside blocks
+                # (default 128; 0: after the calls): the latency-bound decoder leaves issue
+                # slots free (profiles/r04_yin_beside_ab.json)
+                # (not beside a 256-row call: its resident grid holds two blocks on every
+                # CU of the partition, the YIN blocks would keep them from co-residing)
+                yb = self.tuning.yin_beside
+                beside = yb > 0 and n_dec > 0 and st["n"] * st["R"] <= 128
+                if beside:
+                    ys = self._yin_s.stream
+                    ys.wait_stream(ds)
+                    with torch.cuda.stream(ys):
+                        try:
+                            pd = prosody_launch(pcm, offsets[0:n_dec + 1], lengths[0:n_dec], CAPTURE_RATE,
+                                                512, max_blocks=yb)
+                        except Exception:  # engine.py:520-525
+                            pd = None
+                for c in range(C):
+                    g = groups[c]
+                    if g is None and not any(x is not None for x in st["sets"]):
+                        continue
+                    self._stag_call(st, g, gencs[c], S, c)
+                if beside:
+                    ds.wait_stream(ys)
+                    pres = (pd, pres)
+                elif n_dec > 0:
+                    pres = (yin(0, n_dec), pres)
+        elif pcm is not None and n_dec > 0:
+            with torch.cuda.stream(ds):
+                pres = (yin(0, n_dec), pres)
         if pk_dec:
             with torch.cuda.stream(ds):
                 wav_b, pcm_b, _ = self.decode(pk_dec, frames, vocoder=self._vocoder_dec())
