@@ -75,3 +75,61 @@ def test_oracle_noise_matches_scalar_hash():
             u = ((h >> 8) | 1) * 2.0 ** -24
             assert g[t] == -np.log(-np.log(u))
         assert np.isfinite(g).all()
+
+
+class _FakeEngine:
+    """decode_ex stand-in for the sequential fallback: row r's result is a deterministic
+    function of its seed (the real decoder's rows are independent of their neighbours and
+    keyed by fallback_seed(utt, window, ti, h)), so the sequential and speculative walks see
+    the same hypothesis for the same (window, temperature, hypothesis)."""
+
+    class _Out:
+        def __init__(self, rows):
+            self._rows = rows
+
+        def rows(self):
+            return self._rows
+
+    def __init__(self, row_of_seed):
+        self.row_of_seed = row_of_seed
+        self.calls = 0
+
+    def decode_ex(self, enc, prompts=None, max_length=448, temperature=0.0, seeds=None,
+                  enc_index=None, **kw):
+        self.calls += 1
+        return self._Out([self.row_of_seed(int(s)) for s in seeds])
+
+
+def test_speculative_walk_matches_sequential():
+    """_fallback with every temperature's hypotheses decoded up front (presampled, the
+    speculative round) settles every window exactly as the sequential walk: same candidate,
+    same temperature, same number of sampled decodes — for windows passing at T = 0, at an
+    intermediate temperature, and never."""
+    from janus_amd.tokenizer import load_tokenizer
+    tk = load_tokenizer()
+    temps = tr.TEMPERATURES
+
+    def row_of_seed(s):
+        # tokens and avg log-prob from the seed: some hypotheses pass the gates (avg > -1)
+        rng = np.random.default_rng(s)
+        n = int(rng.integers(3, 12))
+        toks = [int(t) for t in rng.integers(0, 5000, n)]
+        avg = float(rng.choice([-0.4, -1.6, -2.5, -0.9]))
+        return (toks, avg, 0.01)
+
+    # T = 0 rows: window 0 passes, windows 1-4 fail
+    first_rows = [([11, 12, 13], -0.3, 0.0)] + [([21, 22], -3.0, 0.0)] * 4
+    keys = [(7, 0), (7, 1), (8, 0), (9, 2), (10, 0)]
+    prompts = [[1, 2, 3]] * len(keys)
+    first = [tr.candidate(tk, t, a, n, 0.0) for t, a, n in first_rows]
+    eng = _FakeEngine(row_of_seed)
+    seq, nseq = tr._fallback(eng, tk, None, prompts, first, keys, 64, temps, tr.BEST_OF)
+    pres = [[[row_of_seed(tr.fallback_seed(k[0], k[1], ti, h)) for h in range(tr.BEST_OF)]
+             for ti in range(1, len(temps))] for k in keys]
+    spec, nspec = tr._fallback(None, tk, None, prompts, first, keys, 64, temps, tr.BEST_OF,
+                               presampled=pres)
+    assert nseq == nspec and nseq[0] == 0
+    for a, b in zip(seq, spec):
+        assert (a.tokens, a.avg_logprob, a.temperature, a.text, a.needs_fallback) == \
+            (b.tokens, b.avg_logprob, b.temperature, b.text, b.needs_fallback)
+    assert any(0 < n < len(temps) - 1 for n in nseq)   # some settle before the last T
