@@ -52,3 +52,37 @@ def run(n, L, batches):
 @pytest.mark.parametrize("batches", [1, 2, 3, 5, 12])
 def test_stagger_plan(n, L, batches):
     assert run(n, L, batches) == list(range(batches))
+
+
+def test_yin_split_start_and_steering():
+    """The staggered step's YIN split (JanusPipeline._yin_split, host logic): 7B/8 on the
+    decoder side to start when the decoder call leaves room beside it (<= 128 rows), 0 when
+    it does not (256-row calls: the decoder side binds); then it follows the previous step's
+    side-time gap over twice the per-utterance YIN time, at most 16 per step, within
+    [0, B - 1]; a fixed tuning.yin_dec_utts wins."""
+    from types import SimpleNamespace
+
+    from janus_amd.pipeline import JanusPipeline, ServingTuning
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def query(self):
+            return True
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    fake = SimpleNamespace(tuning=ServingTuning(), YIN_MS_PER_UTT=JanusPipeline.YIN_MS_PER_UTT)
+    split = JanusPipeline._yin_split
+    assert split(fake, {"n": 2, "R": 64}, 64) == 56
+    assert split(fake, {"n": 2, "R": 128}, 64) == 0
+    # vocoder side 20 ms longer than the decoder side: move 16 (capped) to the decoder side
+    st = {"n": 2, "R": 128, "n_dec": 0, "prev_ev": (Ev(0.0), Ev(300.0), Ev(0.0), Ev(280.0))}
+    assert split(fake, st, 64) == 16 and st["n_dec"] == 16
+    # decoder side longer: back towards 0, never below
+    st["prev_ev"] = (Ev(0.0), Ev(280.0), Ev(0.0), Ev(300.0))
+    assert split(fake, st, 64) == 0
+    fake.tuning = ServingTuning(yin_dec_utts=70)
+    assert split(fake, {"n": 2, "R": 128}, 64) == 63
